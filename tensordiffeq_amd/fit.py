@@ -1,0 +1,281 @@
+"""Training engines (reference tensordiffeq/fit.py: ``fit`` 17-102, ``train_op_inner`` 125-147,
+``fit_dist`` 150-224, ``lbfgs_train`` 107-122).
+
+:class:`AdamEngine` - one optimizer step is: loss + grads (jet kernels / autograd), the DP
+bucket all-reduce, device-side best-model tracking (before the update, so the snapshot is the
+weights that produced the loss - B8), one Keras-Adam update of theta and one Adam *ascent* update
+of the self-adaptive weights (fused HIP kernel on GPU), and a device-side loss-history write.
+Nothing in the step reads back to the host, so on a GPU the whole step is captured once into a
+HIP graph and replayed (reference: a ``tf.function`` step plus a host sync every epoch,
+fit.py:41-55).  Under DP the collective sits between two captured graphs.
+
+:class:`LossGradEngine` - ``(f, grad theta)`` at a given flat parameter vector, the objective
+of both L-BFGS variants; also graph-captured on GPU.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+
+import torch
+
+from .optimizers import adam as adam_mod
+from .ops import fused
+
+
+def _use_graphs(device):
+    return (torch.device(device).type == "cuda" and os.environ.get("TDQ_NO_GRAPH", "0") != "1")
+
+
+class _Bucket:
+    """Pack/unpack of the single per-step all-reduce buffer."""
+
+    def __init__(self, tensors, n_scalars):
+        self.sizes = [t.numel() for t in tensors]
+        self.n_scalars = n_scalars
+
+    def pack(self, grads, scalars):
+        return torch.cat([g.reshape(-1) for g in grads] + [s.reshape(1).to(grads[0].dtype) for s in scalars])
+
+    def unpack(self, buf):
+        out, off = [], 0
+        for n in self.sizes:
+            out.append(buf[off:off + n])
+            off += n
+        scal = [buf[off + i] for i in range(self.n_scalars)]
+        return out, scal
+
+
+class ParamGroup:
+    """Tensors updated by one Adam instance.  ``sign=-1``: gradient ascent (SA weights);
+    ``reduce[i]``: whether tensor i's gradient is all-reduced under DP (False for sharded SA
+    weights, whose gradient is already exact on the owning rank)."""
+
+    def __init__(self, tensors, get_opt, sign=1.0, reduce=None):
+        self.tensors = list(tensors)
+        self.get_opt = get_opt
+        self.sign = float(sign)
+        self.reduce = list(reduce) if reduce is not None else [True] * len(self.tensors)
+
+
+class AdamEngine:
+    def __init__(self, solver, program, groups, n_steps_hint=0, lambdas=None):
+        self.s = solver
+        self.program = program
+        self.groups = [g for g in groups if g.tensors]
+        self.flat = groups[0].tensors[0]
+        self.lambdas = lambdas if lambdas is not None else []
+        self.dist = solver.dist_ctx
+        dev = self.flat.device
+        self.device = dev
+        self.state = solver._train_state(dev)
+        self.term_names = [t.name for t in program.terms]
+        self.graph_a = self.graph_b = None
+        self.static_loss = None
+        self.wrt = [t for g in self.groups for t in g.tensors]
+        self.red_idx = [i for i, r in enumerate(r for g in self.groups for r in g.reduce) if r]
+        self._bind_opts()
+        self._ensure_hist(n_steps_hint)
+
+    def _bind_opts(self):
+        """(Re)read optimizer objects - users may replace e.g. ``model.tf_optimizer``."""
+        self.opts = [g.get_opt() for g in self.groups]
+        self.counters = [o.step_counter(self.device) for o in self.opts]
+        self.moments = [[o.state_for(t) for t in g.tensors] for o, g in zip(self.opts, self.groups)]
+
+    def _ensure_hist(self, n):
+        st = self.state
+        need = int(st["epoch_host"]) + int(n) + 1
+        if st["hist"] is None or st["hist"].shape[0] < need:
+            new = torch.full((max(need, 16), 1 + len(self.term_names)), float("nan"),
+                             device=self.device)
+            if st["hist"] is not None:
+                new[: st["hist"].shape[0]] = st["hist"]
+            st["hist"] = new
+            self.graph_a = self.graph_b = None  # history pointer changed
+
+    # ---------------------------------------------------------------- step pieces -------
+    def _phase_a(self):
+        loss, vals = self.program.evaluate(self.flat, self.lambdas)
+        grads = torch.autograd.grad(loss, self.wrt, allow_unused=True)
+        grads = [torch.zeros_like(w) if g is None else g for g, w in zip(grads, self.wrt)]
+        terms = [vals[n].detach().reshape(()) for n in self.term_names]
+        return loss.detach(), grads, terms
+
+    def _reduce(self, loss, grads, terms):
+        if not self.dist.is_distributed:
+            return loss, grads, terms
+        red_idx = self.red_idx
+        red = [grads[i] for i in red_idx]
+        bucket = _Bucket(red, 1 + len(terms))
+        buf = bucket.pack(red, [loss] + terms)
+        self.dist.all_reduce_(buf)
+        red_out, scal = bucket.unpack(buf)
+        grads = list(grads)
+        for i, g in zip(red_idx, red_out):
+            grads[i] = g.view_as(grads[i])
+        return scal[0], grads, scal[1:]
+
+    def _phase_b(self, loss, grads, terms):
+        st = self.state
+        fused.best_track(loss, st["best_loss"], self.flat, st["best_flat"], st["best_epoch"],
+                         st["epoch"])
+        row = torch.stack([loss.float()] + [t.float() for t in terms])
+        st["hist"].index_copy_(0, st["epoch"].reshape(1), row.unsqueeze(0))
+        off = 0
+        for grp, opt, t, mom in zip(self.groups, self.opts, self.counters, self.moments):
+            n = len(grp.tensors)
+            t.add_(1.0)
+            items = [(p, g, m, v, grp.sign) for p, g, (m, v) in zip(grp.tensors, grads[off:off + n], mom)]
+            fused.adam_multi(items, t, opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon)
+            off += n
+        st["epoch"].add_(1)
+        return loss
+
+    def _eager_step(self):
+        loss, grads, terms = self._phase_a()
+        loss, grads, terms = self._reduce(loss, grads, terms)
+        return self._phase_b(loss, grads, terms)
+
+    # ---------------------------------------------------------------- graphs -------------
+    def _capture(self):
+        stream = torch.cuda.Stream(device=self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        split = self.dist.is_distributed
+        with torch.cuda.stream(stream):
+            # warm-up: one real (counted) step on the side stream
+            warm = self._eager_step()
+            self.state["epoch_host"] += 1
+        torch.cuda.current_stream(self.device).wait_stream(stream)
+        torch.cuda.synchronize(self.device)
+        pool = torch.cuda.graph_pool_handle()
+        if not split:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self.static_loss = self._eager_step()
+            self.graph_a, self.graph_b = g, None
+        else:
+            ga = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga, pool=pool):
+                loss, grads, terms = self._phase_a()
+                red_idx = self.red_idx
+                red = [grads[i] for i in red_idx]
+                self._bucket = _Bucket(red, 1 + len(terms))
+                self._bucket_buf = self._bucket.pack(red, [loss] + terms)
+                self._grads_static = grads
+                self._red_idx = red_idx
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, pool=pool):
+                red_out, scal = self._bucket.unpack(self._bucket_buf)
+                grads = list(self._grads_static)
+                for i, gg in zip(self._red_idx, red_out):
+                    grads[i] = gg.view_as(grads[i])
+                self.static_loss = self._phase_b(scal[0], grads, scal[1:])
+            self.graph_a, self.graph_b = ga, gb
+        return warm
+
+    def _replay(self):
+        self.graph_a.replay()
+        if self.graph_b is not None:
+            self.dist.all_reduce_(self._bucket_buf)
+            self.graph_b.replay()
+        return self.static_loss
+
+    # ---------------------------------------------------------------- driver -------------
+    def run(self, n_steps, progress=None, log_every=100, use_graph=None):
+        """Run ``n_steps`` optimizer steps; returns the last loss (device tensor)."""
+        if n_steps <= 0:
+            return None
+        opts = [g.get_opt() for g in self.groups]
+        sig = [(o.learning_rate, o.beta_1, o.beta_2, o.epsilon) for o in opts]
+        if any(a is not b for a, b in zip(opts, self.opts)) or sig != getattr(self, "_sig", sig):
+            self._bind_opts()
+            self.graph_a = self.graph_b = None
+        self._sig = sig
+        self._ensure_hist(n_steps)
+        use_graph = _use_graphs(self.device) if use_graph is None else use_graph
+        st = self.state
+        loss = None
+        done = 0
+        if use_graph and self.graph_a is None:
+            loss = self._capture()
+            done = 1
+            if progress is not None and n_steps == 1:
+                progress(1, float(loss))
+        while done < n_steps:
+            loss = self._replay() if (use_graph and self.graph_a is not None) else self._eager_step()
+            done += 1
+            st["epoch_host"] += 1
+            if progress is not None and (done % log_every == 0 or done == n_steps):
+                progress(done, float(loss))
+        return loss
+
+
+class LossGradEngine:
+    """``(f, g_theta)`` at a flat parameter vector (lambdas frozen, B15); DP all-reduced."""
+
+    def __init__(self, solver, program, lambdas):
+        self.s = solver
+        self.program = program
+        self.flat = solver.u_model.flat
+        self.lambdas = lambdas
+        self.dist = solver.dist_ctx
+        self.graph = None
+        self.n_evals = 0
+
+    def _body(self):
+        loss, _ = self.program.evaluate(self.flat, self.lambdas)
+        g = torch.autograd.grad(loss, [self.flat])[0]
+        buf = torch.cat([g.reshape(-1), loss.detach().reshape(1)])
+        return buf
+
+    def __call__(self, x):
+        with torch.no_grad():
+            self.flat.copy_(x)
+        use_graph = _use_graphs(self.flat.device)
+        if use_graph and self.graph is None and self.n_evals >= 1:
+            stream = torch.cuda.Stream(device=self.flat.device)
+            stream.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(stream):
+                self._body()
+            torch.cuda.current_stream(self.flat.device).wait_stream(stream)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._static = self._body()
+            self.graph = g
+        if self.graph is not None:
+            self.graph.replay()
+            buf = self._static.clone()
+        else:
+            buf = self._body()
+        self.n_evals += 1
+        if self.dist.is_distributed:
+            self.dist.all_reduce_(buf)
+        return buf[-1], buf[:-1]
+
+
+class Timer:
+    def __init__(self, device):
+        self.device = torch.device(device)
+
+    def sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def __enter__(self):
+        self.sync()
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        self.sync()
+        self.elapsed = time.perf_counter() - self.t0
+        return False
+
+
+def nan_guard(loss):
+    v = float(loss)
+    if math.isnan(v) or math.isinf(v):
+        raise FloatingPointError(f"loss became {v}")
+    return v

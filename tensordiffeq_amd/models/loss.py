@@ -1,0 +1,308 @@
+"""Loss assembly for collocation PINNs (reference ``CollocationSolverND.update_loss``,
+models.py:116-218, and ``DiscoveryModel.loss``, models.py:343-350).
+
+A :class:`LossProgram` is built once at compile time from the domain, BCs and user callables:
+
+* every point set (collocation shard, IC/Dirichlet faces, periodic upper/lower faces, Neumann
+  faces, assimilation data) becomes a *segment* of one device matrix ``X_all``;
+* every user callable (``f_model``, each ``deriv_model``) is run once under a
+  :class:`~tensordiffeq_amd.autodiff.RecordContext` on a few points to learn which derivative
+  streams it needs; the union is one :class:`~tensordiffeq_amd.jet.JetPlan`;
+* at run time ONE jet evaluation of the network over ``X_all`` (HIP kernels on MI355X, torch
+  elsewhere) feeds every term, and the user callables only add elementwise ops.  Callables that
+  cannot be served from a jet run on the generic nested-autograd path instead.
+
+Loss definitions (SURVEY.md §2.5 "Exact numerics to match"):
+  Dirichlet / IC / data   mean((u - val)^2), SA: mean((lam (u - val))^2)   (type 2: lam*mean(...))
+  periodic                sum_k mean((d_k u(upper) - d_k u(lower))^2)  over every output of
+                          every deriv_model (reference enforced only u, B12 - ``periodic_legacy``)
+  Neumann                 sum_k mean((val - d_k u)^2)
+  residual                mean(f^2), SA type 1 mean((lam f)^2), with g: mean(g(lam) f^2),
+                          type 2 lam*mean(f^2); one lambda per residual (B11 fixed).
+Adaptive periodic / Neumann terms, which the reference rejects (B13), take per-point weights.
+
+Data parallel: the collocation segment is this rank's shard; residual means divide by the global
+count and every replicated term is scaled by ``1/world``, so per-rank losses sum to the global one.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import autodiff
+from ..jet import JetPlan, jet_dict
+from ..utils.numerics import MSE, g_MSE
+
+
+class Segment:
+    def __init__(self, name, X):
+        self.name = name
+        self.X = X
+        self.offset = 0
+
+    @property
+    def n(self):
+        return self.X.shape[0]
+
+
+class Term:
+    def __init__(self, name, kind, **kw):
+        self.name = name
+        self.kind = kind
+        self.lam = None          # index into the lambda list or None
+        self.scale = 1.0         # 1/world for replicated terms
+        self.denom = None        # global denominator override for sharded means
+        self.__dict__.update(kw)
+
+
+class LossProgram:
+    def __init__(self, net, d_in, device, dtype=torch.float32, backend="auto", world=1,
+                 weight_outside_sum=False, g=None, periodic_legacy=False):
+        self.net = net
+        self.d_in = d_in
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.requested_backend = backend
+        self.world = world
+        self.weight_outside_sum = weight_outside_sum
+        self.g = g
+        self.periodic_legacy = periodic_legacy
+        self.segments = []
+        self.terms = []
+        self.callables = []   # (fn, segment names, extra_args)
+        self.plan = None
+        self.backend = None
+        self.X_all = None
+        self.reasons = []
+
+    # ---------------------------------------------------------------- building -------
+    def add_segment(self, name, X):
+        X = torch.as_tensor(X, dtype=self.dtype).to(self.device).reshape(-1, self.d_in).contiguous()
+        seg = Segment(name, X)
+        self.segments.append(seg)
+        return len(self.segments) - 1
+
+    def add_term(self, term):
+        self.terms.append(term)
+        return term
+
+    def register_callable(self, fn, seg_idx, extra_args=()):
+        self.callables.append((fn, seg_idx, extra_args))
+
+    def finalize(self):
+        off = 0
+        for s in self.segments:
+            s.offset = off
+            off += s.n
+        self.X_all = torch.cat([s.X for s in self.segments], dim=0).contiguous() if self.segments \
+            else torch.zeros(0, self.d_in, device=self.device)
+        self._plan()
+
+    def _plan(self):
+        from ..models.networks import TanhMLP
+        from ..ops import jet_mlp
+        requests, jetable = set(), True
+        reasons = []
+        if not isinstance(self.net, TanhMLP):
+            jetable = False
+            reasons.append("u_model is not a TanhMLP")
+        for fn, si, extra in self.callables:
+            if not jetable:
+                break
+            X = self.segments[si].X
+            probe = X[: min(8, X.shape[0])].detach().double() if X.shape[0] else X.double()
+            net64 = _Float64View(self.net)
+            req, ok, why, _ = autodiff.record_callable(fn, net64, probe, extra_args=extra)
+            requests |= req
+            if not ok:
+                jetable = False
+                reasons.extend(why)
+        backend = self.requested_backend
+        if backend == "auto":
+            if not jetable:
+                backend = "autograd"
+            else:
+                plan = JetPlan(requests, self.d_in)
+                ok, why = jet_mlp.hip_eligible(self.net, plan, self.device)
+                backend = "hip" if ok else "jet"
+                if not ok:
+                    reasons.append(why)
+        elif backend in ("jet", "hip") and not jetable:
+            raise ValueError("backend %r requested but the callables are not jet-able: %s"
+                             % (backend, "; ".join(reasons)))
+        if backend in ("jet", "hip"):
+            self.plan = JetPlan(requests, self.d_in)
+            if backend == "hip":
+                ok, why = jet_mlp.hip_eligible(self.net, self.plan, self.device)
+                if not ok:
+                    raise RuntimeError("HIP jet backend unavailable: " + why)
+        self.backend = backend
+        self.reasons = reasons
+
+    # ---------------------------------------------------------------- evaluation -----
+    def seg_view(self, J, si):
+        s = self.segments[si]
+        return jet_dict(J[:, s.offset:s.offset + s.n], self.plan)
+
+    def jet(self, params, X=None):
+        from ..ops import jet_mlp
+        X = self.X_all if X is None else X
+        return jet_mlp.jet_eval(X, self.net, params, self.plan, self.backend)
+
+    def call(self, fn, si, extra=(), J=None, X=None):
+        """Evaluate a user callable on segment ``si`` (or explicit points ``X``)."""
+        if self.backend == "autograd":
+            Xs = self.segments[si].X if X is None else X
+            cols = [Xs[:, j:j + 1].detach().clone().requires_grad_(True) for j in range(self.d_in)]
+            return fn(self.net, *extra, *cols)
+        Xs = self.segments[si].X if X is None else X
+        jd = self.seg_view(J, si) if X is None else jet_dict(J, self.plan)
+        cols = [Xs[:, j:j + 1] for j in range(self.d_in)]
+        ctx = autodiff.JetContext(cols, jd)
+        with autodiff.use(ctx):
+            return fn(ctx.proxy(), *extra, *cols)
+
+    def u_on(self, si, J=None, params=None):
+        if self.backend == "autograd":
+            return self.net(self.segments[si].X, params=params)
+        s = self.segments[si]
+        return J[0, s.offset:s.offset + s.n]
+
+    def evaluate(self, params=None, lambdas=None):
+        """Return ``(total, {term_name: value})`` for the current parameters (differentiable)."""
+        params = self.net.flat if params is None else params
+        J = None
+        if self.backend != "autograd":
+            J = self.jet(params)
+            net_params = None
+        else:
+            net_params = params
+        if self.backend == "autograd" and params is not self.net.flat:
+            raise ValueError("autograd backend evaluates the network's own parameters")
+        vals = {}
+        total = None
+        cache = {}
+        for t in self.terms:
+            v = self._term(t, J, lambdas, cache)
+            if t.scale != 1.0:
+                v = v * t.scale
+            vals[t.name] = v
+            total = v if total is None else total + v
+        if total is None:
+            total = torch.zeros((), device=self.device)
+        del net_params
+        return total, vals
+
+    def _lam(self, t, lambdas):
+        return None if (t.lam is None or lambdas is None) else lambdas[t.lam]
+
+    def _term(self, t, J, lambdas, cache):
+        lam = self._lam(t, lambdas)
+        osum = self.weight_outside_sum
+        if t.kind in ("dirichlet", "ic", "data"):
+            u = self.u_on(t.seg, J)
+            val = t.val
+            if lam is not None:
+                return MSE(u, val, lam, osum, denom=t.denom)
+            return MSE(u, val, denom=t.denom)
+        if t.kind == "residual":
+            key = ("res", t.seg)
+            if key not in cache:
+                out = self.call(t.fn, t.seg, t.extra, J)
+                cache[key] = out if isinstance(out, (tuple, list)) else (out,)
+            f = cache[key][t.index]
+            f = f.reshape(-1, 1) if f.dim() != 2 else f
+            if lam is not None:
+                if self.g is not None:
+                    return g_MSE(f, 0.0, self.g(lam), denom=t.denom)
+                return MSE(f, 0.0, lam, osum, denom=t.denom)
+            return MSE(f, 0.0, denom=t.denom)
+        if t.kind == "periodic":
+            loss = None
+            for (si_up, si_lo) in t.pairs:
+                outs_u, outs_l = [], []
+                for fn in t.fns:
+                    ou = self.call(fn, si_up, (), J)
+                    ol = self.call(fn, si_lo, (), J)
+                    outs_u.extend(_as_list(ou))
+                    outs_l.extend(_as_list(ol))
+                    if self.periodic_legacy:
+                        break
+                if self.periodic_legacy:
+                    outs_u, outs_l = outs_u[:1], outs_l[:1]
+                for a, b in zip(outs_u, outs_l):
+                    m = MSE(a, b, lam, osum) if lam is not None else MSE(a, b)
+                    loss = m if loss is None else loss + m
+            return loss
+        if t.kind == "neumann":
+            loss = None
+            for si in t.segs:
+                for fn in t.fns:
+                    for o in _as_list(self.call(fn, si, (), J)):
+                        m = MSE(t.val, o, lam, osum) if lam is not None else MSE(t.val, o)
+                        loss = m if loss is None else loss + m
+            return loss
+        raise ValueError(f"unknown term kind {t.kind}")
+
+    # ---------------------------------------------------------------- prediction -----
+    def residual_on(self, fn, X, params=None, extra=(), chunk=65536):
+        """Evaluate residual(s) of ``fn`` on arbitrary points (no parameter gradients)."""
+        outs = []
+        for lo in range(0, X.shape[0], chunk):
+            Xc = X[lo:lo + chunk]
+            if self.backend == "autograd":
+                cols = [Xc[:, j:j + 1].detach().clone().requires_grad_(True) for j in range(self.d_in)]
+                with torch.enable_grad():
+                    o = fn(_ParamView(self.net, params), *extra, *cols)
+            else:
+                with torch.no_grad():
+                    J = self.jet(params if params is not None else self.net.flat, X=Xc)
+                    cols = [Xc[:, j:j + 1] for j in range(self.d_in)]
+                    ctx = autodiff.JetContext(cols, jet_dict(J, self.plan))
+                    with autodiff.use(ctx):
+                        o = fn(ctx.proxy(), *extra, *cols)
+            o = o if isinstance(o, (tuple, list)) else (o,)
+            outs.append([x.detach().reshape(Xc.shape[0], -1) for x in o])
+        return [torch.cat([c[i] for c in outs], dim=0) for i in range(len(outs[0]))] if outs else []
+
+
+def _as_list(o):
+    return list(o) if isinstance(o, (tuple, list)) else [o]
+
+
+class _Float64View:
+    """Network wrapper evaluating in float64 for the planning pass (exact request recording)."""
+
+    def __init__(self, net):
+        self.net = net
+
+    def __call__(self, *xs, **kw):
+        ws = [(k.double(), b.double()) for k, b in self.net.weights()]
+        x = xs[0] if len(xs) == 1 else torch.cat(xs, dim=1)
+        h = x.double()
+        for i, (k, b) in enumerate(ws):
+            h = torch.addmm(b, h, k)
+            if i < len(ws) - 1:
+                h = torch.tanh(h)
+        return h
+
+
+class _ParamView:
+    def __init__(self, net, params):
+        self.net, self.params = net, params
+
+    def __call__(self, *xs, **kw):
+        return self.net(*xs, params=self.params)
+
+
+def global_count(n_local, ctx):
+    if ctx is None or not ctx.is_distributed:
+        return n_local
+    t = torch.tensor([float(n_local)], dtype=torch.float64, device=ctx.device)
+    ctx.all_reduce_(t)
+    return int(round(t.item()))
+
+
+def is_finite(x):
+    return math.isfinite(float(x))

@@ -1,0 +1,113 @@
+"""Loader for the in-tree native library ``libtdq_hip.so`` (HIP kernels for gfx950).
+
+The kernels are plain HIP C++ compiled by ``hipcc --offload-arch=gfx950`` (see
+``tensordiffeq_amd/csrc/build.py``) and exported through a small C ABI; Python passes device
+pointers and the current HIP stream (``torch.cuda.current_stream().cuda_stream``), so launches
+are captured by torch's HIP-graph capture like any other kernel on that stream.
+
+Policy: on a machine with a GPU, a missing or stale library is an ERROR (never a silent torch
+fallback) unless ``TDQ_ALLOW_TORCH_FALLBACK=1`` is set; on CPU-only machines the torch
+implementations are used.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
+ABI_VERSION = 3
+
+_lock = threading.Lock()
+_lib = None
+_err = None
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def _declare(lib):
+    c = ctypes
+    P, I, F, L = c.c_void_p, c.c_int, c.c_float, c.c_int64
+    sig = {
+        "tdq_abi_version": (I, []),
+        "tdq_jet_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, I, P]),
+        "tdq_jet_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, P, I, P]),
+        "tdq_jet_scratch_floats": (L, [I, I, I, I, I]),
+        "tdq_jet_slab_floats": (L, [I, I, I, I, I]),
+        "tdq_adam_multi": (I, [P, I, P, F, F, F, F, P]),
+        "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
+        "tdq_sq_sum": (I, [P, P, L, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load(required=None):
+    """Return the ctypes library or raise :class:`NativeUnavailable`."""
+    global _lib, _err
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if _err is not None and not required:
+            raise NativeUnavailable(_err)
+        if not os.path.exists(LIB_PATH):
+            _err = f"{LIB_PATH} not built (run `python -m tensordiffeq_amd.csrc.build`)"
+            raise NativeUnavailable(_err)
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+            _declare(lib)
+            ver = lib.tdq_abi_version()
+            if ver != ABI_VERSION:
+                raise NativeUnavailable(f"libtdq_hip.so ABI {ver} != expected {ABI_VERSION}; rebuild")
+        except OSError as e:
+            _err = f"cannot load {LIB_PATH}: {e}"
+            raise NativeUnavailable(_err)
+        _lib = lib
+        return _lib
+
+
+def available():
+    try:
+        load()
+        return True
+    except NativeUnavailable:
+        return False
+
+
+def fallback_allowed():
+    return os.environ.get("TDQ_ALLOW_TORCH_FALLBACK", "0") == "1"
+
+
+def gpu_present():
+    try:
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def require_on_gpu():
+    """Raise when running on a GPU without the native library (unless fallback is allowed)."""
+    if gpu_present() and not fallback_allowed():
+        load(required=True)
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error {rc}")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

@@ -1,0 +1,90 @@
+"""Jet evaluation of a tanh MLP: dispatch between the torch engine and the fused HIP kernels.
+
+``jet_eval(X, net, params, plan, backend)`` returns ``J`` of shape ``(S, N, d_out)`` (stream-major,
+streams in ``plan.streams`` order) and is differentiable w.r.t. ``params`` (the flat buffer).
+
+HIP path (``backend="hip"``, MI355X): two kernels from ``csrc/jet_mlp.hip``
+
+* ``tdq_jet_fwd``  one workgroup = 4 waves x 16 points.  The whole layer stack runs on chip:
+  activations for all derivative streams stay in VGPRs in a *feature-major* MFMA layout
+  (point on the lane, features in registers), so each layer's output accumulator is directly
+  the next layer's B operand - no LDS round trip between layers.  Hidden GEMMs use
+  ``v_mfma_f32_16x16x4_f32`` (exact fp32) with the layer's weights staged in LDS; the tanh-jet
+  epilogue (Faa di Bruno, order <= 2) is fused.  Pre-activations of every hidden layer are
+  written in register-image order (256-B coalesced) for the backward.
+* ``tdq_jet_bwd``  reverse pass through the same stack: recomputes tanh / its derivatives from the
+  saved pre-activations, chains the stream adjoints through ``W^T`` on MFMA, and accumulates
+  ``dW = sum_points sum_streams zbar h^T`` per workgroup through an LDS transpose into MFMA,
+  writing one partial slab per workgroup; a deterministic reduction kernel folds the slabs into
+  the flat gradient (Keras order).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..jet import jet_forward
+from . import _lib
+
+MAX_S = 8
+PTS_PER_WG = 64
+
+
+def _pad16(w):
+    return (w + 15) // 16 * 16
+
+
+def hip_config(net, plan):
+    """Return the kernel geometry or raise ValueError if the kernels cannot serve it."""
+    sizes = net.layer_sizes
+    d_in, d_out = sizes[0], sizes[-1]
+    hidden = sizes[1:-1]
+    if len(hidden) < 1:
+        raise ValueError("needs at least one hidden layer")
+    if len(set(hidden)) != 1:
+        raise ValueError("hidden widths must be equal")
+    if plan.order > 2:
+        raise ValueError("derivative order > 2")
+    S = plan.S
+    if S > MAX_S:
+        raise ValueError(f"{S} streams > {MAX_S}")
+    wpad = _pad16(hidden[0])
+    WT = wpad // 16
+    if WT not in (1, 2, 4, 8):
+        if WT == 3:
+            WT = 4
+        elif WT in (5, 6, 7):
+            WT = 8
+        else:
+            raise ValueError("hidden width > 128")
+    if S * WT > 32:
+        raise ValueError(f"streams x width tiles = {S * WT} > 32 (register budget)")
+    if d_in > 8 or d_out > 4:
+        raise ValueError("input width > 8 or output width > 4")
+    return {"d_in": d_in, "d_out": d_out, "width": hidden[0], "WT": WT, "S": S,
+            "n_hidden": len(hidden)}
+
+
+def hip_eligible(net, plan, device):
+    from ..models.networks import TanhMLP
+    if torch.device(device).type != "cuda":
+        return False, "device is not a GPU"
+    if not isinstance(net, TanhMLP):
+        return False, "network is not a TanhMLP"
+    try:
+        hip_config(net, plan)
+    except ValueError as e:
+        return False, str(e)
+    if not _lib.available():
+        if _lib.fallback_allowed():
+            return False, "native library unavailable (fallback allowed)"
+        _lib.load(required=True)
+    return True, ""
+
+
+def jet_eval(X, net, params, plan, backend):
+    if backend == "jet":
+        return jet_forward(X, net.weights(params), plan)
+    if backend == "hip":
+        from . import jet_hip
+        return jet_hip.JetMLPFunction.apply(X, params, net, plan)
+    raise ValueError(f"jet_eval backend {backend!r}")

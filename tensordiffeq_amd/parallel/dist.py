@@ -1,0 +1,140 @@
+"""Data parallelism over collocation-point shards: one process per GPU, RCCL over xGMI.
+
+Reference: ``tf.distribute.MirroredStrategy`` in one process (models.py:230-277, fit.py:150-224),
+gradients all-reduced with NcclAllReduce inside ``apply_gradients`` (fit.py:180) - but each
+replica recomputed the *full* loss (B3), so there was no speed-up.
+
+Design here:
+* ``torch.distributed`` with backend ``"nccl"`` (= RCCL on ROCm) on GPUs, ``"gloo"`` on CPU;
+  rendezvous from the usual ``RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR`` env variables.
+* Collocation points **and their self-adaptive weights** are block-sharded by rank; residual
+  means use the *global* point count as denominator, boundary terms are computed on every rank
+  and scaled by ``1/world`` - so the SUM over ranks of per-rank losses/grads is exactly the
+  single-device full-batch loss/grad.
+* One contiguous fp32 bucket per step ``[grad theta | grad(BC lambdas) | loss terms]`` is
+  all-reduced (SUM).  For the 50k-parameter Allen-Cahn net that is ~196 KiB: a latency-bound
+  message, so a single collective per step is the right shape for xGMI's point-to-point links.
+* Parameters are broadcast from rank 0 at start, so every rank starts from identical weights.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class DistContext:
+    def __init__(self, rank=0, world=1, local_rank=0, device=None, backend=None, initialized=False):
+        self.rank = rank
+        self.world = world
+        self.local_rank = local_rank
+        self.device = device if device is not None else torch.device("cpu")
+        self.backend = backend
+        self.initialized = initialized
+
+    @property
+    def is_distributed(self):
+        return self.world > 1 and self.initialized
+
+    def barrier(self):
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_reduce_(self, buf):
+        if self.is_distributed:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        return buf
+
+    def broadcast_(self, buf, src=0):
+        if self.is_distributed:
+            dist.broadcast(buf, src=src)
+        return buf
+
+    def max_scalar(self, v):
+        if not self.is_distributed:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def __repr__(self):
+        return (f"DistContext(rank={self.rank}, world={self.world}, device={self.device}, "
+                f"backend={self.backend})")
+
+
+_CTX = None
+
+
+def env_world():
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init_distributed(backend=None, device=None, timeout_s=600):
+    """Initialise (once) from the torchrun environment; returns the process' DistContext."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    world = env_world()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device is None:
+        if torch.cuda.is_available():
+            device = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+        else:
+            device = torch.device("cpu")
+    device = torch.device(device)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    if backend is None:
+        backend = "nccl" if device.type == "cuda" else "gloo"
+    initialized = False
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if not dist.is_initialized():
+            kw = {}
+            if backend == "nccl":
+                kw["device_id"] = device
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        initialized = True
+    _CTX = DistContext(rank, world, local_rank, device, backend, initialized)
+    return _CTX
+
+
+def get_context(device=None):
+    """Current context; a trivial single-process one when never initialised."""
+    if _CTX is not None:
+        return _CTX
+    if device is None:
+        device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+    return DistContext(0, 1, 0, torch.device(device), None, False)
+
+
+def reset_context():
+    global _CTX
+    _CTX = None
+
+
+def shard_range(n, rank, world):
+    """Balanced contiguous block ``[lo, hi)`` of ``n`` items for ``rank``."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def shard(t, rank, world):
+    lo, hi = shard_range(t.shape[0], rank, world)
+    return t[lo:hi]
+
+
+def destroy():
+    global _CTX
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None
