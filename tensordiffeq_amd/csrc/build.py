@@ -1,0 +1,81 @@
+"""Build ``libtdq_hip.so`` (all HIP kernels, gfx950 only) in-tree with hipcc.
+
+    python -m tensordiffeq_amd.csrc.build [--force] [-j N]
+
+Each ``*.hip`` is compiled to an object in ``csrc/build/`` (skipped when up to date w.r.t. the
+source and ``common.h``), then linked into ``csrc/libtdq_hip.so``.  No torch headers are
+involved: the kernels export a C ABI that :mod:`tensordiffeq_amd.ops._lib` loads with ctypes.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "libtdq_hip.so")
+BUILD = os.path.join(HERE, "build")
+ARCH = os.environ.get("TDQ_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _flags():
+    return ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+            "-Wno-unused-result", "-I", HERE]
+
+
+def _compile(src, force):
+    obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
+    deps = [src, os.path.join(HERE, "common.h")]
+    if not force and os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
+        return obj, False
+    cmd = [hipcc()] + _flags() + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    return obj, True
+
+
+def build(force=False, jobs=None, verbose=True):
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(HERE, "*.hip")))
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2)))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        results = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs = [o for o, _ in results]
+    rebuilt = any(r for _, r in results)
+    if rebuilt or force or not os.path.exists(OUT) or any(
+            os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
+        tmp = OUT + ".tmp"
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, OUT)
+        if verbose:
+            print(f"built {OUT}")
+    elif verbose:
+        print(f"{OUT} up to date")
+    return OUT
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,140 @@
+// Fused optimizer-side kernels for gfx950.
+//
+// tdq_adam_multi: one launch updates up to 16 tensors with the Keras/TF ResourceApplyAdam
+//   formula (reference models.py:49-50 -> TF 2.4 Adam):
+//     m <- b1 m + (1-b1) g ; v <- b2 v + (1-b2) g^2 ;
+//     p <- p - lr sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps)
+//   with g multiplied by the group's sign (-1 = gradient ascent for self-adaptive weights,
+//   reference fit.py:136-141).  The step counter t is read from device memory, so the launch
+//   is replayable inside a captured HIP graph.  float4 vector path + scalar tail per group.
+// tdq_best_track: snapshot the flat parameters when the step's loss improves (two tiny
+//   kernels: copy-if-improved, then the scalar update, so no block races on best_loss).
+#include "common.h"
+
+#define TDQ_MAX_GROUPS 16
+
+struct AdamGroup {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+  float sign;
+  float pad;
+};
+
+struct AdamArgs {
+  AdamGroup grp[TDQ_MAX_GROUPS];
+  int64_t start[TDQ_MAX_GROUPS + 1];  // prefix sums of float4 "slots" per group
+  int ngroups;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2,
+                                          float eps, float lr_t) {
+  m = fmaf(1.f - b1, g, b1 * m);
+  v = fmaf(1.f - b2, g * g, b2 * v);
+  p = p - lr_t * m / (sqrtf(v) + eps);
+}
+
+__global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const double* __restrict__ tptr,
+                                                          float lr, float b1, float b2, float eps) {
+  const double t = *tptr;
+  const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
+  const int64_t total = args.start[args.ngroups];
+  for (int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x; slot < total;
+       slot += (int64_t)gridDim.x * 256) {
+    int gi = 0;
+#pragma unroll
+    for (int q = 1; q < TDQ_MAX_GROUPS; ++q)
+      if (q < args.ngroups && slot >= args.start[q]) gi = q;
+    const AdamGroup gr = args.grp[gi];
+    const int64_t e0 = (slot - args.start[gi]) * 4;
+    const float sg = gr.sign;
+    const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
+    if (aligned && e0 + 4 <= gr.n) {
+      f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gr.g + e0);
+      f32x4 m = *reinterpret_cast<const f32x4*>(gr.m + e0);
+      f32x4 v = *reinterpret_cast<const f32x4*>(gr.v + e0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float pc = p[c], mc = m[c], vc = v[c];
+        adam_elem(pc, sg * g[c], mc, vc, b1, b2, eps, lr_t);
+        p[c] = pc; m[c] = mc; v[c] = vc;
+      }
+      *reinterpret_cast<f32x4*>(gr.p + e0) = p;
+      *reinterpret_cast<f32x4*>(gr.m + e0) = m;
+      *reinterpret_cast<f32x4*>(gr.v + e0) = v;
+    } else {
+      for (int c = 0; c < 4; ++c) {
+        const int64_t e = e0 + c;
+        if (e < gr.n) adam_elem(gr.p[e], sg * gr.g[e], gr.m[e], gr.v[e], b1, b2, eps, lr_t);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) best_copy_kernel(const float* __restrict__ loss,
+                                                         const float* __restrict__ best_loss,
+                                                         const float* __restrict__ flat,
+                                                         float* __restrict__ best_flat, int64_t n) {
+  const float lv = *loss;
+  if (!(lv < *best_loss)) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    best_flat[i] = flat[i];
+}
+
+__global__ void best_scalar_kernel(const float* __restrict__ loss, float* __restrict__ best_loss,
+                                   int64_t* __restrict__ best_epoch, const int64_t* __restrict__ epoch) {
+  const float lv = *loss;
+  if (lv < *best_loss) {
+    *best_loss = lv;
+    *best_epoch = *epoch;
+  }
+}
+
+extern "C" {
+
+int tdq_abi_version() { return 3; }
+
+int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, float b1, float b2,
+                   float eps, void* stream) {
+  if (ngroups <= 0 || ngroups > TDQ_MAX_GROUPS) return (int)hipErrorInvalidValue;
+  AdamArgs args;
+  const AdamGroup* src = reinterpret_cast<const AdamGroup*>(groups);
+  args.ngroups = ngroups;
+  args.start[0] = 0;
+  for (int i = 0; i < TDQ_MAX_GROUPS; ++i) {
+    if (i < ngroups) {
+      args.grp[i] = src[i];
+      args.start[i + 1] = args.start[i] + (src[i].n + 3) / 4;
+    } else {
+      args.grp[i] = AdamGroup{nullptr, nullptr, nullptr, nullptr, 0, 1.f, 0.f};
+      if (i + 1 <= TDQ_MAX_GROUPS) args.start[i + 1] = args.start[i];
+    }
+  }
+  const int64_t total = args.start[ngroups];
+  if (total == 0) return 0;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), args, t, lr, b1, b2, eps);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+int tdq_best_track(const float* loss, float* best_loss, const float* flat, float* best_flat,
+                   int64_t* best_epoch, const int64_t* epoch, int64_t n, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(best_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, st, loss, best_loss, flat,
+                     best_flat, n);
+  TDQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(best_scalar_kernel, dim3(1), dim3(1), 0, st, loss, best_loss, best_epoch, epoch);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

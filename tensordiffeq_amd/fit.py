@@ -59,8 +59,21 @@ class ParamGroup:
         self.reduce = list(reduce) if reduce is not None else [True] * len(self.tensors)
 
 
+def default_bind(n_lambdas):
+    """Map the per-step parameter aliases to ``LossProgram.evaluate`` arguments."""
+    def bind(alias):
+        return {"params": alias[0], "lambdas": alias[1:1 + n_lambdas]}
+    return bind
+
+
 class AdamEngine:
-    def __init__(self, solver, program, groups, n_steps_hint=0, lambdas=None):
+    """Captured/eager optimizer step.  Gradients are taken w.r.t. fresh
+    ``detach().requires_grad_()`` aliases of the parameter buffers (same storage), never the
+    persistent leaves: an AccumulateGrad node of a leaf created on the default stream by an
+    earlier eager backward would otherwise make autograd sync the legacy null stream inside
+    the HIP-graph capture."""
+
+    def __init__(self, solver, program, groups, n_steps_hint=0, lambdas=None, bind=None):
         self.s = solver
         self.program = program
         self.groups = [g for g in groups if g.tensors]
@@ -74,6 +87,7 @@ class AdamEngine:
         self.graph_a = self.graph_b = None
         self.static_loss = None
         self.wrt = [t for g in self.groups for t in g.tensors]
+        self.bind = bind if bind is not None else default_bind(len(self.lambdas))
         self.red_idx = [i for i, r in enumerate(r for g in self.groups for r in g.reduce) if r]
         self._bind_opts()
         self._ensure_hist(n_steps_hint)
@@ -97,9 +111,10 @@ class AdamEngine:
 
     # ---------------------------------------------------------------- step pieces -------
     def _phase_a(self):
-        loss, vals = self.program.evaluate(self.flat, self.lambdas)
-        grads = torch.autograd.grad(loss, self.wrt, allow_unused=True)
-        grads = [torch.zeros_like(w) if g is None else g for g, w in zip(grads, self.wrt)]
+        alias = [t.detach().requires_grad_(True) for t in self.wrt]
+        loss, vals = self.program.evaluate(**self.bind(alias))
+        grads = torch.autograd.grad(loss, alias, allow_unused=True)
+        grads = [torch.zeros_like(w) if g is None else g for g, w in zip(grads, alias)]
         terms = [vals[n].detach().reshape(()) for n in self.term_names]
         return loss.detach(), grads, terms
 
@@ -225,8 +240,10 @@ class LossGradEngine:
         self.n_evals = 0
 
     def _body(self):
-        loss, _ = self.program.evaluate(self.flat, self.lambdas)
-        g = torch.autograd.grad(loss, [self.flat])[0]
+        p = self.flat.detach().requires_grad_(True)
+        lams = [l.detach() for l in self.lambdas]
+        loss, _ = self.program.evaluate(p, lams)
+        g = torch.autograd.grad(loss, [p])[0]
         buf = torch.cat([g.reshape(-1), loss.detach().reshape(1)])
         return buf
 

@@ -154,7 +154,7 @@ class CollocationSolverND:
                 if sharded:
                     t = t.reshape(-1, 1)[self._lo:self._hi]
                 t = t.reshape(-1, 1).contiguous() if t.numel() > 1 else t.reshape(()).contiguous()
-                lambdas.append(t)
+                lambdas.append(t.detach().requires_grad_(True))
                 kinds.append("residual" if key == "residual" else "bc")
                 idx.append(len(lambdas) - 1)
                 lam_for[(kinds[-1], j)] = len(lambdas) - 1
@@ -298,7 +298,7 @@ class CollocationSolverND:
     # ================================================================== loss API =========
     def update_loss(self):
         total, vals = self.program().evaluate(self._flat(), self.lambdas)
-        self.loss_terms = {k: v for k, v in vals.items()}
+        self.loss_terms = {k: v.detach() for k, v in vals.items()}
         return total
 
     def grad(self):

@@ -78,7 +78,7 @@ class DiscoveryModel:
             if ctx.is_distributed:
                 cw = cw.to(self.device)
                 ctx.broadcast_(cw)
-            self.col_weights = cw[self._lo:self._hi].to(self.device).contiguous()
+            self.col_weights = cw[self._lo:self._hi].to(self.device).contiguous().detach().requires_grad_(True)
         else:
             self.col_weights = None
         self.backend = backend
@@ -139,7 +139,12 @@ class DiscoveryModel:
             groups = [ParamGroup([self.u_model.flat], lambda: self.tf_optimizer, 1.0),
                       ParamGroup(self._lambdas(), lambda: self.tf_optimizer_weights, -1.0, [rep]),
                       ParamGroup(self.vars, lambda: self.tf_optimizer_vars, 1.0)]
-            self._engine = AdamEngine(self, prog, groups, n_steps_hint=n_hint, lambdas=self._lambdas())
+            ncw = len(self._lambdas())
+
+            def bind(alias):
+                return {"params": alias[0], "lambdas": alias[1:1 + ncw], "extras": (alias[1 + ncw:],)}
+            self._engine = AdamEngine(self, prog, groups, n_steps_hint=n_hint, lambdas=self._lambdas(),
+                                      bind=bind)
         return self._engine
 
     def train_op(self):

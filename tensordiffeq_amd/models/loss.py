@@ -155,7 +155,7 @@ class LossProgram:
         if self.backend == "autograd":
             Xs = self.segments[si].X if X is None else X
             cols = [Xs[:, j:j + 1].detach().clone().requires_grad_(True) for j in range(self.d_in)]
-            return fn(self.net, *extra, *cols)
+            return fn(getattr(self, "_cur_net", self.net), *extra, *cols)
         Xs = self.segments[si].X if X is None else X
         jd = self.seg_view(J, si) if X is None else jet_dict(J, self.plan)
         cols = [Xs[:, j:j + 1] for j in range(self.d_in)]
@@ -165,24 +165,28 @@ class LossProgram:
 
     def u_on(self, si, J=None, params=None):
         if self.backend == "autograd":
-            return self.net(self.segments[si].X, params=params)
+            return getattr(self, "_cur_net", self.net)(self.segments[si].X)
         s = self.segments[si]
         return J[0, s.offset:s.offset + s.n]
 
-    def evaluate(self, params=None, lambdas=None):
-        """Return ``(total, {term_name: value})`` for the current parameters (differentiable)."""
+    def evaluate(self, params=None, lambdas=None, extras=None):
+        """Return ``(total, {term_name: value})`` (differentiable w.r.t. ``params``, ``lambdas``
+        and ``extras``).  ``extras`` replaces the extra callable arguments of residual terms
+        (the DiscoveryModel's coefficients)."""
+        from .networks import TanhMLP
         params = self.net.flat if params is None else params
         J = None
+        self._cur_net = self.net
         if self.backend != "autograd":
             J = self.jet(params)
-            net_params = None
-        else:
-            net_params = params
-        if self.backend == "autograd" and params is not self.net.flat:
-            raise ValueError("autograd backend evaluates the network's own parameters")
+        elif params is not getattr(self.net, "flat", None):
+            if not isinstance(self.net, TanhMLP):
+                raise ValueError("custom networks are evaluated at their own parameters")
+            self._cur_net = _ParamView(self.net, params)
         vals = {}
         total = None
         cache = {}
+        self._extras = extras
         for t in self.terms:
             v = self._term(t, J, lambdas, cache)
             if t.scale != 1.0:
@@ -191,7 +195,8 @@ class LossProgram:
             total = v if total is None else total + v
         if total is None:
             total = torch.zeros((), device=self.device)
-        del net_params
+        self._cur_net = self.net
+        self._extras = None
         return total, vals
 
     def _lam(self, t, lambdas):
@@ -209,7 +214,8 @@ class LossProgram:
         if t.kind == "residual":
             key = ("res", t.seg)
             if key not in cache:
-                out = self.call(t.fn, t.seg, t.extra, J)
+                extra = self._extras if getattr(self, "_extras", None) is not None else t.extra
+                out = self.call(t.fn, t.seg, extra, J)
                 cache[key] = out if isinstance(out, (tuple, list)) else (out,)
             f = cache[key][t.index]
             f = f.reshape(-1, 1) if f.dim() != 2 else f
@@ -289,10 +295,14 @@ class _Float64View:
 
 
 class _ParamView:
+    """A TanhMLP evaluated at an explicit flat parameter tensor."""
+
     def __init__(self, net, params):
         self.net, self.params = net, params
 
     def __call__(self, *xs, **kw):
+        if self.params is None:
+            return self.net(*xs)
         return self.net(*xs, params=self.params)
 
 

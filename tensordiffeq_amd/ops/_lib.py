@@ -35,13 +35,12 @@ def _declare(lib):
     P, I, F, L = c.c_void_p, c.c_int, c.c_float, c.c_int64
     sig = {
         "tdq_abi_version": (I, []),
-        "tdq_jet_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, I, P]),
-        "tdq_jet_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, P, I, P]),
+        "tdq_jet_fwd": (I, [P, P, P, P, I, I, I, I, I, I, P, P]),
+        "tdq_jet_bwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P]),
         "tdq_jet_scratch_floats": (L, [I, I, I, I, I]),
         "tdq_jet_slab_floats": (L, [I, I, I, I, I]),
         "tdq_adam_multi": (I, [P, I, P, F, F, F, F, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
-        "tdq_sq_sum": (I, [P, P, L, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

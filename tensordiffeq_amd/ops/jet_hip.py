@@ -1,0 +1,71 @@
+"""torch.autograd binding of the HIP jet kernels (``csrc/jet_mlp.hip``).
+
+Forward: ``tdq_jet_fwd`` -> J (S, N, d_out) + scratch (saved pre-activation streams).
+Backward: ``tdq_jet_bwd`` -> flat parameter gradient (per-workgroup slabs, deterministic
+two-pass reduction).  Buffers are allocated with torch so they come from the caching
+allocator (and from the private pool while a HIP graph is being captured).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .jet_mlp import hip_config
+
+
+def stream_spec(plan):
+    """3 ints per stream: (type, a, b) - see ``make_spec`` in jet_mlp.hip."""
+    idx = plan.index
+    out = []
+    for mi in plan.streams:
+        if len(mi) == 0:
+            out += [0, 0, 0]
+        elif len(mi) == 1:
+            out += [1, mi[0], 0]
+        else:
+            out += [2, idx[(mi[0],)], idx[(mi[1],)]]
+    return out
+
+
+class JetMLPFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, params, net, plan):
+        lib = _lib.load()
+        cfg = hip_config(net, plan)
+        X = X.contiguous()
+        P = params.contiguous()
+        N = X.shape[0]
+        S = plan.S
+        spec = stream_spec(plan)
+        spec_c = (ctypes.c_int * len(spec))(*spec)
+        J = torch.empty((S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
+        nscr = lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], S, 0)
+        scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
+        rc = lib.tdq_jet_fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
+                             cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c,
+                             _lib.stream_ptr(X.device))
+        _lib.check(rc, "tdq_jet_fwd")
+        ctx.save_for_backward(X, P, scratch)
+        ctx.cfg = cfg
+        ctx.spec = spec
+        ctx.S = S
+        return J
+
+    @staticmethod
+    def backward(ctx, dJ):
+        lib = _lib.load()
+        X, P, scratch = ctx.saved_tensors
+        cfg = ctx.cfg
+        N = X.shape[0]
+        dJ = dJ.contiguous() if dJ is not None else torch.zeros((ctx.S, N, cfg["d_out"]), device=X.device)
+        nwork = lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"])
+        work = torch.empty(max(int(nwork), 1), dtype=torch.float32, device=X.device)
+        grad = torch.empty_like(P)
+        spec_c = (ctypes.c_int * len(ctx.spec))(*ctx.spec)
+        rc = lib.tdq_jet_bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
+                             _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"],
+                             ctx.S, spec_c, _lib.stream_ptr(X.device))
+        _lib.check(rc, "tdq_jet_bwd")
+        return None, grad, None, None

@@ -1,0 +1,191 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (run on MI355X: ``pytest -m gpu``).
+
+Jet forward: every derivative stream against the torch jet engine (itself checked against nested
+autograd in test_jet.py) AND directly against nested ``torch.autograd.grad``.
+Jet backward: the flat parameter gradient of a random linear functional of J against autograd
+through the torch jet.  Shapes cover non-multiple-of-64 point counts, every width-tile class
+(WT = 1, 2, 4, 8 incl. padded widths), 1-8 streams, d_in 1-3, d_out 1-2, 1-4 hidden layers.
+"""
+import pytest
+import torch
+
+from tensordiffeq_amd.jet import JetPlan, jet_forward
+from tensordiffeq_amd.models.networks import TanhMLP
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # layer_sizes, requests, N
+    ([2, 128, 128, 128, 128, 1], [(0,), (1,), (0, 0)], 1000),      # Allen-Cahn / Burgers plan
+    ([2, 20, 20, 20, 20, 20, 20, 20, 20, 1], [(0,), (1,), (0, 0)], 777),  # Burgers net (WT=2)
+    ([2, 50, 50, 50, 50, 1], [(0, 0), (1, 1)], 333),               # Helmholtz plan, S=5 (WT=4)
+    ([3, 64, 64, 1], [(0, 0), (1, 1), (2,)], 130),                 # 3-D heat, S=6
+    ([2, 16, 16, 1], [(0, 0), (0, 1), (1, 1)], 65),                # mixed derivative, S=6 (WT=1)
+    ([1, 32, 2], [(0,), (0, 0)], 100),                             # 1-D, 2 outputs
+    ([2, 128, 1], [], 70),                                          # value only, 1 hidden layer
+    ([2, 128, 128, 128, 1], [(0,), (1,)], 64),                     # first order only
+    ([3, 40, 40, 40, 1], [(0, 0), (1, 1), (2, 2), (0, 1)], 257),    # S=8, WT=4... (S*WT=32)
+]
+
+
+def _setup(sizes, reqs, N, seed=0):
+    torch.manual_seed(seed)
+    net = TanhMLP(sizes, device="cuda")
+    with torch.no_grad():
+        net.flat.add_(0.05 * torch.randn_like(net.flat))  # non-zero biases
+    X = (torch.rand(N, sizes[0], device="cuda") * 2 - 1).contiguous()
+    plan = JetPlan(reqs, sizes[0])
+    return net, X, plan
+
+
+@pytest.mark.parametrize("sizes,reqs,N", CASES)
+def test_jet_forward_matches_torch(sizes, reqs, N):
+    from tensordiffeq_amd.ops import jet_hip, jet_mlp
+    net, X, plan = _setup(sizes, reqs, N)
+    try:
+        jet_mlp.hip_config(net, plan)
+    except ValueError:
+        pytest.skip("configuration outside the kernel envelope")
+    with torch.no_grad():
+        J = jet_hip.JetMLPFunction.apply(X, net.flat, net, plan)
+        Jref = jet_forward(X.double(), [(k.double(), b.double()) for k, b in net.weights()], plan)
+    assert J.shape == Jref.shape
+    scale = Jref.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
+    err = ((J.double() - Jref).abs() / scale).max().item()
+    assert err < 2e-5, err
+
+
+def test_jet_forward_matches_autograd():
+    from tensordiffeq_amd.ops import jet_hip
+    net, X, plan = _setup([2, 128, 128, 128, 128, 1], [(0,), (1,), (0, 0)], 300)
+    with torch.no_grad():
+        J = jet_hip.JetMLPFunction.apply(X, net.flat, net, plan)
+    cols = [X[:, j:j + 1].double().clone().requires_grad_(True) for j in range(2)]
+    ws = [(k.double(), b.double()) for k, b in net.weights()]
+    h = torch.cat(cols, 1)
+    for i, (k, b) in enumerate(ws):
+        h = torch.addmm(b, h, k)
+        if i < len(ws) - 1:
+            h = torch.tanh(h)
+    u = h
+    ux = torch.autograd.grad(u.sum(), cols[0], create_graph=True)[0]
+    ut = torch.autograd.grad(u.sum(), cols[1], create_graph=True)[0]
+    uxx = torch.autograd.grad(ux.sum(), cols[0])[0]
+    for i, ref in enumerate([u, ux, ut, uxx]):
+        err = (J[i].double() - ref.detach()).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-5, (i, err)
+
+
+@pytest.mark.parametrize("sizes,reqs,N", CASES)
+def test_jet_backward_matches_autograd(sizes, reqs, N):
+    from tensordiffeq_amd.ops import jet_hip, jet_mlp
+    net, X, plan = _setup(sizes, reqs, N, seed=1)
+    try:
+        jet_mlp.hip_config(net, plan)
+    except ValueError:
+        pytest.skip("configuration outside the kernel envelope")
+    G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
+    p = net.flat.detach().clone().requires_grad_(True)
+    J = jet_hip.JetMLPFunction.apply(X, p, net, plan)
+    (J.double() * G).sum().backward()
+    g_hip = p.grad.double()
+    p64 = net.flat.detach().double().clone().requires_grad_(True)
+    Jr = jet_forward(X.double(), net.weights(p64), plan)
+    (Jr * G).sum().backward()
+    g_ref = p64.grad
+    rel = ((g_hip - g_ref).norm() / g_ref.norm()).item()
+    assert rel < 5e-5, rel
+
+
+def test_jet_deterministic():
+    from tensordiffeq_amd.ops import jet_hip
+    net, X, plan = _setup([2, 128, 128, 128, 128, 1], [(0,), (1,), (0, 0)], 5000)
+    G = torch.randn(plan.S, 5000, 1, device="cuda")
+    outs = []
+    for _ in range(2):
+        p = net.flat.detach().clone().requires_grad_(True)
+        J = jet_hip.JetMLPFunction.apply(X, p, net, plan)
+        (J * G).sum().backward()
+        outs.append(p.grad.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_adam_multi_matches_reference():
+    from tensordiffeq_amd.ops import fused
+    from tensordiffeq_amd.optimizers.adam import torch_update
+    torch.manual_seed(0)
+    shapes = [(50049,), (1000, 1), (7,)]
+    ps = [torch.randn(s, device="cuda") for s in shapes]
+    gs = [torch.randn(s, device="cuda") for s in shapes]
+    ms = [torch.zeros(s, device="cuda") for s in shapes]
+    vs = [torch.zeros(s, device="cuda") for s in shapes]
+    ref = [(p.clone(), m.clone(), v.clone()) for p, m, v in zip(ps, ms, vs)]
+    t = torch.zeros((), dtype=torch.float64, device="cuda")
+    for step in range(3):
+        t.add_(1)
+        fused.adam_multi([(p, g, m, v, -1.0 if i == 1 else 1.0) for i, (p, g, m, v) in enumerate(zip(ps, gs, ms, vs))],
+                         t, 0.005, 0.99, 0.999, 1e-7)
+        for i, ((p, m, v), g) in enumerate(zip(ref, gs)):
+            torch_update(p, g, m, v, t, 0.005, 0.99, 0.999, 1e-7, -1.0 if i == 1 else 1.0)
+    for p, (pr, _, _) in zip(ps, ref):
+        assert torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
+
+
+def test_best_track():
+    from tensordiffeq_amd.ops import fused
+    flat = torch.randn(1000, device="cuda")
+    best = torch.zeros(1000, device="cuda")
+    bl = torch.full((), float("inf"), device="cuda")
+    be = torch.full((), -1, dtype=torch.int64, device="cuda")
+    ep = torch.tensor(3, dtype=torch.int64, device="cuda")
+    fused.best_track(torch.tensor(1.5, device="cuda"), bl, flat, best, be, ep)
+    assert torch.equal(best, flat) and bl.item() == 1.5 and be.item() == 3
+    flat2 = torch.randn(1000, device="cuda")
+    fused.best_track(torch.tensor(2.5, device="cuda"), bl, flat2, best, be, ep + 1)
+    assert torch.equal(best, flat) and bl.item() == 1.5 and be.item() == 3
+
+
+def test_solver_hip_matches_jet_backend():
+    import math
+    import numpy as np
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.boundaries import DomainND, IC, periodicBC
+
+    def build(backend):
+        tdq.set_seed(0)
+        D = DomainND(["x", "t"], time_var="t")
+        D.add("x", [-1.0, 1.0], 512)
+        D.add("t", [0.0, 1.0], 201)
+        D.generate_collocation_points(3000)
+
+        def deriv_model(u_model, x, t):
+            u = u_model(torch.cat([x, t], 1))
+            return u, tdq.grad(u, x)
+
+        def f_model(u_model, x, t):
+            u = u_model(torch.cat([x, t], 1))
+            u_xx = tdq.grad(tdq.grad(u, x), x)
+            return tdq.grad(u, t) - 0.0001 * u_xx + 5.0 * u ** 3 - 5.0 * u
+
+        init = IC(D, [lambda x: x ** 2 * np.cos(math.pi * x)], var=[["x"]])
+        per = periodicBC(D, ["x"], [deriv_model])
+        m = tdq.CollocationSolverND(verbose=False)
+        g = torch.Generator().manual_seed(1)
+        m.compile([2, 128, 128, 128, 128, 1], f_model, D, [init, per], Adaptive_type="self-adaptive",
+                  dict_adaptive={"residual": [True], "BCs": [True, False]},
+                  init_weights={"residual": [torch.rand(3000, 1, generator=g)],
+                                "BCs": [100 * torch.rand(512, 1, generator=g), None]},
+                  backend=backend, device="cuda")
+        return m
+
+    a, b = build("hip"), build("jet")
+    assert a.active_backend == "hip" and b.active_backend == "jet"
+    la, ga = a.grad()
+    lb, gb = b.grad()
+    assert abs(la.item() - lb.item()) / abs(lb.item()) < 1e-5
+    for x, y in zip(ga, gb):
+        assert ((x - y).norm() / y.norm().clamp_min(1e-12)).item() < 1e-4
+    a.fit(tf_iter=20)
+    b.fit(tf_iter=20)
+    la, lb = a.losses[-1]["Total Loss"], b.losses[-1]["Total Loss"]
+    assert abs(la - lb) / abs(lb) < 1e-3, (la, lb)
