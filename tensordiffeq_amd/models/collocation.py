@@ -26,7 +26,7 @@ from ..optimizers import Adam, eager_lbfgs, graph_lbfgs
 from ..output import print_screen
 from ..parallel import dist as pdist
 from .loss import LossProgram, Term
-from .networks import TanhMLP
+from .networks import FlatModule, TanhMLP
 
 _ADAPTIVE = {0: 0, "none": 0, "baseline": 0, "pinn": 0,
              1: 1, "self-adaptive": 1, "self_adaptive": 1, "sa": 1, "sa-pinn": 1,
@@ -110,9 +110,11 @@ class CollocationSolverND:
         self.X_f_local = X_f[self._lo:self._hi].to(self.device)
         self.X_f_in = [self.X_f_local[:, j:j + 1] for j in range(X_f.shape[1])]
         self.X_f_len = np.array([self.N_f])
+        if network is not None and not isinstance(network, (TanhMLP, FlatModule)):
+            network = FlatModule(network)
         self.u_model = network if network is not None else TanhMLP(self.layer_sizes, device=self.device)
         self.u_model.to(self.device)
-        if ctx.is_distributed and isinstance(self.u_model, TanhMLP):
+        if ctx.is_distributed:
             ctx.broadcast_(self.u_model.flat.data)
 
         self.Adaptive_type = parse_adaptive_type(Adaptive_type)
@@ -181,10 +183,12 @@ class CollocationSolverND:
         return list(d.get(key, d.get(key.lower(), [])))
 
     def _residual_count(self):
-        probe = self.X_f_local[:4].detach().double()
-        cols = [probe[:, j:j + 1].clone().requires_grad_(True) for j in range(probe.shape[1])]
         from .loss import _Float64View
-        net = _Float64View(self.u_model) if isinstance(self.u_model, TanhMLP) else self.u_model
+        is_mlp = isinstance(self.u_model, TanhMLP)
+        probe = self.X_f_local[:4].detach()
+        probe = probe.double() if is_mlp else probe
+        cols = [probe[:, j:j + 1].clone().requires_grad_(True) for j in range(probe.shape[1])]
+        net = _Float64View(self.u_model) if is_mlp else self.u_model
         out = self.f_model(net, *cols)
         return len(out) if isinstance(out, (tuple, list)) else 1
 
@@ -253,6 +257,7 @@ class CollocationSolverND:
         return prog
 
     def program(self, batch=None):
+        self._flat()  # wraps a user-assigned custom network
         if self._programs.get("net") is not self.u_model:
             self._programs = {"net": self.u_model}
             self._engine = None
@@ -281,9 +286,8 @@ class CollocationSolverND:
         return self._state
 
     def _flat(self):
-        if not isinstance(self.u_model, TanhMLP):
-            raise TypeError("training needs a TanhMLP u_model (flat parameter buffer); wrap custom "
-                            "networks with tensordiffeq_amd.models.networks.FlatModule")
+        if not isinstance(self.u_model, (TanhMLP, FlatModule)):
+            self.u_model = FlatModule(self.u_model).to(self.device)  # user replaced u_model
         return self.u_model.flat
 
     @property
@@ -439,8 +443,8 @@ class CollocationSolverND:
         X = torch.as_tensor(np.asarray(X_star) if not torch.is_tensor(X_star) else X_star,
                             dtype=torch.float32).to(self.device)
         with torch.no_grad():
-            u = torch.cat([self.u_model(X[i:i + chunk], params=params) if isinstance(self.u_model, TanhMLP)
-                           else self.u_model(X[i:i + chunk]) for i in range(0, X.shape[0], chunk)], dim=0)
+            u = torch.cat([self.u_model(X[i:i + chunk], params=params)
+                           for i in range(0, X.shape[0], chunk)], dim=0)
         prog = self.program()
         f = prog.residual_on(self.f_model, X, params=params, chunk=chunk)
         f_np = [x.cpu().numpy() for x in f]

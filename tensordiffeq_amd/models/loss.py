@@ -173,15 +173,12 @@ class LossProgram:
         """Return ``(total, {term_name: value})`` (differentiable w.r.t. ``params``, ``lambdas``
         and ``extras``).  ``extras`` replaces the extra callable arguments of residual terms
         (the DiscoveryModel's coefficients)."""
-        from .networks import TanhMLP
         params = self.net.flat if params is None else params
         J = None
         self._cur_net = self.net
         if self.backend != "autograd":
             J = self.jet(params)
-        elif params is not getattr(self.net, "flat", None):
-            if not isinstance(self.net, TanhMLP):
-                raise ValueError("custom networks are evaluated at their own parameters")
+        elif params is not self.net.flat:
             self._cur_net = _ParamView(self.net, params)
         vals = {}
         total = None

@@ -109,3 +109,43 @@ class TanhMLP(nn.Module):
 def neural_net(layer_sizes, device=None, generator=None):
     """Reference-named constructor (networks.py:10)."""
     return TanhMLP(layer_sizes, device=device, generator=generator)
+
+
+class FlatModule(nn.Module):
+    """Any user ``nn.Module`` (the reference allowed replacing ``u_model`` with a custom Keras
+    model, models.py:31) trained through the same flat-buffer engine: the module's parameters
+    are re-materialised as views of ``self.flat`` on every call with ``torch.func.functional_call``,
+    so gradients, Adam, L-BFGS, DP all-reduce and checkpoints see one contiguous vector.  Such
+    networks run on the generic nested-autograd backend."""
+
+    activation = None
+
+    def __init__(self, module):
+        super().__init__()
+        self.inner = module
+        names, shapes, chunks = [], [], []
+        for n, p in module.named_parameters():
+            names.append(n)
+            shapes.append(tuple(p.shape))
+            chunks.append(p.detach().reshape(-1))
+            p.requires_grad_(False)
+        self._names, self._shapes = names, shapes
+        self._numels = [int(torch.tensor(s).prod().item()) if s else 1 for s in shapes]
+        self.flat = nn.Parameter(torch.cat(chunks).clone())
+        self.layer_sizes = None
+
+    @property
+    def num_params(self):
+        return self.flat.numel()
+
+    def forward(self, *xs, params=None):
+        flat = self.flat if params is None else params
+        pd, off = {}, 0
+        for n, s, k in zip(self._names, self._shapes, self._numels):
+            pd[n] = flat[off:off + k].view(s)
+            off += k
+        x = xs[0] if len(xs) == 1 else torch.cat(xs, dim=1)
+        return torch.func.functional_call(self.inner, pd, (x,))
+
+    def summary(self):
+        return f"FlatModule({self.inner.__class__.__name__}, params={self.num_params})\n{self.inner}"
