@@ -110,7 +110,57 @@ class AdamEngine:
             self.graph_a = self.graph_b = None  # history pointer changed
 
     # ---------------------------------------------------------------- step pieces -------
+    def _fused_map(self, fop):
+        """wrt index -> where its gradient comes from in the fused kernel outputs."""
+        fl = fop.fl
+        n_lam = len(self.lambdas)
+        src = [("flat", 0)]
+        for i in range(1, len(self.wrt)):
+            if i <= n_lam:
+                k = i - 1
+                if k in fl.lam_slots:
+                    src.append(("dlam", fl.lam_slots.index(k)))
+                elif ("lam", k) in fl.scal_slots:
+                    src.append(("dscal", fl.scal_slots.index(("lam", k))))
+                else:
+                    src.append(("zero", 0))
+            else:
+                k = i - 1 - n_lam
+                src.append(("dscal", fl.scal_slots.index(("extra", k))) if ("extra", k) in fl.scal_slots
+                           else ("zero", 0))
+        return src
+
+    def _phase_a_fused(self, fop):
+        from .ops import jet_hip
+        prog = self.program
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan)
+        total, losses, dJ, dlam, dscal = fop(J)
+        gflat = jet_hip.backward_raw(saved, dJ)
+        if getattr(self, "_fsrc", None) is None:
+            self._fsrc = self._fused_map(fop)
+        grads = []
+        for (kind, k), w in zip(self._fsrc, self.wrt):
+            if kind == "flat":
+                grads.append(gflat)
+            elif kind == "dlam":
+                g = dlam[k]
+                rng = fop.fl.lam_offsets.get(fop.fl.lam_slots[k])
+                if rng is not None:
+                    full = torch.zeros(w.numel(), device=w.device)
+                    full[rng[0]:rng[1]] = g
+                    g = full
+                grads.append(g.view_as(w))
+            elif kind == "dscal":
+                grads.append(dscal[k].view_as(w))
+            else:
+                grads.append(torch.zeros_like(w))
+        terms = [losses[k] for k in range(len(self.term_names))]
+        return total, grads, terms
+
     def _phase_a(self):
+        fop = getattr(self.program, "fused_op", None)
+        if fop is not None:
+            return self._phase_a_fused(fop)
         alias = [t.detach().requires_grad_(True) for t in self.wrt]
         loss, vals = self.program.evaluate(**self.bind(alias))
         grads = torch.autograd.grad(loss, alias, allow_unused=True)
@@ -240,6 +290,14 @@ class LossGradEngine:
         self.n_evals = 0
 
     def _body(self):
+        fop = getattr(self.program, "fused_op", None)
+        if fop is not None:
+            from .ops import jet_hip
+            prog = self.program
+            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan)
+            total, _, dJ, _, _ = fop(J)
+            g = jet_hip.backward_raw(saved, dJ)
+            return torch.cat([g.reshape(-1), total.reshape(1)])
         p = self.flat.detach().requires_grad_(True)
         lams = [l.detach() for l in self.lambdas]
         loss, _ = self.program.evaluate(p, lams)

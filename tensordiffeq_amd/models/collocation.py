@@ -251,8 +251,11 @@ class CollocationSolverND:
         self._n_res = n_res
         for k in range(n_res):
             lam = self._lam_for.get(("residual", k))
-            prog.add_term(Term(f"Residual_{k}", "residual", seg=sr, fn=self.f_model, extra=(), index=k,
-                               lam=lam, denom=float(n_glob) if world > 1 or batch is not None else None))
+            term = Term(f"Residual_{k}", "residual", seg=sr, fn=self.f_model, extra=(), index=k,
+                        lam=lam, denom=float(n_glob) if world > 1 or batch is not None else None)
+            if batch is not None and lam is not None and self.lambdas[lam].numel() > 1:
+                term.lam_range = batch
+            prog.add_term(term)
         prog.finalize()
         return prog
 
@@ -264,7 +267,9 @@ class CollocationSolverND:
             self._lbfgs_engine = None
         key = ("batch", batch)
         if key not in self._programs:
-            self._programs[key] = self._build_program(batch)
+            prog = self._build_program(batch)
+            prog.enable_fusion(self.lambdas)
+            self._programs[key] = prog
         return self._programs[key]
 
     @property

@@ -101,6 +101,7 @@ class DiscoveryModel:
             prog.add_term(Term("Residual_0", "residual", seg=s, fn=self.f_model, extra=(self.vars,),
                                index=0, lam=0 if self.col_weights is not None else None, denom=denom))
             prog.finalize()
+            prog.enable_fusion(self._lambdas(), extras=(self.vars,))
             self._program = prog
             self._engine = None
         return self._program

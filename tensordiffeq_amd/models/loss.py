@@ -75,6 +75,7 @@ class LossProgram:
         self.backend = None
         self.X_all = None
         self.reasons = []
+        self.fused_op = None
 
     # ---------------------------------------------------------------- building -------
     def add_segment(self, name, X):
@@ -197,7 +198,11 @@ class LossProgram:
         return total, vals
 
     def _lam(self, t, lambdas):
-        return None if (t.lam is None or lambdas is None) else lambdas[t.lam]
+        if t.lam is None or lambdas is None:
+            return None
+        lam = lambdas[t.lam]
+        rng = getattr(t, "lam_range", None)
+        return lam if rng is None else lam[rng[0]:rng[1]]
 
     def _term(self, t, J, lambdas, cache):
         lam = self._lam(t, lambdas)
@@ -247,6 +252,26 @@ class LossProgram:
                         loss = m if loss is None else loss + m
             return loss
         raise ValueError(f"unknown term kind {t.kind}")
+
+    # ---------------------------------------------------------------- fusion ---------
+    def enable_fusion(self, lambdas, extras=None):
+        """Compile every term into the fused HIP loss kernel (HIP backend only).  Returns True
+        when the program runs fused; otherwise the autograd-composed loss stays in use."""
+        import os
+        from .. import fusion
+        self.fused_op = None
+        if self.backend != "hip" or os.environ.get("TDQ_FUSED_LOSS", "1") == "0":
+            return False
+        fl = fusion.build(self, lambdas)
+        if fl is None:
+            return False
+        from ..ops.loss_fused import FusedLossOp
+        scalars = fusion.scalar_values(fl, lambdas, extras)
+        try:
+            self.fused_op = FusedLossOp(fl, self, lambdas, scalars, fl.lam_offsets)
+        except ValueError:
+            return False
+        return True
 
     # ---------------------------------------------------------------- prediction -----
     def residual_on(self, fn, X, params=None, extra=(), chunk=65536):

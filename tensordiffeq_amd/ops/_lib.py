@@ -41,6 +41,8 @@ def _declare(lib):
         "tdq_jet_slab_floats": (L, [I, I, I, I, I]),
         "tdq_adam_multi": (I, [P, I, P, F, F, F, F, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
+        "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, P]),
+        "tdq_loss_meta_sizes": (I, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

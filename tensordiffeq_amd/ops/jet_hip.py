@@ -29,43 +29,53 @@ def stream_spec(plan):
     return out
 
 
+def forward_raw(X, P, net, plan):
+    """Autograd-free forward: returns ``(J, saved)`` where ``saved`` feeds :func:`backward_raw`."""
+    lib = _lib.load()
+    cfg = hip_config(net, plan)
+    X = X.contiguous()
+    N = X.shape[0]
+    S = plan.S
+    spec = stream_spec(plan)
+    spec_c = (ctypes.c_int * len(spec))(*spec)
+    J = torch.empty((S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
+    nscr = lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], S, 0)
+    scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
+    rc = lib.tdq_jet_fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
+                         cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_jet_fwd")
+    return J, (X, P, scratch, cfg, spec, S)
+
+
+def backward_raw(saved, dJ):
+    """Flat parameter gradient for the adjoint ``dJ`` of the jet."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    N = X.shape[0]
+    dJ = dJ.contiguous()
+    nwork = lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"])
+    work = torch.empty(max(int(nwork), 1), dtype=torch.float32, device=X.device)
+    grad = torch.empty_like(P)
+    spec_c = (ctypes.c_int * len(spec))(*spec)
+    rc = lib.tdq_jet_bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
+                         _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S,
+                         spec_c, _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_jet_bwd")
+    return grad
+
+
 class JetMLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, params, net, plan):
-        lib = _lib.load()
-        cfg = hip_config(net, plan)
-        X = X.contiguous()
-        P = params.contiguous()
-        N = X.shape[0]
-        S = plan.S
-        spec = stream_spec(plan)
-        spec_c = (ctypes.c_int * len(spec))(*spec)
-        J = torch.empty((S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
-        nscr = lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], S, 0)
-        scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
-        rc = lib.tdq_jet_fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
-                             cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c,
-                             _lib.stream_ptr(X.device))
-        _lib.check(rc, "tdq_jet_fwd")
-        ctx.save_for_backward(X, P, scratch)
-        ctx.cfg = cfg
-        ctx.spec = spec
-        ctx.S = S
+        J, saved = forward_raw(X, params.contiguous(), net, plan)
+        ctx.save_for_backward(saved[0], saved[1], saved[2])
+        ctx.meta = saved[3:]
         return J
 
     @staticmethod
     def backward(ctx, dJ):
-        lib = _lib.load()
         X, P, scratch = ctx.saved_tensors
-        cfg = ctx.cfg
-        N = X.shape[0]
-        dJ = dJ.contiguous() if dJ is not None else torch.zeros((ctx.S, N, cfg["d_out"]), device=X.device)
-        nwork = lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"])
-        work = torch.empty(max(int(nwork), 1), dtype=torch.float32, device=X.device)
-        grad = torch.empty_like(P)
-        spec_c = (ctypes.c_int * len(ctx.spec))(*ctx.spec)
-        rc = lib.tdq_jet_bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
-                             _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"],
-                             ctx.S, spec_c, _lib.stream_ptr(X.device))
-        _lib.check(rc, "tdq_jet_bwd")
-        return None, grad, None, None
+        cfg, spec, S = ctx.meta
+        if dJ is None:
+            dJ = torch.zeros((S, X.shape[0], cfg["d_out"]), device=X.device)
+        return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None

@@ -1,0 +1,97 @@
+"""Host side of the fused loss kernel (``csrc/loss_fused.hip``).
+
+Built once per :class:`~tensordiffeq_amd.models.loss.LossProgram` from its traced
+:class:`~tensordiffeq_amd.fusion.FusedLoss`: bytecode, constants, outputs, the group table and a
+pointer table are uploaded to device buffers; every output buffer (dJ, dlam, block partials,
+losses, scalar grads) is persistent, so a captured HIP graph replays the same pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ..fusion import OP
+
+LF_BLOCK = 128
+MAX_GROUPS, MAX_SLOTS, MAX_VAL, MAX_LAM, MAX_SCAL, MAX_TERMS = 32, 2, 16, 8, 8, 32
+
+
+class FusedLossOp:
+    def __init__(self, fl, prog, lambdas, scalars, lam_offsets=None):
+        dev = prog.device
+        if len(fl.groups) > MAX_GROUPS or len(fl.val_arrays) > MAX_VAL or len(fl.lam_slots) > MAX_LAM \
+                or len(fl.scal_slots) > MAX_SCAL or len(fl.term_names) > MAX_TERMS:
+            raise ValueError("fused loss program exceeds kernel table limits")
+        self.fl, self.prog = fl, prog
+        code, consts, outs, groups = [], [], [], []
+        block_off = 0
+        self.max_regs = 1
+        for gr in fl.groups:
+            P = gr.program
+            if len(gr.segs) > MAX_SLOTS:
+                raise ValueError("group reads more than 2 segments")
+            loaded = [0] * MAX_SLOTS
+            for (slot, s) in P.stream_regs:
+                loaded[slot] |= 1 << s
+            seg_off = [prog.segments[s].offset for s in gr.segs] + [0] * (MAX_SLOTS - len(gr.segs))
+            groups.append([len(code), len(P.code), len(consts), P.n_regs, gr.n, block_off, len(outs),
+                           len(P.outputs), len(gr.segs)] + seg_off + loaded)
+            code += P.code
+            consts += P.consts
+            outs += P.outputs
+            block_off += max(1, math.ceil(gr.n / LF_BLOCK))
+            self.max_regs = max(self.max_regs, P.n_regs)
+        self.n_blocks = block_off
+        self.n_groups = len(groups)
+        self.n_terms = len(fl.term_names)
+        self.n_scal = len(fl.scal_slots)
+        self.code = torch.tensor(np.asarray(code, dtype=np.int32).reshape(-1, 4), device=dev)
+        self.consts = torch.tensor(np.asarray(consts + [0.0], dtype=np.float32), device=dev)
+        ob = np.zeros(max(1, len(outs)), dtype=[("f", "<i4"), ("w", "<i4"), ("t", "<i4"), ("c", "<f4")])
+        for k, (f, w, t, c) in enumerate(outs):
+            ob[k] = (f, w, t, c)
+        self.outs = torch.from_numpy(ob.view(np.uint8).copy()).to(dev)
+        self.groups = torch.tensor(np.asarray(groups, dtype=np.int32), device=dev)
+        # persistent inputs / outputs
+        self.vals = [v.to(dev).contiguous() for v in fl.val_arrays]
+        lam_offsets = lam_offsets or {}
+        self.lams = lambdas
+        self.dlam = []
+        for k in fl.lam_slots:
+            lo, hi = lam_offsets.get(k, (0, lambdas[k].shape[0]))
+            self.dlam.append(torch.zeros(hi - lo, device=dev))
+        self.scalars = scalars
+        ptrs = np.zeros(MAX_VAL + 3 * MAX_LAM + MAX_SCAL, dtype=np.int64)
+        ptrs[MAX_VAL + 3 * MAX_LAM:] = 0
+        for i, v in enumerate(self.vals):
+            ptrs[i] = v.data_ptr()
+        for i, k in enumerate(fl.lam_slots):
+            lo = lam_offsets.get(k, (0, 0))[0]
+            ptrs[MAX_VAL + i] = lambdas[k].data_ptr() + 4 * lo
+            ptrs[MAX_VAL + MAX_LAM + i] = self.dlam[i].data_ptr()
+        for i, s in enumerate(scalars):
+            ptrs[MAX_VAL + 2 * MAX_LAM + i] = s.data_ptr()
+        # layout of LFPtrs: val[16], lam[8], dlam[8], scal[8]
+        self.ptrs = torch.from_numpy(ptrs[:MAX_VAL + 2 * MAX_LAM + MAX_SCAL].copy()).to(dev)
+        N = prog.X_all.shape[0]
+        self.N = N
+        self.dJ = torch.zeros((fl.n_streams, N, 1), device=dev)
+        self.partials = torch.zeros(self.n_blocks * (self.n_terms + self.n_scal), device=dev)
+        self.losses = torch.zeros(self.n_terms, device=dev)
+        self.total = torch.zeros((), device=dev)
+        self.dscal = torch.zeros(max(1, self.n_scal), device=dev)
+
+    def __call__(self, J):
+        lib = _lib.load()
+        rc = lib.tdq_loss_fused(_lib.ptr(self.code), _lib.ptr(self.consts), _lib.ptr(self.outs),
+                                _lib.ptr(self.groups), _lib.ptr(self.ptrs), self.n_groups, self.n_terms,
+                                self.n_scal, self.fl.n_streams, self.prog.d_in, self.N, _lib.ptr(J),
+                                _lib.ptr(self.prog.X_all), _lib.ptr(self.dJ), _lib.ptr(self.partials),
+                                self.n_blocks, self.max_regs, _lib.ptr(self.losses), _lib.ptr(self.total),
+                                _lib.ptr(self.dscal), _lib.stream_ptr(J.device))
+        _lib.check(rc, "tdq_loss_fused")
+        return self.total, self.losses, self.dJ, self.dlam, self.dscal
