@@ -34,7 +34,7 @@ sys.path.insert(0, HERE)
 METRIC = "collocation-pts/sec + L2 rel-error, Allen-Cahn SA-PINN @ 1/2/4/8 GPU"
 
 
-def build_problem(n_per_gpu, world, backend, device, dist):
+def build_problem(n_per_gpu, world, backend, device, dist, precision=None):
     import tensordiffeq_amd as tdq
     from tensordiffeq_amd.boundaries import DomainND, IC, periodicBC
 
@@ -69,7 +69,8 @@ def build_problem(n_per_gpu, world, backend, device, dist):
     model.compile([2, 128, 128, 128, 128, 1], f_model, D, [init, x_periodic],
                   Adaptive_type="self-adaptive",
                   dict_adaptive={"residual": [True], "BCs": [True, False]},
-                  init_weights=init_weights, backend=backend, device=device, dist=dist)
+                  init_weights=init_weights, backend=backend, device=device, dist=dist,
+                  precision=precision)
     return model
 
 
@@ -94,6 +95,8 @@ def main(argv=None):
     ap.add_argument("--npts", type=int, default=50000, help="collocation points per GPU")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--no-l2", action="store_true")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"],
+                    help="GEMM precision of the HIP jet kernels (bf16x3 = split-bf16 MFMA, fp32 accumulate)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +108,7 @@ def main(argv=None):
     if device.type == "cuda":
         torch.cuda.set_device(device)
 
-    model = build_problem(args.npts, world, args.backend, device, dist)
+    model = build_problem(args.npts, world, args.backend, device, dist, args.precision)
     eng = model._get_engine(None, args.warmup + args.steps + 2)
     backend = model.active_backend
 
@@ -146,11 +149,14 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "bf16" if (backend == "hip" and args.precision == "bf16x3") else "fp32",
             "data": "synthetic (LHS collocation points, random Keras-init weights); L2 on data/AC.mat",
             "config": {"model": "Allen-Cahn SA-PINN tanh MLP [2,128,128,128,128,1]",
                        "global_batch": n_glob, "seq_len": None, "parallelism": f"dp{world}",
                        "points_per_gpu": args.npts, "backend": backend,
+                       "precision": (("bf16x3: split-bf16 MFMA (hi*hi+hi*lo+lo*hi), fp32 accumulate, "
+                                      "fp32 elementwise/loss/optimizer") if args.precision == "bf16x3"
+                                     else "fp32 MFMA") if backend == "hip" else "fp32",
                        "bc_points": "IC 512 (SA) + periodic 2x201 (u, u_x)"},
             "loss_after": loss,
             "l2_rel_error_after_steps": l2,

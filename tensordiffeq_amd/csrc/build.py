@@ -36,7 +36,7 @@ def _flags():
 
 def _compile(src, force):
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
-    deps = [src, os.path.join(HERE, "common.h")]
+    deps = [src] + glob.glob(os.path.join(HERE, "*.h"))
     if not force and os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj, False
     cmd = [hipcc()] + _flags() + ["-c", src, "-o", obj]

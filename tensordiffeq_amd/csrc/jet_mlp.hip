@@ -26,31 +26,8 @@
 //     dK = sum_points sum_streams h_prev zb^T on MFMA after an LDS transpose (points move from
 //     the lane index to the k index).  Each workgroup writes one partial-gradient slab; a
 //     deterministic two-pass reduction folds the slabs into the flat gradient (Keras order).
-#include "common.h"
+#include "jet_common.h"
 
-#define TDQ_MAXS 8
-#define TDQ_MAXD 8
-#define TDQ_MAXO 4
-
-// Stream plan.  Second-order streams pick their two first-order factors with one-hot FLOAT
-// weights (selA/selB) instead of an integer index: an index-driven select over a register
-// array is turned back into a scratch-memory lookup by LLVM, an FMA chain is not.
-struct JetSpec {
-  int stype[TDQ_MAXS];             // 0 value, 1 first order, 2 second order
-  int var[TDQ_MAXS];               // type 1: input variable index
-  float selA[TDQ_MAXS][TDQ_MAXS];  // type 2: one-hot over streams of first-order factor a
-  float selB[TDQ_MAXS][TDQ_MAXS];  // type 2: one-hot over streams of first-order factor b
-  int ia[TDQ_MAXS], ib[TDQ_MAXS];  // type 2: the same factors as stream indices (memory addressing only)
-};
-
-struct NetDims {
-  int d_in, width, d_out, n_hidden;
-};
-
-__device__ __forceinline__ int off_layer(const NetDims& d, int i) {
-  // start of dense layer i (>= 1) in the flat Keras-order buffer
-  return d.d_in * d.width + d.width + (i - 1) * (d.width * d.width + d.width);
-}
 
 template <int S, int WT>
 __device__ __forceinline__ f32x4 pick(const f32x4 (&v)[S][WT], const float (&sel)[TDQ_MAXS], int t) {
@@ -93,11 +70,6 @@ __device__ __forceinline__ void tanh_jet_fwd(const JetSpec sp, const f32x4 (&z)[
   }
 }
 
-__device__ __forceinline__ size_t zs_index(int layer, int nwg, int wg, int S, int s, int w, int WT,
-                                           int t, int lane) {
-  // (wave-uniform tile base) + (32-bit lane offset): lets hipcc use SGPR-base addressing
-  return ((((((size_t)layer * nwg + wg) * S + s) * 4 + w) * WT + t) * 256) + (unsigned)(lane * 4);
-}
 
 // ------------------------------------------------------------------------------------------
 // weight images: zero-padded W x W copies of the hidden kernels, read directly by the MFMA
@@ -654,14 +626,6 @@ __global__ void __launch_bounds__(256) slab_reduce2(const float* __restrict__ pa
 // ------------------------------------------------------------------------------------------
 namespace {
 
-int width_tiles(int width) {
-  int wt = (width + 15) / 16;
-  if (wt <= 1) return 1;
-  if (wt <= 2) return 2;
-  if (wt <= 4) return 4;
-  if (wt <= 8) return 8;
-  return -1;
-}
 
 size_t fwd_lds_bytes(int WT, int S) { return (size_t)4 * S * WT * 256 * sizeof(float); }
 
@@ -672,29 +636,6 @@ size_t bwd_lds_bytes(int WT, int S) {
   return floats * sizeof(float);
 }
 
-int param_count(int d_in, int width, int d_out, int n_hidden) {
-  return d_in * width + width + (n_hidden - 1) * (width * width + width) + width * d_out + d_out;
-}
-
-// spec: 3 ints per stream (type, a, b): type 1 -> a = input variable; type 2 -> a, b = stream
-// indices of the two first-order factors.
-bool make_spec(int S, const int* spec, JetSpec& sp) {
-  if (S < 1 || S > TDQ_MAXS) return false;
-  for (int s = 0; s < TDQ_MAXS; ++s) {
-    const int ty = s < S ? spec[3 * s] : 0, a = s < S ? spec[3 * s + 1] : 0, b = s < S ? spec[3 * s + 2] : 0;
-    sp.stype[s] = ty;
-    sp.var[s] = ty == 1 ? a : 0;
-    sp.ia[s] = ty == 2 ? a : 0;
-    sp.ib[s] = ty == 2 ? b : 0;
-    for (int q = 0; q < TDQ_MAXS; ++q) {
-      sp.selA[s][q] = (ty == 2 && q == a) ? 1.f : 0.f;
-      sp.selB[s][q] = (ty == 2 && q == b) ? 1.f : 0.f;
-    }
-    if (ty == 2 && (a <= 0 || a >= S || b <= 0 || b >= S || spec[3 * a] != 1 || spec[3 * b] != 1)) return false;
-    if (ty == 1 && a < 0) return false;
-  }
-  return true;
-}
 
 template <int WT, int S>
 int launch_fwd(const float* X, const float* P, const float* Wt, float* J, float* Zs, int N, NetDims d,
@@ -833,6 +774,14 @@ int tdq_jet_bwd(const float* X, const float* P, const float* dJ, const float* Zs
     rc = run();
   }
   if (rc) return rc;
+  return tdq_slab_reduce(work, grad, nwg, Ptot, chunks, stream);
+}
+
+// slabs [nwg][Ptot] at work, partials [chunks][Ptot] right after them -> grad[Ptot]
+int tdq_slab_reduce(float* work, float* grad, int nwg, int Ptot, int chunks, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* slab = work;
+  float* part = work + (size_t)nwg * Ptot;
   dim3 g1((Ptot + 255) / 256, chunks);
   hipLaunchKernelGGL(slab_reduce1, g1, dim3(256), 0, st, slab, part, nwg, Ptot, chunks);
   TDQ_CHECK_LAUNCH();

@@ -133,7 +133,7 @@ class AdamEngine:
     def _phase_a_fused(self, fop):
         from .ops import jet_hip
         prog = self.program
-        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan)
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
         total, losses, dJ, dlam, dscal = fop(J)
         gflat = jet_hip.backward_raw(saved, dJ)
         if getattr(self, "_fsrc", None) is None:
@@ -294,7 +294,7 @@ class LossGradEngine:
         if fop is not None:
             from .ops import jet_hip
             prog = self.program
-            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan)
+            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
             total, _, dJ, _, _ = fop(J)
             g = jet_hip.backward_raw(saved, dJ)
             return torch.cat([g.reshape(-1), total.reshape(1)])

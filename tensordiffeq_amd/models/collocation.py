@@ -81,7 +81,7 @@ class CollocationSolverND:
     # ================================================================== compile =========
     def compile(self, layer_sizes, f_model, domain, bcs, Adaptive_type=0, dict_adaptive=None,
                 init_weights=None, g=None, dist=False, backend="auto", device=None,
-                periodic_legacy=False, seed=None, network=None):
+                periodic_legacy=False, seed=None, network=None, precision=None):
         if seed is not None:
             from ..utils.seeding import set_seed
             set_seed(seed)
@@ -99,6 +99,7 @@ class CollocationSolverND:
         self.g = g
         self.domain = domain
         self.backend = backend
+        self.precision = precision
         self.periodic_legacy = periodic_legacy
         if domain.X_f is None:
             raise ValueError("call domain.generate_collocation_points(N_f) before compile")
@@ -197,6 +198,7 @@ class CollocationSolverND:
         world = ctx.world if ctx.is_distributed else 1
         rep_scale = 1.0 / world
         prog = LossProgram(self.u_model, len(self.domain.vars), self.device, backend=self.backend,
+                           precision=self.precision,
                            world=world, weight_outside_sum=self.weight_outside_sum, g=self.g,
                            periodic_legacy=self.periodic_legacy)
         for i, bc in enumerate(self.bcs):

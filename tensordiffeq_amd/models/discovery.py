@@ -43,7 +43,7 @@ class DiscoveryModel:
         self.var_history = []
 
     def compile(self, layer_sizes, f_model, X, u, var, col_weights=None, dist=False,
-                backend="auto", device=None, seed=None):
+                backend="auto", device=None, seed=None, precision=None):
         if seed is not None:
             from ..utils.seeding import set_seed
             set_seed(seed)
@@ -82,6 +82,7 @@ class DiscoveryModel:
         else:
             self.col_weights = None
         self.backend = backend
+        self.precision = precision
         self._engine = None
         self._program = None
         self._state = None
@@ -93,6 +94,7 @@ class DiscoveryModel:
             world = ctx.world if ctx.is_distributed else 1
             g = (lambda l: l * l) if self.col_weights is not None else None
             prog = LossProgram(self.u_model, self.X.shape[1], self.device, backend=self.backend,
+                           precision=self.precision,
                                world=world, g=g)
             s = prog.add_segment("data", self.X)
             prog.register_callable(self.f_model, s, extra_args=(self.vars,))

@@ -58,8 +58,9 @@ class Term:
 
 class LossProgram:
     def __init__(self, net, d_in, device, dtype=torch.float32, backend="auto", world=1,
-                 weight_outside_sum=False, g=None, periodic_legacy=False):
+                 weight_outside_sum=False, g=None, periodic_legacy=False, precision=None):
         self.net = net
+        self.precision = precision   # HIP jet GEMM precision (None: ops.jet_mlp default)
         self.d_in = d_in
         self.device = torch.device(device)
         self.dtype = dtype
@@ -149,7 +150,7 @@ class LossProgram:
     def jet(self, params, X=None):
         from ..ops import jet_mlp
         X = self.X_all if X is None else X
-        return jet_mlp.jet_eval(X, self.net, params, self.plan, self.backend)
+        return jet_mlp.jet_eval(X, self.net, params, self.plan, self.backend, self.precision)
 
     def call(self, fn, si, extra=(), J=None, X=None):
         """Evaluate a user callable on segment ``si`` (or explicit points ``X``)."""

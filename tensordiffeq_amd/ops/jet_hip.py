@@ -29,21 +29,37 @@ def stream_spec(plan):
     return out
 
 
-def forward_raw(X, P, net, plan):
-    """Autograd-free forward: returns ``(J, saved)`` where ``saved`` feeds :func:`backward_raw`."""
+def _fns(lib, cfg):
+    if cfg["precision"] == "bf16x3":
+        return (lib.tdq_jet_fwd_bf3, lib.tdq_jet_bwd_bf3,
+                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["width"], cfg["n_hidden"], cfg["S"]),
+                lambda N: lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
+    return (lib.tdq_jet_fwd, lib.tdq_jet_bwd,
+            lambda N: lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], cfg["S"], 0),
+            lambda N: lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
+
+
+def forward_raw(X, P, net, plan, precision=None):
+    """Autograd-free forward: returns ``(J, saved)`` where ``saved`` feeds :func:`backward_raw`.
+
+    ``precision``: ``"bf16x3"`` (csrc/jet_bf3.hip, saves post-activations) or ``"fp32"``
+    (csrc/jet_mlp.hip, saves pre-activations); the saved buffer only fits its own backward."""
     lib = _lib.load()
-    cfg = hip_config(net, plan)
+    cfg = hip_config(net, plan, precision)
+    fwd, _, scratch_floats, _ = _fns(lib, cfg)
     X = X.contiguous()
     N = X.shape[0]
     S = plan.S
     spec = stream_spec(plan)
     spec_c = (ctypes.c_int * len(spec))(*spec)
     J = torch.empty((S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
-    nscr = lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], S, 0)
+    nscr = scratch_floats(N)
+    if nscr < 0:
+        raise ValueError(f"jet kernels cannot serve {cfg}")
     scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
-    rc = lib.tdq_jet_fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
+    rc = fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
                          cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, _lib.stream_ptr(X.device))
-    _lib.check(rc, "tdq_jet_fwd")
+    _lib.check(rc, f"tdq_jet_fwd[{cfg['precision']}]")
     return J, (X, P, scratch, cfg, spec, S)
 
 
@@ -51,23 +67,24 @@ def backward_raw(saved, dJ):
     """Flat parameter gradient for the adjoint ``dJ`` of the jet."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
+    _, bwd, _, slab_floats = _fns(lib, cfg)
     N = X.shape[0]
     dJ = dJ.contiguous()
-    nwork = lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"])
+    nwork = slab_floats(N)
     work = torch.empty(max(int(nwork), 1), dtype=torch.float32, device=X.device)
     grad = torch.empty_like(P)
     spec_c = (ctypes.c_int * len(spec))(*spec)
-    rc = lib.tdq_jet_bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
+    rc = bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
                          _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S,
                          spec_c, _lib.stream_ptr(X.device))
-    _lib.check(rc, "tdq_jet_bwd")
+    _lib.check(rc, f"tdq_jet_bwd[{cfg['precision']}]")
     return grad
 
 
 class JetMLPFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, X, params, net, plan):
-        J, saved = forward_raw(X, params.contiguous(), net, plan)
+    def forward(ctx, X, params, net, plan, precision=None):
+        J, saved = forward_raw(X, params.contiguous(), net, plan, precision)
         ctx.save_for_backward(saved[0], saved[1], saved[2])
         ctx.meta = saved[3:]
         return J
@@ -78,4 +95,4 @@ class JetMLPFunction(torch.autograd.Function):
         cfg, spec, S = ctx.meta
         if dJ is None:
             dJ = torch.zeros((S, X.shape[0], cfg["d_out"]), device=X.device)
-        return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None
+        return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None

@@ -20,6 +20,8 @@ HIP path (``backend="hip"``, MI355X): two kernels from ``csrc/jet_mlp.hip``
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..jet import jet_forward
@@ -27,14 +29,32 @@ from . import _lib
 
 MAX_S = 8
 PTS_PER_WG = 64
+PRECISIONS = ("bf16x3", "fp32")
+_precision = os.environ.get("TDQ_PRECISION", "bf16x3")
+
+
+def set_precision(p):
+    """Default GEMM precision of the HIP jet kernels: ``"bf16x3"`` (split-bf16 MFMA, ~2^-16 relative
+    error per product, default) or ``"fp32"`` (exact-fp32 MFMA)."""
+    global _precision
+    if p not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}")
+    _precision = p
+
+
+def get_precision():
+    return _precision
 
 
 def _pad16(w):
     return (w + 15) // 16 * 16
 
 
-def hip_config(net, plan):
-    """Return the kernel geometry or raise ValueError if the kernels cannot serve it."""
+def hip_config(net, plan, precision=None):
+    """Return the kernel geometry or raise ValueError if the kernels cannot serve it.
+
+    ``precision`` (default: :func:`get_precision`) picks the kernel family; bf16x3 needs at least
+    two 16-feature tiles (width > 16) and falls back to fp32 below that."""
     sizes = net.layer_sizes
     d_in, d_out = sizes[0], sizes[-1]
     hidden = sizes[1:-1]
@@ -60,8 +80,13 @@ def hip_config(net, plan):
         raise ValueError(f"streams x width tiles = {S * WT} > 32 (register budget)")
     if d_in > 8 or d_out > 4:
         raise ValueError("input width > 8 or output width > 4")
+    precision = precision or _precision
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision {precision!r} not in {PRECISIONS}")
+    if precision == "bf16x3" and WT < 2:
+        precision = "fp32"
     return {"d_in": d_in, "d_out": d_out, "width": hidden[0], "WT": WT, "S": S,
-            "n_hidden": len(hidden)}
+            "n_hidden": len(hidden), "precision": precision}
 
 
 def hip_eligible(net, plan, device):
@@ -81,10 +106,10 @@ def hip_eligible(net, plan, device):
     return True, ""
 
 
-def jet_eval(X, net, params, plan, backend):
+def jet_eval(X, net, params, plan, backend, precision=None):
     if backend == "jet":
         return jet_forward(X, net.weights(params), plan)
     if backend == "hip":
         from . import jet_hip
-        return jet_hip.JetMLPFunction.apply(X, params, net, plan)
+        return jet_hip.JetMLPFunction.apply(X, params, net, plan, precision)
     raise ValueError(f"jet_eval backend {backend!r}")
