@@ -6,9 +6,9 @@ B="python3 $R/bench.py --steps 10 --warmup 2 --no-l2"
 i=0
 for G in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES" \
          "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
-         "FETCH_SIZE WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
-         "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_FLAT SQ_INSTS_SMEM"; do
+         "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_LDS_UNALIGNED_STALL SQ_INSTS_SMEM" \
+         "TCC_HIT_sum TCC_MISS_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $G --kernel-include-regex "jet_|loss_fused" -d $R/gpurun_out/pmc$i --output-format csv -- $B > $R/gpurun_out/pmc$i.log 2>&1 || { echo "fail $i"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $G --kernel-include-regex "jet_" -d $R/gpurun_out/pmcb$i --output-format csv -- $B > $R/gpurun_out/pmcb$i.log 2>&1 || { echo "fail $i"; tail -3 $R/gpurun_out/pmcb$i.log; exit 1; }
 done
 echo done

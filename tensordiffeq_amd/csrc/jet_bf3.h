@@ -1,0 +1,756 @@
+// Split-bf16 ("bf16x3") Taylor-jet tanh-MLP forward / backward kernels for gfx950 (MI355X, CDNA4).
+//
+// Same contract as jet_mlp.hip (stream jets J[s][n][q] of a tanh MLP and the flat parameter
+// gradient of <dJ, J>), re-tiled for the bf16 matrix cores: on gfx950 the exact-fp32 MFMA runs
+// at the fp32 VECTOR rate (64 FLOP/clk/SIMD) while v_mfma_f32_16x16x32_bf16 runs 16x faster.
+// Every GEMM operand is split x = hi + lo (two bf16, |x - hi - lo| <= 2^-17 |x|) and a product
+// is formed as ah*bh + ah*bl + al*bh with fp32 accumulation: 3 bf16 MFMAs per fp32-equivalent
+// product (5.3x the fp32-MFMA rate) at ~2^-16 relative error per product (the dropped al*bl
+// term), i.e. ~19 significant bits instead of bf16's 8.
+//
+// Layout (16x16x32 MFMA: lane l = (p = l&15, g = l>>4); A[p][8g+j], B[8g+j][p], D[4g+r][p]):
+//   * one workgroup = 4 waves x 16 points, one point per lane column, features in registers;
+//   * k-block kb of a layer covers features 32kb..32kb+31 in the PERMUTED order
+//       k = 8g + j  <->  feature 32kb + (j < 4 ? 4g + j : 16 + 4g + j - 4)
+//     so the fp32 accumulator tiles 2kb and 2kb+1 (lane holds rows 4g..4g+3 of each) ARE the
+//     B fragment of k-block kb after a hi/lo split - no lane movement between layers;
+//   * weights are pre-split into hi/lo A-fragment images in that permuted k order
+//     (pack_bf3_kernel: 16 B per lane per (layer, out tile, k-block)), streamed from L2 with a
+//     4-step register prefetch ring; biases / first and last layer come from a zero-padded
+//     fp32 "aux" image so that no load in a kernel needs a bounds guard (no exec branches);
+//   * streams are in JetPlan's canonical order - value, S1 first-order, NSO second-order - and
+//     NSO is a template parameter: the jet epilogues are branch-free straight-line code, the
+//     two first-order factors of a second-order stream are picked by uniform-index selects;
+//   * forward: the epilogue of output tile o-1 (bias, tanh jet, save, hi/lo split, stage) is
+//     issued in the same scheduling region as the MFMAs of tile o (double-buffered
+//     accumulators), so VALU work fills the MFMA shadow; it saves the POST-activation streams
+//     h (fp32).  The backward needs no tanh recompute: with s1 = 1 - h^2 and s2 z_a = -2 h h_a
+//       zb_ab = s1 hb_ab
+//       zb_a  = s1 hb_a - 2 h sum_{(a,b)} h_b hb_ab
+//       zb    = s1 hb - 2 h sum_{s>0} h_s hb_s - 2 sum_{(a,b)} h_a h_b hb_ab
+//   * dK = sum_points sum_streams h_prev zb^T reduces over POINTS: both operands go through
+//     [point][feature] bf16 LDS images read back transposed with ds_read_b64_tr_b16, so points
+//     land on the MFMA k index (8 consecutive points per lane); the next stream's h_prev tiles
+//     are in flight from HBM while the current stream's MFMAs run.
+// Reference behaviour: the nested tf.gradients of the PDE residual (SURVEY.md §2.2 K2-K8,
+// tensordiffeq/models.py:update_loss / utils.py:get_tf_model); jet_mlp.hip is the fp32 twin.
+#pragma once
+#include "jet_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// aux image (fp32, zero padded to W = 16 WT features; TDQ_MAXO output columns):
+//   K0 [d_in][W] | b0 [W] | b_1..b_{Lh-1} [Lh-1][W] | Ko [W][4] | bo [4]
+__host__ __device__ inline int aux_b0(const NetDims& d, int W) { return d.d_in * W; }
+__host__ __device__ inline int aux_bh(const NetDims& d, int W) { return (d.d_in + 1) * W; }
+__host__ __device__ inline int aux_ko(const NetDims& d, int W) { return (d.d_in + d.n_hidden) * W; }
+__host__ __device__ inline int aux_bo(const NetDims& d, int W) { return (d.d_in + d.n_hidden + 4) * W; }
+__host__ __device__ inline int aux_floats(const NetDims& d, int W) { return (d.d_in + d.n_hidden + 4) * W + 4; }
+
+__device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// c += a * b  with a ~ ah + al, b ~ bh + bl  (al*bl dropped)
+__device__ __forceinline__ f32x4 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
+  c = mfma_bf(al, bh, c);
+  c = mfma_bf(ah, bl, c);
+  return mfma_bf(ah, bh, c);
+}
+
+// hi = rne_bf16(x), lo = rne_bf16(x - hi), two values per v_cvt_pk_bf16_f32
+__device__ __forceinline__ void split4(const f32x4 v, bf16x4& hi, bf16x4& lo) {
+  u32x2 H, L;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const f32x2 x = {v[2 * k], v[2 * k + 1]};
+    const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+    // scalar subtracts: packed f32 VALU (v_pk_add_f32) next to MFMAs costs extra issue cycles
+    const float r0 = v[2 * k] - __builtin_bit_cast(float, hb << 16);
+    const float r1 = v[2 * k + 1] - __builtin_bit_cast(float, hb & 0xffff0000u);
+    const f32x2 rl = {r0, r1};
+    H[k] = hb;
+    L[k] = __builtin_bit_cast(unsigned, __builtin_convertvector(rl, bf16x2));
+  }
+  hi = __builtin_bit_cast(bf16x4, H);
+  lo = __builtin_bit_cast(bf16x4, L);
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x4 half8(bf16x8 v, int hi_half) {
+  return hi_half ? __builtin_shufflevector(v, v, 4, 5, 6, 7) : __builtin_shufflevector(v, v, 0, 1, 2, 3);
+}
+
+// transposed LDS read (T10): lane 4q+c of each 16-lane group addresses row q, columns 4c..4c+3
+// of a 4 x 16 block; lane i of the group receives column i, rows 0..3.
+__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// tanh(z) and s1 = 1 - tanh(z)^2 without cancellation: e = exp(-2|z|),
+//   tanh|z| = (1 - e) / (1 + e)  (odd Taylor polynomial below 1/8),  s1 = 4 e / (1 + e)^2
+__device__ __forceinline__ void tanh_s1(float z, float& h, float& s1) {
+  const float az = fabsf(z);
+  const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * az);
+  const float r = __builtin_amdgcn_rcpf(1.f + e);
+  const float z2 = az * az;
+  const float poly = az * fmaf(z2, fmaf(z2, fmaf(z2, -0.053968254f, 0.13333334f), -0.33333334f), 1.f);
+  const float t = az < 0.125f ? poly : (1.f - e) * r;
+  h = __builtin_copysignf(t, z);
+  s1 = 4.f * e * (r * r);
+}
+
+// first-order stream `idx` (uniform, 1..S1) of a per-stream array.  Up to two candidates: a
+// select; more: the one-hot FMA over `sel` (LLVM turns a longer select chain over a register
+// array back into an indexed scratch load).
+template <int S, int S1, typename T>
+__device__ __forceinline__ T sel_first(const T (&v)[S], int idx, const float (&sel)[TDQ_MAXS]) {
+  if constexpr (S1 <= 2) {
+    T r = v[1];
+    if constexpr (S1 == 2) r = (idx == 2) ? v[2] : r;
+    return r;
+  } else {
+    T r = sel[1] * v[1];
+#pragma unroll
+    for (int q = 2; q <= S1; ++q) r += sel[q] * v[q];
+    return r;
+  }
+}
+
+// forward tanh jet of one feature tile: z -> h
+template <int S, int NSO>
+__device__ __forceinline__ void tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  f32x4 za[S], zb[S];
+#pragma unroll
+  for (int s = SO; s < S; ++s) {
+    za[s] = sel_first<S, S1>(z, sp.ia[s], sp.selA[s]);
+    zb[s] = sel_first<S, S1>(z, sp.ib[s], sp.selB[s]);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float hv, s1;
+    tanh_s1(z[0][c], hv, s1);
+    const float s2 = -2.f * hv * s1;
+    h[0][c] = hv;
+#pragma unroll
+    for (int s = 1; s < SO; ++s) h[s][c] = s1 * z[s][c];
+#pragma unroll
+    for (int s = SO; s < S; ++s) h[s][c] = fmaf(s2 * za[s][c], zb[s][c], s1 * z[s][c]);
+  }
+}
+
+// backward tanh jet of one feature tile from the saved post-activations h: hb -> zb
+template <int S, int NSO>
+__device__ __forceinline__ void tanh_jet_b(const JetSpec& sp, const f32x4 (&h)[S], const f32x4 (&hb)[S],
+                                           f32x4 (&zb)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float hc[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) hc[s] = h[s][c];
+    const float hv = hc[0];
+    const float s1 = fmaf(-hv, hv, 1.f);
+    const float m2h = -2.f * hv;
+    float zbv[S];
+    float sb1 = 0.f, sb2 = 0.f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) zbv[s] = s1 * hb[s][c];
+#pragma unroll
+    for (int s = 1; s < S; ++s) sb1 = fmaf(hc[s], hb[s][c], sb1);
+#pragma unroll
+    for (int s = SO; s < S; ++s) {
+      const float ha = sel_first<S, S1>(hc, sp.ia[s], sp.selA[s]), hq = sel_first<S, S1>(hc, sp.ib[s], sp.selB[s]);
+      const float hbs = hb[s][c];
+      sb2 = fmaf(ha * hq, hbs, sb2);
+      const float ga = m2h * hq * hbs, gb = m2h * ha * hbs;
+#pragma unroll
+      for (int q = 1; q < SO; ++q) zbv[q] = fmaf(sp.selA[s][q], ga, fmaf(sp.selB[s][q], gb, zbv[q]));
+    }
+    zbv[0] = fmaf(m2h, sb1, fmaf(-2.f, sb2, zbv[0]));
+#pragma unroll
+    for (int s = 0; s < S; ++s) zb[s][c] = zbv[s];
+  }
+}
+
+// Hs (saved post-activations, fp32): [layer][wg][s][wave][tile][lane][4]
+__device__ __forceinline__ size_t hs_base(int layer, int nwg, int wg, int S, int w, int WT, int lane) {
+  return ((((size_t)layer * nwg + wg) * S * 4 + w) * WT) * 256 + (unsigned)(lane * 4);
+}
+__device__ __forceinline__ int hs_off(int s, int t, int WT) { return (s * 4 * WT + t) * 256; }
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int WT, int S, int NSO, bool LAST>
+__device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)[S][WT / 2],
+                                           const bf16x8* __restrict__ Wi, const float* __restrict__ bi,
+                                           float* __restrict__ Hl, bf16x4* stage, float* hlast,
+                                           const JetSpec& sp, int l, int g) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
+  bf16x8 wh[D], wl[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    wh[k] = Wi[k * 128];
+    wl[k] = Wi[k * 128 + 64];
+  }
+  f32x4 accA[S], accB[S], biasA = zero4(), biasB = zero4();
+#pragma unroll
+  for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
+#pragma unroll
+  for (int o = 0; o <= WT; ++o) {
+    f32x4(&accC)[S] = (o & 1) ? accB : accA;
+    f32x4(&accP)[S] = (o & 1) ? accA : accB;
+    f32x4& biasC = (o & 1) ? biasB : biasA;
+    const f32x4& biasP = (o & 1) ? biasA : biasB;
+    if (o < WT) {  // MFMAs of output tile o
+      biasC = *reinterpret_cast<const f32x4*>(bi + 16 * o + 4 * g);
+#pragma unroll
+      for (int s = 0; s < S; ++s) accC[s] = zero4();
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const int st = o * KB + kb;
+        const bf16x8 Ah = wh[st % D], Al = wl[st % D];
+        if (st + D < NSTEP) {
+          wh[st % D] = Wi[(st + D) * 128];
+          wl[st % D] = Wi[(st + D) * 128 + 64];
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) accC[s] = mfma3(Ah, Al, ah[s][kb], al[s][kb], accC[s]);
+      }
+    }
+    if (o > 0) {  // epilogue of tile o-1 in the same scheduling region
+      const int t = o - 1;
+      f32x4 z[S], h[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) z[s] = accP[s];
+      z[0] += biasP;
+      tanh_jet_f<S, NSO>(sp, z, h);
+#pragma unroll
+      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(Hl + hs_off(s, t, WT)) = h[s];
+      if (LAST) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(h[s], hi, lo);
+          stage[(((s * KB + (t >> 1)) * 2 + 0) * 64 + l) * 2 + (t & 1)] = hi;
+          stage[(((s * KB + (t >> 1)) * 2 + 1) * 64 + l) * 2 + (t & 1)] = lo;
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (!LAST) {  // wave-private region: program order suffices
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        ah[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 0) * 64 + l) * 2]);
+        al[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
+      }
+  }
+}
+
+template <int WT, int S, int NSO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
+                   float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wg = blockIdx.x, nwg = gridDim.x;
+  const int n = wg * 64 + w * 16 + p;
+  const bool valid = n < N;
+  const int nc = valid ? n : N - 1;  // clamped: every load is in bounds, no exec branches
+  const int Lh = d.n_hidden;
+  // wave-private staging image of the next layer's B fragments: [s][kb][hl][lane][2 halves]
+  bf16x4* stage = reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * 2 * 64 * 2);
+  float* hlast = reinterpret_cast<float*>(stage);  // last layer: fp32 h image [s][t][lane][4]
+  const float* K0 = aux;
+  const float* b0 = aux + aux_b0(d, W);
+  const float* Ko = aux + aux_ko(d, W);
+
+  float x[TDQ_MAXD];
+#pragma unroll
+  for (int j = 0; j < TDQ_MAXD; ++j) x[j] = j < d.d_in ? X[(size_t)nc * d.d_in + j] : 0.f;
+
+  bf16x8 ah[S][KB], al[S][KB];
+
+  // ---- layer 0 (input -> width) on VALU: derivative streams are rows of K0 ----------------
+  {
+    float* H0 = Hs + hs_base(0, nwg, wg, S, w, WT, l);
+    bf16x4 ph[S], pl[S];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      const int f0 = 16 * t + 4 * g;
+      f32x4 z[S], h[S];
+      z[0] = *reinterpret_cast<const f32x4*>(b0 + f0);
+#pragma unroll
+      for (int j = 0; j < TDQ_MAXD; ++j)
+        if (j < d.d_in) z[0] += x[j] * *reinterpret_cast<const f32x4*>(K0 + j * W + f0);
+#pragma unroll
+      for (int s = 1; s < SO; ++s) z[s] = *reinterpret_cast<const f32x4*>(K0 + sp.var[s] * W + f0);
+#pragma unroll
+      for (int s = SO; s < S; ++s) z[s] = zero4();
+      tanh_jet_f<S, NSO>(sp, z, h);
+#pragma unroll
+      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(H0 + hs_off(s, t, WT)) = h[s];
+      if (Lh == 1) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(h[s], hi, lo);
+          if (t & 1) {
+            ah[s][t >> 1] = cat8(ph[s], hi);
+            al[s][t >> 1] = cat8(pl[s], lo);
+          } else {
+            ph[s] = hi;
+            pl[s] = lo;
+          }
+        }
+      }
+    }
+  }
+
+  // ---- hidden layers on bf16x3 MFMA --------------------------------------------------------
+  for (int i = 1; i < Lh - 1; ++i)
+    fwd_hidden<WT, S, NSO, false>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
+                                  Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+  if (Lh >= 2) {
+    const int i = Lh - 1;
+    fwd_hidden<WT, S, NSO, true>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
+                                 Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+  }
+
+  // ---- output layer (width -> d_out): VALU dot over the staged fp32 h + cross-lane sum ----
+  float v[S][TDQ_MAXO];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = 0.f;
+#pragma unroll
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 kq = *reinterpret_cast<const f32x4*>(Ko + (16 * t + 4 * g + c) * 4);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const float hv = hlast[((s * WT + t) * 64 + l) * 4 + c];
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = fmaf(hv, kq[q], v[s][q]);
+      }
+    }
+  const f32x4 bo = *reinterpret_cast<const f32x4*>(aux + aux_bo(d, W));
+#pragma unroll
+  for (int q = 0; q < TDQ_MAXO; ++q) {
+    if (q >= d.d_out) break;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float r = col4_sum(v[s][q]);
+      if (s == 0) r += bo[q];
+      if (g == 0 && valid) J[((size_t)s * N + n) * d.d_out + q] = r;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+template <int S, int WT>
+__device__ __forceinline__ void h_tile(f32x4 (&h)[S], const float* __restrict__ Hl, int t) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) h[s] = *reinterpret_cast<const f32x4*>(Hl + hs_off(s, t, WT));
+}
+
+template <int WT, int S, int NSO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
+                   const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
+                   int Ptot, NetDims d, JetSpec sp) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int W = 16 * WT;
+  constexpr int KB = WT / 2;
+  constexpr int NSTEP = WT * KB;
+  constexpr int D = NSTEP < 4 ? NSTEP : 4;
+  // [point][feature] bf16 images (h hi/lo, zb hi/lo).  Row stride 144 bf16 = 72 words (= 8 mod 64)
+  // and the 64-column XOR on bit 3 of the row put the 8 rows of a transposed read's 32-lane half
+  // (4 rows x 2 groups 8 rows apart, 8 words each) on 8 disjoint bank windows: conflict-free.
+  constexpr int RS = 144;
+  constexpr int IMG = 64 * RS;
+  // dK tile ownership: WT >= 4 -> wave w owns tile rows {w, w+4, ..} x all columns;
+  // WT = 2 -> one tile (w>>1, w&1) per wave
+  constexpr int NR = WT >= 4 ? WT / 4 : 1;
+  constexpr int NC = WT >= 4 ? WT : 1;
+  constexpr int U1 = (4 * IMG) / 2;           // images, in floats
+  constexpr int U2 = 4 * S * WT * 256;        // per-wave hb staging (fp32)
+  constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
+  __bf16* img = reinterpret_cast<__bf16*>(lds);
+  float* accK0 = lds + U;                     // [4][TDQ_MAXD * W]
+  float* accB = accK0 + 4 * TDQ_MAXD * W;     // [2 (layer parity)][4][W]
+  float* accKo = accB + 8 * W;                // [4][W * TDQ_MAXO]
+  float* accBo = accKo + 4 * W * TDQ_MAXO;    // [4][TDQ_MAXO]
+
+  const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wg = blockIdx.x, nwg = gridDim.x;
+  const int n = wg * 64 + w * 16 + p;
+  const bool valid = n < N;
+  const int nc = valid ? n : N - 1;
+  const float vmask = valid ? 1.f : 0.f;
+  const int Lh = d.n_hidden;
+  float* gs = slab + (size_t)wg * Ptot;
+  float* hstage = lds + (size_t)w * (S * WT * 256);
+  auto dw_row = [](int wv, int r) { return WT >= 4 ? wv + 4 * r : (wv >> 1); };
+  auto dw_col = [](int wv, int c) { return WT >= 4 ? c : (wv & 1); };
+  // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
+  const int tr_row = 8 * g + ((l & 15) >> 2), tr_col = 4 * (l & 3);
+  const int swz = (g & 1) << 6;  // bit 3 of every row this lane's transposed reads touch
+
+  // ---- output layer: hb = Ko ub ; dKo += h_last ub ; dbo += ub_value ----------------------
+  {
+    const float* Ko = aux + aux_ko(d, W);
+    const float* Hl = Hs + hs_base(Lh - 1, nwg, wg, S, w, WT, l);
+    float ub[S][TDQ_MAXO];
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q)
+#pragma unroll
+      for (int s = 0; s < S; ++s) ub[s][q] = q < d.d_out ? vmask * dJ[((size_t)s * N + nc) * d.d_out + q] : 0.f;
+    f32x4 hc[S], hn[S];
+    h_tile<S, WT>(hc, Hl, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      if (t + 1 < WT) h_tile<S, WT>(hn, Hl, t + 1);
+      f32x4 hbt[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) hbt[s] = zero4();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * t + 4 * g + c;
+        const f32x4 kq = *reinterpret_cast<const f32x4*>(Ko + f * 4);
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q) {
+          if (q >= d.d_out) break;
+          float part = 0.f;
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            hbt[s][c] = fmaf(kq[q], ub[s][q], hbt[s][c]);
+            part = fmaf(hc[s][c], ub[s][q], part);
+          }
+          part = row16_sum(part);
+          if (p == 0 && f < d.width) accKo[w * W * TDQ_MAXO + f * TDQ_MAXO + q] = part;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hstage[((s * WT + t) * 64 + l) * 4]) = hbt[s];
+      if (t + 1 < WT) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) hc[s] = hn[s];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q) {
+      if (q >= d.d_out) break;
+      const float v = row16_sum(ub[0][q]);
+      if (l == 0) accBo[w * TDQ_MAXO + q] = v;
+    }
+  }
+
+  // ---- hidden layers i = Lh-1 .. 1 ---------------------------------------------------------
+  for (int i = Lh - 1; i >= 1; --i) {
+    const float* Hi = Hs + hs_base(i, nwg, wg, S, w, WT, l);
+    const float* Hp = Hs + hs_base(i - 1, nwg, wg, S, w, WT, l);
+    // h_{i-1} tiles of stream 0 for the dK images: in flight during (a)
+    f32x4 hp[WT];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, t, WT));
+
+    // (a) stream adjoints of the pre-activation, split into B fragments; (b) bias partials
+    bf16x8 zh[S][KB], zl[S][KB];
+    float* accBi = accB + (i & 1) * 4 * W;
+    {
+      bf16x4 ph[S], pl[S];
+      f32x4 hc[S], hn[S];
+      h_tile<S, WT>(hc, Hi, 0);
+#pragma unroll
+      for (int t = 0; t < WT; ++t) {
+        if (t + 1 < WT) h_tile<S, WT>(hn, Hi, t + 1);
+        f32x4 hb[S], zb[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) hb[s] = *reinterpret_cast<const f32x4*>(&hstage[((s * WT + t) * 64 + l) * 4]);
+        tanh_jet_b<S, NSO>(sp, hc, hb, zb);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int f = 16 * t + 4 * g + c;
+          const float v = row16_sum(zb[0][c] * vmask);
+          if (p == 0 && f < d.width) accBi[w * W + f] = v;
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(zb[s] * vmask, hi, lo);
+          if (t & 1) {
+            zh[s][t >> 1] = cat8(ph[s], hi);
+            zl[s][t >> 1] = cat8(pl[s], lo);
+          } else {
+            ph[s] = hi;
+            pl[s] = lo;
+          }
+        }
+        if (t + 1 < WT) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) hc[s] = hn[s];
+        }
+      }
+    }
+
+    // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index
+    f32x4 dw[NR][NC];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dw[r][c] = zero4();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      __syncthreads();  // previous readers of the region (hb staging / last stream's images) done
+      {
+        const int row = 16 * w + p;
+        const int rsw = ((row >> 3) & 1) << 6;
+#pragma unroll
+        for (int t = 0; t < WT; ++t) {
+          bf16x4 hi, lo;
+          split4(hp[t], hi, lo);
+          const int off = row * RS + ((16 * t + 4 * g) ^ rsw);
+          *reinterpret_cast<bf16x4*>(img + off) = hi;
+          *reinterpret_cast<bf16x4*>(img + IMG + off) = lo;
+          *reinterpret_cast<bf16x4*>(img + 2 * IMG + off) = half8(zh[s][t >> 1], t & 1);
+          *reinterpret_cast<bf16x4*>(img + 3 * IMG + off) = half8(zl[s][t >> 1], t & 1);
+        }
+      }
+      if (s + 1 < S) {  // next stream's h_{i-1} tiles fly while this stream's MFMAs run
+#pragma unroll
+        for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(s + 1, t, WT));
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {  // 64 points = 2 k-blocks of 32
+        bf16x8 Ah[NR], Al[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int off = (32 * kb + tr_row) * RS + ((16 * dw_row(w, r) + tr_col) ^ swz);
+          Ah[r] = cat8(tr_read(img + off), tr_read(img + off + 4 * RS));
+          Al[r] = cat8(tr_read(img + IMG + off), tr_read(img + IMG + off + 4 * RS));
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int off = (32 * kb + tr_row) * RS + ((16 * dw_col(w, c) + tr_col) ^ swz);
+          const bf16x8 Bh = cat8(tr_read(img + 2 * IMG + off), tr_read(img + 2 * IMG + off + 4 * RS));
+          const bf16x8 Bl = cat8(tr_read(img + 3 * IMG + off), tr_read(img + 3 * IMG + off + 4 * RS));
+#pragma unroll
+          for (int r = 0; r < NR; ++r) dw[r][c] = mfma3(Ah[r], Al[r], Bh, Bl, dw[r][c]);
+        }
+      }
+    }
+    {
+      const int ko = off_layer(d, i);
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c2 = 0; c2 < NC; ++c2) {
+          const int out = 16 * dw_col(w, c2) + p;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int in = 16 * dw_row(w, r) + 4 * g + c;
+            if (in < d.width && out < d.width) gs[ko + in * d.width + out] = dw[r][c2][c];
+          }
+        }
+    }
+    __syncthreads();  // images consumed: the region becomes hb staging again
+
+    // (d) hb_{i-1} = K_i zb on bf16x3 MFMA (A = [in][out] image, B = zb fragments)
+    {
+      const bf16x8* Ki = Kimg + (size_t)(i - 1) * NSTEP * 128 + l;
+      bf16x8 wh[D], wl[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        wh[k] = Ki[k * 128];
+        wl[k] = Ki[k * 128 + 64];
+      }
+#pragma unroll
+      for (int o = 0; o < WT; ++o) {
+        f32x4 acc[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) acc[s] = zero4();
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          const int st = o * KB + kb;
+          const bf16x8 Ah = wh[st % D], Al = wl[st % D];
+          if (st + D < NSTEP) {
+            wh[st % D] = Ki[(st + D) * 128];
+            wl[st % D] = Ki[(st + D) * 128 + 64];
+          }
+#pragma unroll
+          for (int s = 0; s < S; ++s) acc[s] = mfma3(Ah, Al, zh[s][kb], zl[s][kb], acc[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hstage[((s * WT + o) * 64 + l) * 4]) = acc[s];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();  // bias partials of all waves are in LDS
+    if (w == 0) {
+      const int bo = off_layer(d, i) + d.width * d.width;
+      for (int f = l; f < d.width; f += 64)
+        gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
+    }
+  }
+
+  // ---- first layer (i = 0): bias + dK0[j][f] = sum_p x_j zb + sum_{first-order on var j} zb_s
+  {
+    constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+    float* accBi = accB;
+    const float* H0 = Hs + hs_base(0, nwg, wg, S, w, WT, l);
+    float x[TDQ_MAXD];
+#pragma unroll
+    for (int j = 0; j < TDQ_MAXD; ++j) x[j] = j < d.d_in ? vmask * X[(size_t)nc * d.d_in + j] : 0.f;
+    f32x4 zb0[S][WT];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      f32x4 h[S], hb[S], zb[S];
+      h_tile<S, WT>(h, H0, t);
+#pragma unroll
+      for (int s = 0; s < S; ++s) hb[s] = *reinterpret_cast<const f32x4*>(&hstage[((s * WT + t) * 64 + l) * 4]);
+      tanh_jet_b<S, NSO>(sp, h, hb, zb);
+#pragma unroll
+      for (int s = 0; s < S; ++s) zb0[s][t] = zb[s] * vmask;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * t + 4 * g + c;
+        const float v = row16_sum(zb0[0][t][c]);
+        if (p == 0 && f < d.width) accBi[w * W + f] = v;
+      }
+    }
+    for (int j = 0; j < d.d_in; ++j) {
+      float xj = 0.f;
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXD; ++q) xj = (q == j) ? x[q] : xj;
+#pragma unroll
+      for (int t = 0; t < WT; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int f = 16 * t + 4 * g + c;
+          float v = xj * zb0[0][t][c];
+#pragma unroll
+          for (int s = 1; s < SO; ++s) v += (sp.var[s] == j) ? zb0[s][t][c] : 0.f;
+          v = row16_sum(v);
+          if (p == 0 && f < d.width) accK0[w * TDQ_MAXD * W + j * W + f] = v;
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+      const int bo = d.d_in * d.width;
+      for (int f = l; f < d.width; f += 64)
+        gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
+    } else if (w == 1) {
+      for (int e = l; e < d.d_in * d.width; e += 64) {
+        const int j = e / d.width, f = e - j * d.width;
+        const int k = j * W + f;
+        gs[e] = ((accK0[k] + accK0[TDQ_MAXD * W + k]) + accK0[2 * TDQ_MAXD * W + k]) + accK0[3 * TDQ_MAXD * W + k];
+      }
+    } else if (w == 2) {
+      const int ko = off_layer(d, Lh);
+      for (int e = l; e < d.width * d.d_out; e += 64) {
+        const int f = e / d.d_out, q = e - f * d.d_out;
+        const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
+        gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
+      }
+      if (l < d.d_out)
+        gs[ko + d.width * d.d_out + l] =
+            ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launch templates (instantiated per width class in jet_bf3_w{2,4,8}.hip)
+// ------------------------------------------------------------------------------------------
+inline size_t fwd_bf3_lds(int WT, int S) { return (size_t)4 * S * WT * 1024; }
+
+inline size_t bwd_bf3_lds(int WT, int S) {
+  const int W = 16 * WT;
+  const size_t u1 = (size_t)(4 * 64 * 144) / 2, u2 = (size_t)4 * S * WT * 256;
+  const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
+  return (u + 4 * TDQ_MAXD * W + 8 * W + 4 * W * TDQ_MAXO + 4 * TDQ_MAXO) * sizeof(float);
+}
+
+struct Bf3Args {
+  const float* X;
+  const float* aux;
+  const bf16x8* img;
+  const float* dJ;   // bwd
+  float* J;          // fwd
+  float* Hs;
+  float* slab;       // bwd
+  int N, Ptot;
+  NetDims d;
+  JetSpec sp;
+  hipStream_t st;
+};
+
+template <int WT, int S, int NSO>
+int launch_fwd_bf3(const Bf3Args& a) {
+  const int nwg = (a.N + 63) / 64;
+  const size_t lds = fwd_bf3_lds(WT, S);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_fwd_bf3_kernel<WT, S, NSO>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
+                     a.Hs, a.N, a.d, a.sp);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int WT, int S, int NSO>
+int launch_bwd_bf3(const Bf3Args& a) {
+  const int nwg = (a.N + 63) / 64;
+  const size_t lds = bwd_bf3_lds(WT, S);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_bwd_bf3_kernel<WT, S, NSO>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// per-width-class entry points (jet_bf3_w{2,4,8}.hip); return hipErrorInvalidValue when
+// (S, NSO) has no instantiation
+int bf3_fwd_w2(int S, int nso, const Bf3Args& a);
+int bf3_fwd_w4(int S, int nso, const Bf3Args& a);
+int bf3_fwd_w8(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w2(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w4(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w8(int S, int nso, const Bf3Args& a);

@@ -66,4 +66,18 @@ static inline bool make_spec(int S, const int* spec, JetSpec& sp) {
   return true;
 }
 
+// number of second-order streams when the plan is in canonical order (value, first-order
+// streams, second-order streams - JetPlan always emits this order); -1 otherwise
+static inline int spec_nso(int S, const int* spec) {
+  int nso = 0, prev = 0;
+  for (int s = 0; s < S; ++s) {
+    const int ty = spec[3 * s];
+    if (ty < prev || (s == 0) != (ty == 0)) return -1;
+    prev = ty;
+    nso += ty == 2;
+  }
+  if (nso > 0 && S - 1 - nso < 1) return -1;
+  return nso;
+}
+
 extern "C" int tdq_slab_reduce(float* work, float* grad, int nwg, int Ptot, int chunks, void* stream);

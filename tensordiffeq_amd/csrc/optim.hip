@@ -95,7 +95,7 @@ __global__ void best_scalar_kernel(const float* __restrict__ loss, float* __rest
 
 extern "C" {
 
-int tdq_abi_version() { return 4; }
+int tdq_abi_version() { return 5; }
 
 int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, float b1, float b2,
                    float eps, void* stream) {

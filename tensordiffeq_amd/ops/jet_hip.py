@@ -32,7 +32,7 @@ def stream_spec(plan):
 def _fns(lib, cfg):
     if cfg["precision"] == "bf16x3":
         return (lib.tdq_jet_fwd_bf3, lib.tdq_jet_bwd_bf3,
-                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["width"], cfg["n_hidden"], cfg["S"]),
+                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["d_in"], cfg["width"], cfg["n_hidden"], cfg["S"]),
                 lambda N: lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
     return (lib.tdq_jet_fwd, lib.tdq_jet_bwd,
             lambda N: lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], cfg["S"], 0),
