@@ -1,0 +1,60 @@
+"""Allen-Cahn baseline PINN (no self-adaptive weights).
+
+Same PDE / IC as AC-SA.py; the periodic BC is enforced on u, u_x, u_xxx and u_xxxx (3rd/4th-order
+derivatives run through the general Taylor-jet engine on the 201 boundary points).  Reference:
+examples/AC-baseline.py (Adam 10k + L-BFGS 10k).
+"""
+import math
+
+import numpy as np
+import torch
+
+from _common import ac_data, l2_on_data_grid, parser, report, solver_kw
+
+import tensordiffeq_amd as tdq
+from tensordiffeq_amd.boundaries import IC, DomainND, periodicBC
+
+
+def main(argv=None):
+    args = parser(__doc__.splitlines()[0], iters=10000, newton=10000).parse_args(argv)
+    tdq.set_seed(args.seed)
+    Domain = DomainND(["x", "t"], time_var="t")
+    Domain.add("x", [-1.0, 1.0], 512)
+    Domain.add("t", [0.0, 1.0], 201)
+    Domain.generate_collocation_points(args.n_f or 50000)
+
+    def func_ic(x):
+        return x ** 2 * np.cos(math.pi * x)
+
+    def deriv_model(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        u_x = tdq.grad(u, x)
+        u_xx = tdq.grad(u_x, x)
+        u_xxx = tdq.grad(u_xx, x)
+        u_xxxx = tdq.grad(u_xxx, x)
+        return u, u_x, u_xxx, u_xxxx
+
+    def f_model(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        u_x = tdq.grad(u, x)
+        u_xx = tdq.grad(u_x, x)
+        u_t = tdq.grad(u, t)
+        c1 = tdq.utils.constant(.0001)
+        c2 = tdq.utils.constant(5.0)
+        return u_t - c1 * u_xx + c2 * u * u * u - c2 * u
+
+    BCs = [IC(Domain, [func_ic], var=[["x"]]), periodicBC(Domain, ["x"], [deriv_model])]
+    model = tdq.CollocationSolverND(verbose=not args.quiet)
+    model.compile([2, 128, 128, 128, 128, 1], f_model, Domain, BCs, **solver_kw(args))
+    model.fit(tf_iter=args.iters, newton_iter=args.newton)
+    x, t, U = ac_data()
+    err, *_ = l2_on_data_grid(model, x, t, U)
+    res = report("AC-baseline", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"])}, args.quiet)
+    if args.plot:
+        tdq.plotting.plot_solution_domain1D(model, [x, t], ub=np.array([1.0, 1.0]), lb=np.array([-1.0, 0.0]),
+                                            Exact_u=U)
+    return res
+
+
+if __name__ == "__main__":
+    main()

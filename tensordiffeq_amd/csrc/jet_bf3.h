@@ -45,6 +45,21 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+// Optional per-phase timestamps (build with -DTDQ_PHASE_TIMING, tools/phase_timing.py): lane 0
+// of every wave stores s_memtime at numbered points into tdq_ts[(wg * 4 + wave) * 64 + k].
+#ifdef TDQ_PHASE_TIMING
+static __device__ unsigned long long* tdq_ts;  // per translation unit (no -fgpu-rdc)
+#define TDQ_TS(k)                                                                                 \
+  do {                                                                                            \
+    if ((threadIdx.x & 63) == 0)                                                                  \
+      tdq_ts[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TDQ_TS(k) \
+  do {            \
+  } while (0)
+#endif
+
 // aux image (fp32, zero padded to W = 16 WT features; TDQ_MAXO output columns):
 //   K0 [d_in][W] | b0 [W] | b_1..b_{Lh-1} [Lh-1][W] | Ko [W][4] | bo [4]
 __host__ __device__ inline int aux_b0(const NetDims& d, int W) { return d.d_in * W; }
@@ -174,8 +189,16 @@ __device__ __forceinline__ void tanh_jet_b(const JetSpec& sp, const f32x4 (&h)[S
       const float hbs = hb[s][c];
       sb2 = fmaf(ha * hq, hbs, sb2);
       const float ga = m2h * hq * hbs, gb = m2h * ha * hbs;
+      if constexpr (S1 <= 2) {
 #pragma unroll
-      for (int q = 1; q < SO; ++q) zbv[q] = fmaf(sp.selA[s][q], ga, fmaf(sp.selB[s][q], gb, zbv[q]));
+        for (int q = 1; q < SO; ++q) {
+          zbv[q] += (sp.ia[s] == q) ? ga : 0.f;
+          zbv[q] += (sp.ib[s] == q) ? gb : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 1; q < SO; ++q) zbv[q] = fmaf(sp.selA[s][q], ga, fmaf(sp.selB[s][q], gb, zbv[q]));
+      }
     }
     zbv[0] = fmaf(m2h, sb1, fmaf(-2.f, sb2, zbv[0]));
 #pragma unroll
@@ -285,6 +308,7 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const float* b0 = aux + aux_b0(d, W);
   const float* Ko = aux + aux_ko(d, W);
 
+  TDQ_TS(0);
   float x[TDQ_MAXD];
 #pragma unroll
   for (int j = 0; j < TDQ_MAXD; ++j) x[j] = j < d.d_in ? X[(size_t)nc * d.d_in + j] : 0.f;
@@ -330,14 +354,18 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     }
   }
 
+  TDQ_TS(1);
   // ---- hidden layers on bf16x3 MFMA --------------------------------------------------------
-  for (int i = 1; i < Lh - 1; ++i)
+  for (int i = 1; i < Lh - 1; ++i) {
     fwd_hidden<WT, S, NSO, false>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
                                   Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+    TDQ_TS(1 + i);
+  }
   if (Lh >= 2) {
     const int i = Lh - 1;
     fwd_hidden<WT, S, NSO, true>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
                                  Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+    TDQ_TS(1 + i);
   }
 
   // ---- output layer (width -> d_out): VALU dot over the staged fp32 h + cross-lane sum ----
@@ -369,6 +397,7 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       if (g == 0 && valid) J[((size_t)s * N + n) * d.d_out + q] = r;
     }
   }
+  TDQ_TS(15);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -380,6 +409,109 @@ __device__ __forceinline__ void h_tile(f32x4 (&h)[S], const float* __restrict__ 
   for (int s = 0; s < S; ++s) h[s] = *reinterpret_cast<const f32x4*>(Hl + hs_off(s, t, WT));
 }
 
+// first-layer partials from zb_0 (fp32) of one feature tile: bias b0 and dK0[j][f] (one LDS slot
+// per wave, summed in fixed wave order later)
+template <int WT, int S, int NSO>
+__device__ __forceinline__ void first_layer_partials(const JetSpec& sp, const f32x4 (&zb)[S],
+                                                     const float* __restrict__ xrow, const NetDims& d, int t,
+                                                     int w, int p, int g, float* accB0, float* accK0) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  const int fo = 16 * t + 4 * g + (p >> 2);  // feature this lane stores after row16_sum4
+  {
+    const float r = row16_sum4(zb[0]);
+    if ((p & 3) == 0) accB0[w * W + fo] = r;
+  }
+  for (int j = 0; j < d.d_in; ++j) {
+    const float xj = xrow[j];
+    f32x4 v;  // scalar per component: packed f32 VALU beside MFMAs costs issue cycles
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float a = xj * zb[0][c];
+#pragma unroll
+      for (int s = 1; s < SO; ++s) a += (sp.var[s] == j) ? zb[s][c] : 0.f;
+      v[c] = a;
+    }
+    const float r = row16_sum4(v);
+    if ((p & 3) == 0) accK0[w * TDQ_MAXD * W + j * W + fo] = r;
+  }
+}
+
+// zb of one feature tile -> bias partial of its layer + hi/lo halves into the wave's fragment
+// stage ([s][kb][hl][lane][2 halves] bf16x4, the forward's staging layout)
+template <int WT, int S>
+__device__ __forceinline__ void zb_to_stage(const f32x4 (&zb)[S], const NetDims& d, int t, int w, int l, int p,
+                                            int g, float* accBslot, bf16x4* stage) {
+  constexpr int KB = WT / 2, W = 16 * WT;
+  {
+    const float r = row16_sum4(zb[0]);
+    if ((p & 3) == 0) accBslot[w * W + 16 * t + 4 * g + (p >> 2)] = r;
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    bf16x4 hi, lo;
+    split4(zb[s], hi, lo);
+    stage[(((s * KB + (t >> 1)) * 2 + 0) * 64 + l) * 2 + (t & 1)] = hi;
+    stage[(((s * KB + (t >> 1)) * 2 + 1) * 64 + l) * 2 + (t & 1)] = lo;
+  }
+}
+
+// (d) of hidden layer i: hb_{i-1} = K_i zb_i on bf16x3 MFMA; the epilogue of output tile o-1
+// (tanh-jet adjoint with the saved h_{i-1}, bias partials, split + stage - or, when i = 1, the
+// first-layer partials) runs in the scheduling region of tile o's MFMAs.
+template <int WT, int S, int NSO, bool TO_FIRST>
+__device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], const bf16x8 (&zl)[S][WT / 2],
+                                             const bf16x8* __restrict__ Ki, const float* __restrict__ Hp,
+                                             bf16x4* stage, float* accBslot, float* accK0,
+                                             const float* __restrict__ xrow, const JetSpec& sp, const NetDims& d,
+                                             int w, int l, int p, int g) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
+  bf16x8 wh[D], wl[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    wh[k] = Ki[k * 128];
+    wl[k] = Ki[k * 128 + 64];
+  }
+  f32x4 hr[2][S];
+  h_tile<S, WT>(hr[0], Hp, 0);
+  if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
+  f32x4 accA[S], accB[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
+#pragma unroll
+  for (int o = 0; o <= WT; ++o) {
+    f32x4(&accC)[S] = (o & 1) ? accB : accA;
+    f32x4(&accP)[S] = (o & 1) ? accA : accB;
+    if (o < WT) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) accC[s] = zero4();
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const int st = o * KB + kb;
+        const bf16x8 Ah = wh[st % D], Al = wl[st % D];
+        if (st + D < NSTEP) {
+          wh[st % D] = Ki[(st + D) * 128];
+          wl[st % D] = Ki[(st + D) * 128 + 64];
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) accC[s] = mfma3(Ah, Al, zh[s][kb], zl[s][kb], accC[s]);
+      }
+    }
+    if (o > 0) {
+      const int t = o - 1;
+      f32x4 h[S], zb[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) h[s] = hr[t & 1][s];
+      if (t + 2 < WT) h_tile<S, WT>(hr[t & 1], Hp, t + 2);
+      tanh_jet_b<S, NSO>(sp, h, accP, zb);
+      if (TO_FIRST)
+        first_layer_partials<WT, S, NSO>(sp, zb, xrow, d, t, w, p, g, accBslot, accK0);
+      else
+        zb_to_stage<WT, S>(zb, d, t, w, l, p, g, accBslot, stage);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int WT, int S, int NSO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
@@ -388,8 +520,6 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int W = 16 * WT;
   constexpr int KB = WT / 2;
-  constexpr int NSTEP = WT * KB;
-  constexpr int D = NSTEP < 4 ? NSTEP : 4;
   // [point][feature] bf16 images (h hi/lo, zb hi/lo).  Row stride 144 bf16 = 72 words (= 8 mod 64)
   // and the 64-column XOR on bit 3 of the row put the 8 rows of a transposed read's 32-lane half
   // (4 rows x 2 groups 8 rows apart, 8 words each) on 8 disjoint bank windows: conflict-free.
@@ -400,12 +530,12 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   constexpr int NR = WT >= 4 ? WT / 4 : 1;
   constexpr int NC = WT >= 4 ? WT : 1;
   constexpr int U1 = (4 * IMG) / 2;           // images, in floats
-  constexpr int U2 = 4 * S * WT * 256;        // per-wave hb staging (fp32)
+  constexpr int U2 = 4 * S * WT * 256;        // per-wave zb fragment stage (bf16 hi/lo)
   constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
   __bf16* img = reinterpret_cast<__bf16*>(lds);
   float* accK0 = lds + U;                     // [4][TDQ_MAXD * W]
-  float* accB = accK0 + 4 * TDQ_MAXD * W;     // [2 (layer parity)][4][W]
-  float* accKo = accB + 8 * W;                // [4][W * TDQ_MAXO]
+  float* accB = accK0 + 4 * TDQ_MAXD * W;     // [3: layer parity 0/1, layer 0][4][W]
+  float* accKo = accB + 12 * W;               // [4][W * TDQ_MAXO]
   float* accBo = accKo + 4 * W * TDQ_MAXO;    // [4][TDQ_MAXO]
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
@@ -414,55 +544,91 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const int n = wg * 64 + w * 16 + p;
   const bool valid = n < N;
   const int nc = valid ? n : N - 1;
-  const float vmask = valid ? 1.f : 0.f;
+  const float vmask = valid ? 1.f : 0.f;  // zero adjoints for padding points: zb = 0 downstream
   const int Lh = d.n_hidden;
   float* gs = slab + (size_t)wg * Ptot;
-  float* hstage = lds + (size_t)w * (S * WT * 256);
+  bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * 2 * 64 * 2);
   auto dw_row = [](int wv, int r) { return WT >= 4 ? wv + 4 * r : (wv >> 1); };
   auto dw_col = [](int wv, int c) { return WT >= 4 ? c : (wv & 1); };
   // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
   const int tr_row = 8 * g + ((l & 15) >> 2), tr_col = 4 * (l & 3);
   const int swz = (g & 1) << 6;  // bit 3 of every row this lane's transposed reads touch
+  const float* xrow = X + (size_t)nc * d.d_in;  // padding points: zb = 0, x is irrelevant
+  TDQ_TS(0);
 
-  // ---- output layer: hb = Ko ub ; dKo += h_last ub ; dbo += ub_value ----------------------
+  bf16x8 zh[S][KB], zl[S][KB];
+
+  // ---- output layer: hb = Ko ub ; dKo += h_last ub ; dbo += ub ; then the top tanh layer's
+  //      adjoint zb_{Lh-1} tile by tile (bias partials + B fragments, or first-layer partials)
   {
     const float* Ko = aux + aux_ko(d, W);
     const float* Hl = Hs + hs_base(Lh - 1, nwg, wg, S, w, WT, l);
+    float* accBslot = Lh >= 2 ? accB + ((Lh - 1) & 1) * 4 * W : accB + 8 * W;
     float ub[S][TDQ_MAXO];
 #pragma unroll
     for (int q = 0; q < TDQ_MAXO; ++q)
 #pragma unroll
       for (int s = 0; s < S; ++s) ub[s][q] = q < d.d_out ? vmask * dJ[((size_t)s * N + nc) * d.d_out + q] : 0.f;
-    f32x4 hc[S], hn[S];
-    h_tile<S, WT>(hc, Hl, 0);
+    constexpr int DH = WT < 3 ? WT : 3;  // H tiles in flight
+    f32x4 hr[DH][S];
+#pragma unroll
+    for (int k = 0; k < DH; ++k) h_tile<S, WT>(hr[k], Hl, k);
+    bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
-      if (t + 1 < WT) h_tile<S, WT>(hn, Hl, t + 1);
+      f32x4 h[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) h[s] = hr[t % DH][s];
+      if (t + DH < WT) h_tile<S, WT>(hr[t % DH], Hl, t + DH);
+      // hb = Ko ub over the zero-padded 4 output columns: no branches
       f32x4 hbt[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) hbt[s] = zero4();
+      f32x4 kq[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int f = 16 * t + 4 * g + c;
-        const f32x4 kq = *reinterpret_cast<const f32x4*>(Ko + f * 4);
+      for (int c = 0; c < 4; ++c) kq[c] = *reinterpret_cast<const f32x4*>(Ko + (16 * t + 4 * g + c) * 4);
 #pragma unroll
-        for (int q = 0; q < TDQ_MAXO; ++q) {
-          if (q >= d.d_out) break;
-          float part = 0.f;
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            hbt[s][c] = fmaf(kq[q], ub[s][q], hbt[s][c]);
-            part = fmaf(hc[s][c], ub[s][q], part);
-          }
-          part = row16_sum(part);
-          if (p == 0 && f < d.width) accKo[w * W * TDQ_MAXO + f * TDQ_MAXO + q] = part;
+        for (int q = 0; q < TDQ_MAXO; ++q)
+#pragma unroll
+          for (int s = 0; s < S; ++s) hbt[s][c] = fmaf(kq[c][q], ub[s][q], hbt[s][c]);
+      // dKo[f][q] partials: sum over points of sum_s h_s ub_s
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) {
+        if (q >= d.d_out) break;
+        f32x4 part;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float a = 0.f;
+#pragma unroll
+          for (int s = 0; s < S; ++s) a = fmaf(ub[s][q], h[s][c], a);
+          part[c] = a;
         }
+        const float r = row16_sum4(part);
+        if ((p & 3) == 0) accKo[w * W * TDQ_MAXO + (16 * t + 4 * g + (p >> 2)) * TDQ_MAXO + q] = r;
       }
+      f32x4 zb[S];
+      tanh_jet_b<S, NSO>(sp, h, hbt, zb);
+      if (Lh >= 2) {
+        {
+          const float r = row16_sum4(zb[0]);
+          if ((p & 3) == 0) accBslot[w * W + 16 * t + 4 * g + (p >> 2)] = r;
+        }
 #pragma unroll
-      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hstage[((s * WT + t) * 64 + l) * 4]) = hbt[s];
-      if (t + 1 < WT) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) hc[s] = hn[s];
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(zb[s], hi, lo);
+          if (t & 1) {
+            zh[s][t >> 1] = cat8(ph[s], hi);
+            zl[s][t >> 1] = cat8(pl[s], lo);
+          } else {
+            ph[s] = hi;
+            pl[s] = lo;
+          }
+        }
+      } else {
+        first_layer_partials<WT, S, NSO>(sp, zb, xrow, d, t, w, p, g, accBslot, accK0);
       }
     }
 #pragma unroll
@@ -472,54 +638,17 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       if (l == 0) accBo[w * TDQ_MAXO + q] = v;
     }
   }
+  TDQ_TS(1);
 
-  // ---- hidden layers i = Lh-1 .. 1 ---------------------------------------------------------
+  // ---- hidden layers i = Lh-1 .. 1: zh/zl hold zb_i --------------------------------------
   for (int i = Lh - 1; i >= 1; --i) {
-    const float* Hi = Hs + hs_base(i, nwg, wg, S, w, WT, l);
+    const int tsb = 2 + 8 * (Lh - 1 - i);
     const float* Hp = Hs + hs_base(i - 1, nwg, wg, S, w, WT, l);
-    // h_{i-1} tiles of stream 0 for the dK images: in flight during (a)
+    // h_{i-1} tiles of stream 0 for the dK images
     f32x4 hp[WT];
 #pragma unroll
     for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, t, WT));
-
-    // (a) stream adjoints of the pre-activation, split into B fragments; (b) bias partials
-    bf16x8 zh[S][KB], zl[S][KB];
-    float* accBi = accB + (i & 1) * 4 * W;
-    {
-      bf16x4 ph[S], pl[S];
-      f32x4 hc[S], hn[S];
-      h_tile<S, WT>(hc, Hi, 0);
-#pragma unroll
-      for (int t = 0; t < WT; ++t) {
-        if (t + 1 < WT) h_tile<S, WT>(hn, Hi, t + 1);
-        f32x4 hb[S], zb[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) hb[s] = *reinterpret_cast<const f32x4*>(&hstage[((s * WT + t) * 64 + l) * 4]);
-        tanh_jet_b<S, NSO>(sp, hc, hb, zb);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int f = 16 * t + 4 * g + c;
-          const float v = row16_sum(zb[0][c] * vmask);
-          if (p == 0 && f < d.width) accBi[w * W + f] = v;
-        }
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          bf16x4 hi, lo;
-          split4(zb[s] * vmask, hi, lo);
-          if (t & 1) {
-            zh[s][t >> 1] = cat8(ph[s], hi);
-            zl[s][t >> 1] = cat8(pl[s], lo);
-          } else {
-            ph[s] = hi;
-            pl[s] = lo;
-          }
-        }
-        if (t + 1 < WT) {
-#pragma unroll
-          for (int s = 0; s < S; ++s) hc[s] = hn[s];
-        }
-      }
-    }
+    TDQ_TS(tsb);
 
     // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index
     f32x4 dw[NR][NC];
@@ -529,7 +658,13 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       for (int c = 0; c < NC; ++c) dw[r][c] = zero4();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      __syncthreads();  // previous readers of the region (hb staging / last stream's images) done
+      __syncthreads();  // previous readers of the region (zb stage / last stream's images) done
+      if (s == 0 && w == 0) {  // bias of layer i: partials of all waves landed before this barrier
+        const float* accBi = accB + (i & 1) * 4 * W;
+        const int bo = off_layer(d, i) + d.width * d.width;
+        for (int f = l; f < d.width; f += 64)
+          gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
+      }
       {
         const int row = 16 * w + p;
         const int rsw = ((row >> 3) & 1) << 6;
@@ -549,6 +684,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
         for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(s + 1, t, WT));
       }
       __syncthreads();
+      if (s == 0) TDQ_TS(tsb + 1);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {  // 64 points = 2 k-blocks of 32
         bf16x8 Ah[NR], Al[NR];
@@ -582,110 +718,53 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
           }
         }
     }
-    __syncthreads();  // images consumed: the region becomes hb staging again
+    TDQ_TS(tsb + 2);
+    __syncthreads();  // images consumed: the region becomes the zb fragment stage
+    TDQ_TS(tsb + 3);
 
-    // (d) hb_{i-1} = K_i zb on bf16x3 MFMA (A = [in][out] image, B = zb fragments)
-    {
-      const bf16x8* Ki = Kimg + (size_t)(i - 1) * NSTEP * 128 + l;
-      bf16x8 wh[D], wl[D];
+    // (d) hb_{i-1} = K_i zb_i, fused with the adjoint of tanh layer i-1
+    const bf16x8* Ki = Kimg + (size_t)(i - 1) * (WT * KB) * 128 + l;
+    if (i >= 2) {
+      bwd_hidden_d<WT, S, NSO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, w, l,
+                                      p, g);
 #pragma unroll
-      for (int k = 0; k < D; ++k) {
-        wh[k] = Ki[k * 128];
-        wl[k] = Ki[k * 128 + 64];
-      }
+      for (int s = 0; s < S; ++s)
 #pragma unroll
-      for (int o = 0; o < WT; ++o) {
-        f32x4 acc[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) acc[s] = zero4();
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          const int st = o * KB + kb;
-          const bf16x8 Ah = wh[st % D], Al = wl[st % D];
-          if (st + D < NSTEP) {
-            wh[st % D] = Ki[(st + D) * 128];
-            wl[st % D] = Ki[(st + D) * 128 + 64];
-          }
-#pragma unroll
-          for (int s = 0; s < S; ++s) acc[s] = mfma3(Ah, Al, zh[s][kb], zl[s][kb], acc[s]);
+        for (int kb = 0; kb < KB; ++kb) {  // wave-private stage: program order suffices
+          zh[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 0) * 64 + l) * 2]);
+          zl[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
         }
-#pragma unroll
-        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hstage[((s * WT + o) * 64 + l) * 4]) = acc[s];
-        __builtin_amdgcn_sched_barrier(0);
-      }
+    } else {
+      bwd_hidden_d<WT, S, NSO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, w, l, p, g);
     }
-    __syncthreads();  // bias partials of all waves are in LDS
-    if (w == 0) {
-      const int bo = off_layer(d, i) + d.width * d.width;
-      for (int f = l; f < d.width; f += 64)
-        gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
-    }
+    TDQ_TS(tsb + 4);
   }
 
-  // ---- first layer (i = 0): bias + dK0[j][f] = sum_p x_j zb + sum_{first-order on var j} zb_s
-  {
-    constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
-    float* accBi = accB;
-    const float* H0 = Hs + hs_base(0, nwg, wg, S, w, WT, l);
-    float x[TDQ_MAXD];
-#pragma unroll
-    for (int j = 0; j < TDQ_MAXD; ++j) x[j] = j < d.d_in ? vmask * X[(size_t)nc * d.d_in + j] : 0.f;
-    f32x4 zb0[S][WT];
-#pragma unroll
-    for (int t = 0; t < WT; ++t) {
-      f32x4 h[S], hb[S], zb[S];
-      h_tile<S, WT>(h, H0, t);
-#pragma unroll
-      for (int s = 0; s < S; ++s) hb[s] = *reinterpret_cast<const f32x4*>(&hstage[((s * WT + t) * 64 + l) * 4]);
-      tanh_jet_b<S, NSO>(sp, h, hb, zb);
-#pragma unroll
-      for (int s = 0; s < S; ++s) zb0[s][t] = zb[s] * vmask;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int f = 16 * t + 4 * g + c;
-        const float v = row16_sum(zb0[0][t][c]);
-        if (p == 0 && f < d.width) accBi[w * W + f] = v;
-      }
+  // ---- first-layer / output-layer slabs (partials of all waves are in LDS) ----------------
+  __syncthreads();
+  if (w == 0) {
+    const float* accB0 = accB + 8 * W;
+    const int bo = d.d_in * d.width;
+    for (int f = l; f < d.width; f += 64)
+      gs[bo + f] = ((accB0[f] + accB0[W + f]) + accB0[2 * W + f]) + accB0[3 * W + f];
+  } else if (w == 1) {
+    for (int e = l; e < d.d_in * d.width; e += 64) {
+      const int j = e / d.width, f = e - j * d.width;
+      const int k = j * W + f;
+      gs[e] = ((accK0[k] + accK0[TDQ_MAXD * W + k]) + accK0[2 * TDQ_MAXD * W + k]) + accK0[3 * TDQ_MAXD * W + k];
     }
-    for (int j = 0; j < d.d_in; ++j) {
-      float xj = 0.f;
-#pragma unroll
-      for (int q = 0; q < TDQ_MAXD; ++q) xj = (q == j) ? x[q] : xj;
-#pragma unroll
-      for (int t = 0; t < WT; ++t)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int f = 16 * t + 4 * g + c;
-          float v = xj * zb0[0][t][c];
-#pragma unroll
-          for (int s = 1; s < SO; ++s) v += (sp.var[s] == j) ? zb0[s][t][c] : 0.f;
-          v = row16_sum(v);
-          if (p == 0 && f < d.width) accK0[w * TDQ_MAXD * W + j * W + f] = v;
-        }
+  } else if (w == 2) {
+    const int ko = off_layer(d, Lh);
+    for (int e = l; e < d.width * d.d_out; e += 64) {
+      const int f = e / d.d_out, q = e - f * d.d_out;
+      const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
+      gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
     }
-    __syncthreads();
-    if (w == 0) {
-      const int bo = d.d_in * d.width;
-      for (int f = l; f < d.width; f += 64)
-        gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
-    } else if (w == 1) {
-      for (int e = l; e < d.d_in * d.width; e += 64) {
-        const int j = e / d.width, f = e - j * d.width;
-        const int k = j * W + f;
-        gs[e] = ((accK0[k] + accK0[TDQ_MAXD * W + k]) + accK0[2 * TDQ_MAXD * W + k]) + accK0[3 * TDQ_MAXD * W + k];
-      }
-    } else if (w == 2) {
-      const int ko = off_layer(d, Lh);
-      for (int e = l; e < d.width * d.d_out; e += 64) {
-        const int f = e / d.d_out, q = e - f * d.d_out;
-        const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
-        gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
-      }
-      if (l < d.d_out)
-        gs[ko + d.width * d.d_out + l] =
-            ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
-    }
+    if (l < d.d_out)
+      gs[ko + d.width * d.d_out + l] =
+          ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
   }
+  TDQ_TS(63);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -697,7 +776,7 @@ inline size_t bwd_bf3_lds(int WT, int S) {
   const int W = 16 * WT;
   const size_t u1 = (size_t)(4 * 64 * 144) / 2, u2 = (size_t)4 * S * WT * 256;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
-  return (u + 4 * TDQ_MAXD * W + 8 * W + 4 * W * TDQ_MAXO + 4 * TDQ_MAXO) * sizeof(float);
+  return (u + 4 * TDQ_MAXD * W + 12 * W + 4 * W * TDQ_MAXO + 4 * TDQ_MAXO) * sizeof(float);
 }
 
 struct Bf3Args {

@@ -2,6 +2,12 @@
 // Generated case list: every (S, NSO) with S <= 4, NSO <= S - 2 (or S = 1).
 #include "jet_bf3.h"
 
+#ifdef TDQ_PHASE_TIMING
+extern "C" int tdq_set_timing_buffer(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(tdq_ts), &p, sizeof(p));
+}
+#endif
+
 int bf3_fwd_w8(int S, int nso, const Bf3Args& a) {
   switch (S * 16 + nso) {
     case 16: return launch_fwd_bf3<8, 1, 0>(a);

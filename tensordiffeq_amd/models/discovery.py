@@ -165,7 +165,7 @@ class DiscoveryModel:
 
         def progress(done, loss):
             bar.n = done
-            vals = [float(v) for v in self.vars]
+            vals = [float(v.detach()) for v in self.vars]
             self.var_history.append((done, vals))
             if loss is not None:
                 bar.set_postfix(loss=loss, vars=vals)
