@@ -22,10 +22,14 @@ networks = models.networks
 
 __version__ = "0.2.0"
 
+from . import config, metrics  # noqa: E402
+from .config import SolverConfig  # noqa: E402
+
 __all__ = ["models", "networks", "plotting", "utils", "helpers", "optimizers", "boundaries",
            "domains", "fit", "sampling", "parallel", "ops", "checkpoint", "jet", "autodiff",
            "grad", "gradients", "DomainND", "dirichletBC", "FunctionDirichletBC",
            "FunctionNeumannBC", "IC", "periodicBC", "CollocationSolverND", "DiscoveryModel",
            "TanhMLP", "neural_net", "Variable", "constant", "tensor", "convertTensor",
            "LatinHypercubeSample", "MSE", "g_MSE", "set_seed", "multimesh", "flatten_and_stack",
-           "find_L2_error", "newfig", "get_griddata", "init_distributed"]
+           "find_L2_error", "newfig", "get_griddata", "init_distributed", "config", "metrics",
+           "SolverConfig"]

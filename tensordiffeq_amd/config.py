@@ -1,0 +1,76 @@
+"""Configuration: constructor kwargs stay the primary interface (reference parity, SURVEY.md §5
+"Config / flag system"); :class:`SolverConfig` gathers the framework-level knobs with ``TDQ_*``
+environment overrides so that a run can be re-tuned without code changes.
+
+=====================  ==========================  =========================================
+field                  env var                     meaning
+=====================  ==========================  =========================================
+backend                TDQ_BACKEND                 auto | hip | jet | autograd
+precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | fp32 (fp32 MFMA)
+seed                   TDQ_SEED                    global seed applied at compile
+periodic_legacy        TDQ_PERIODIC_LEGACY         1: reference periodic-BC quirk (B12)
+log_every              TDQ_LOG_EVERY               progress / metrics cadence (steps)
+metrics_path           TDQ_METRICS                 JSONL metrics file (rank-suffixed under DP)
+graphs                 TDQ_NO_GRAPH=1 disables     HIP-graph capture of the training step
+fused_loss             TDQ_FUSED_LOSS=0 disables   single-kernel loss program
+allow_torch_fallback   TDQ_ALLOW_TORCH_FALLBACK    1: let GPU runs fall back to torch ops
+=====================  ==========================  =========================================
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+
+def _env_bool(name, default):
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")
+
+
+@dataclasses.dataclass(frozen=True)
+class SolverConfig:
+    backend: str = "auto"
+    precision: str = "bf16x3"
+    seed: int | None = None
+    periodic_legacy: bool = False
+    log_every: int = 100
+    metrics_path: str | None = None
+    graphs: bool = True
+    fused_loss: bool = True
+    allow_torch_fallback: bool = False
+
+    @classmethod
+    def from_env(cls, **overrides):
+        """Defaults <- TDQ_* environment <- explicit ``overrides`` (``None`` values are ignored)."""
+        e = os.environ
+        vals = {
+            "backend": e.get("TDQ_BACKEND", cls.backend),
+            "precision": e.get("TDQ_PRECISION", cls.precision),
+            "seed": int(e["TDQ_SEED"]) if "TDQ_SEED" in e else None,
+            "periodic_legacy": _env_bool("TDQ_PERIODIC_LEGACY", False),
+            "log_every": int(e.get("TDQ_LOG_EVERY", cls.log_every)),
+            "metrics_path": e.get("TDQ_METRICS") or None,
+            "graphs": not _env_bool("TDQ_NO_GRAPH", False),
+            "fused_loss": _env_bool("TDQ_FUSED_LOSS", True),
+            "allow_torch_fallback": _env_bool("TDQ_ALLOW_TORCH_FALLBACK", False),
+        }
+        vals.update({k: v for k, v in overrides.items() if v is not None})
+        cfg = cls(**vals)
+        cfg.validate()
+        return cfg
+
+    def validate(self):
+        if self.backend not in ("auto", "hip", "jet", "autograd"):
+            raise ValueError(f"backend {self.backend!r}")
+        if self.precision not in ("bf16x3", "fp32"):
+            raise ValueError(f"precision {self.precision!r}")
+        if self.log_every < 1:
+            raise ValueError("log_every must be >= 1")
+
+    def apply_process_env(self):
+        """Push the process-wide switches that the kernels / engines read."""
+        os.environ["TDQ_FUSED_LOSS"] = "1" if self.fused_loss else "0"
+        os.environ["TDQ_NO_GRAPH"] = "0" if self.graphs else "1"
+        os.environ["TDQ_ALLOW_TORCH_FALLBACK"] = "1" if self.allow_torch_fallback else "0"

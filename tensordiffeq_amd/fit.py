@@ -354,3 +354,40 @@ def nan_guard(loss):
     if math.isnan(v) or math.isinf(v):
         raise FloatingPointError(f"loss became {v}")
     return v
+
+
+# ---- reference functional API (tensordiffeq/fit.py) ------------------------------------------
+def fit(obj, tf_iter=0, newton_iter=0, batch_sz=None, newton_eager=True):
+    """Functional form of :meth:`CollocationSolverND.fit` (reference ``fit.py:17-102``): Adam for
+    ``tf_iter`` steps (graph-captured fused step), then L-BFGS for ``newton_iter`` iterations."""
+    return obj.fit(tf_iter=tf_iter, newton_iter=newton_iter, batch_sz=batch_sz, newton_eager=newton_eager)
+
+
+def fit_dist(obj, tf_iter=0, newton_iter=0, batch_sz=None, newton_eager=True):
+    """Data-parallel fit (reference ``fit.py:150-224``).  ``obj`` must be compiled with ``dist=True``
+    under torchrun (one process per GPU); points and SA weights are sharded, one flat all-reduce per
+    step.  Unlike the reference, L-BFGS also runs under DP and repeated calls resume (B6, B7)."""
+    if not getattr(obj, "dist", False):
+        raise ValueError("fit_dist needs a solver compiled with dist=True (launch with torchrun)")
+    return obj.fit(tf_iter=tf_iter, newton_iter=newton_iter, batch_sz=batch_sz, newton_eager=newton_eager)
+
+
+def train_op_inner(obj):
+    """One optimizer step: Adam descent on the network, Adam ascent on the SA weights
+    (reference ``fit.py:125-147``).  Returns the loss before the step (device scalar)."""
+    eng = obj._get_engine(None, 1)
+    return eng.run(1, use_graph=False)
+
+
+def lbfgs_train(obj, newton_iter=100):
+    """Strong-Wolfe L-BFGS on the network parameters (the reference's TFP graph path,
+    ``fit.py:107-112``); SA weights stay frozen (B15).  The final iterate is kept (B10)."""
+    obj._fit_lbfgs(newton_iter, newton_eager=False)
+    return obj.min_loss["l-bfgs"]
+
+
+def lbfgs_op(func, init_params, newton_iter):
+    """Minimise ``func(x) -> (loss, grad)`` from ``init_params`` (reference ``fit.py:115-122``,
+    ``tfp.optimizer.lbfgs_minimize`` with tolerance 1e-20).  Returns ``(x, loss)``."""
+    from .optimizers.lbfgs import graph_lbfgs
+    return graph_lbfgs(func, init_params, newton_iter)

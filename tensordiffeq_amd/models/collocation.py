@@ -77,11 +77,21 @@ class CollocationSolverND:
         self._programs = {}
         self._best_flat = {}
         self.log_every = 100
+        self.metrics = None   # MetricsLogger (compile(metrics_path=...) or TDQ_METRICS)
 
     # ================================================================== compile =========
     def compile(self, layer_sizes, f_model, domain, bcs, Adaptive_type=0, dict_adaptive=None,
                 init_weights=None, g=None, dist=False, backend="auto", device=None,
-                periodic_legacy=False, seed=None, network=None, precision=None):
+                periodic_legacy=False, seed=None, network=None, precision=None, metrics_path=None,
+                log_every=None):
+        from ..config import SolverConfig
+        self.config = SolverConfig.from_env(backend=None if backend == "auto" else backend, precision=precision,
+                                            seed=seed, metrics_path=metrics_path, log_every=log_every)
+        backend = self.config.backend
+        precision = self.config.precision
+        seed = self.config.seed
+        periodic_legacy = periodic_legacy or self.config.periodic_legacy
+        self.log_every = self.config.log_every
         if seed is not None:
             from ..utils.seeding import set_seed
             set_seed(seed)
@@ -106,6 +116,10 @@ class CollocationSolverND:
         X_f = torch.as_tensor(np.asarray(domain.X_f) if not torch.is_tensor(domain.X_f) else domain.X_f,
                               dtype=torch.float32)
         self.N_f = int(X_f.shape[0])
+        if self.config.metrics_path:
+            from ..metrics import MetricsLogger
+            self.metrics = MetricsLogger(self.config.metrics_path, self.dist_ctx.rank, self.dist_ctx.world,
+                                         n_points=None)
         ctx = self.dist_ctx
         self._lo, self._hi = pdist.shard_range(self.N_f, ctx.rank, ctx.world)
         self.X_f_local = X_f[self._lo:self._hi].to(self.device)
@@ -355,10 +369,16 @@ class CollocationSolverND:
                 print("Starting Adam training")
             bar = tqdm(total=tf_iter, disable=not (self.verbose and ctx.rank == 0), desc="Adam")
 
+            if self.metrics is not None:
+                self.metrics.n_points = self.X_f_local.shape[0]
+                self.metrics.mark(start_epoch)
+
             def progress(done, loss):
                 bar.n = done
                 if loss is not None:
                     bar.set_postfix(loss=loss)
+                    if self.metrics is not None:
+                        self._log_metrics("adam", loss)
                 bar.refresh()
 
             if batches == [None]:
@@ -381,6 +401,15 @@ class CollocationSolverND:
             self._fit_lbfgs(newton_iter, newton_eager)
         self._select_overall(start_epoch, tf_iter)
 
+    def _log_metrics(self, phase, loss):
+        st = self._state
+        ep = int(st["epoch_host"])
+        terms = None
+        if st["hist"] is not None and ep > 0:
+            row = st["hist"][ep - 1].detach().cpu().tolist()
+            terms = {t.name: v for t, v in zip(self.program().terms, row[1:])}
+        self.metrics.log(phase, ep, loss, terms)
+
     def _fit_lbfgs(self, newton_iter, newton_eager):
         ctx = self.dist_ctx
         if self.verbose and ctx.rank == 0:
@@ -390,6 +419,8 @@ class CollocationSolverND:
         bar = tqdm(total=newton_iter, disable=not (self.verbose and ctx.rank == 0), desc="L-BFGS")
 
         def on_eval(it, f):
+            if self.metrics is not None and (it % self.log_every == 0 or it == newton_iter):
+                self.metrics.log("lbfgs", it, f)
             if it % 10 == 0 or it == newton_iter:
                 bar.n = min(it, newton_iter)
                 bar.set_postfix(loss=f)

@@ -149,17 +149,80 @@ def scale_to_limits(u, xlimits):
     return xlimits[:, 0] + u * (xlimits[:, 1] - xlimits[:, 0])
 
 
-class LHS:
-    """Callable sampler mirroring the reference's ``LHS(xlimits=..., criterion=..., random_state=...)``."""
+class OptionsDictionary(dict):
+    """Declared options with defaults / allowed values / types (the SMT options object the
+    reference's sampler carries, ``sampling.py:14-146``)."""
 
-    def __init__(self, xlimits, criterion="c", random_state=None, iterations=5):
-        self.options = {"xlimits": np.asarray(xlimits, dtype=np.float64), "criterion": criterion,
-                        "random_state": random_state, "iterations": iterations}
+    def __init__(self):
+        super().__init__()
+        self._decl = {}
+
+    def declare(self, name, default=None, values=None, types=None, desc=""):
+        self._decl[name] = {"default": default, "values": values, "types": types, "desc": desc}
+        if name not in self:
+            dict.__setitem__(self, name, default)
+
+    def __setitem__(self, name, value):
+        d = self._decl.get(name)
+        if d is None:
+            raise KeyError(f"option {name!r} was not declared")
+        if d["values"] is not None and value not in d["values"]:
+            raise ValueError(f"option {name!r}: {value!r} not in {d['values']}")
+        if d["types"] is not None and value is not None and not isinstance(value, d["types"]):
+            raise TypeError(f"option {name!r}: {type(value).__name__} is not {d['types']}")
+        dict.__setitem__(self, name, value)
+
+    def update(self, other=(), **kw):
+        for k, v in dict(other, **kw).items():
+            self[k] = v
+
+
+class SamplingMethod:
+    """Base sampler: ``sampler(nt) -> (nt, nx)`` points (reference ``sampling.py:148-198``)."""
+
+    def __init__(self, **kwargs):
+        self.options = OptionsDictionary()
+        self.options.declare("xlimits", types=np.ndarray, desc="(nx, 2) bounds per dimension")
+        self._initialize()
+        if "xlimits" in kwargs:
+            kwargs["xlimits"] = np.asarray(kwargs["xlimits"], dtype=np.float64)
+        self.options.update(kwargs)
+
+    def _initialize(self):
+        pass
 
     def __call__(self, nt):
+        return self._compute(int(nt))
+
+    def _compute(self, nt):
+        raise NotImplementedError
+
+
+class ScaledSamplingMethod(SamplingMethod):
+    """Samples on the unit hypercube, then maps to ``xlimits`` (reference ``sampling.py:201-254``)."""
+
+    def __call__(self, nt):
+        return scale_to_limits(self._compute(int(nt)), self.options["xlimits"])
+
+
+class LHS(ScaledSamplingMethod):
+    """Latin hypercube: ``LHS(xlimits=..., criterion='c', random_state=None)`` (reference
+    ``sampling.py:257-313``); criteria c/center, m/maximin, cm/centermaximin, corr/correlation, ese."""
+
+    def __init__(self, xlimits=None, criterion="c", random_state=None, iterations=5, **kw):
+        super().__init__(xlimits=xlimits, criterion=criterion, random_state=random_state, iterations=iterations,
+                         **kw)
+
+    def _initialize(self):
         o = self.options
-        u = lhs_unit(int(nt), o["xlimits"].shape[0], o["criterion"], o["random_state"], o["iterations"])
-        return scale_to_limits(u, o["xlimits"])
+        o.declare("criterion", "c", values=["center", "maximin", "centermaximin", "correlation", "c", "m", "cm",
+                                            "corr", "ese"])
+        o.declare("random_state", None)
+        o.declare("iterations", 5, types=int)
+
+    def _compute(self, nt):
+        o = self.options
+        return lhs_unit(nt, o["xlimits"].shape[0], o["criterion"], o["random_state"], o["iterations"])
 
 
 def LatinHypercubeSample(N_f, bounds, criterion="c", random_state=None):

@@ -1,0 +1,49 @@
+"""SolverConfig env overrides and JSONL metrics (CPU)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import tensordiffeq_amd as tdq
+from tensordiffeq_amd.config import SolverConfig
+from tensordiffeq_amd.metrics import read_jsonl
+
+
+def test_config_env_and_overrides(monkeypatch):
+    monkeypatch.setenv("TDQ_PRECISION", "fp32")
+    monkeypatch.setenv("TDQ_LOG_EVERY", "7")
+    monkeypatch.setenv("TDQ_NO_GRAPH", "1")
+    c = SolverConfig.from_env()
+    assert c.precision == "fp32" and c.log_every == 7 and not c.graphs
+    c = SolverConfig.from_env(precision="bf16x3", log_every=None)
+    assert c.precision == "bf16x3" and c.log_every == 7
+    with pytest.raises(ValueError):
+        SolverConfig.from_env(backend="cuda")
+
+
+def test_metrics_jsonl(tmp_path):
+    from tensordiffeq_amd.boundaries import DomainND, dirichletBC
+    tdq.set_seed(0)
+    D = DomainND(["x", "t"], time_var="t")
+    D.add("x", [-1.0, 1.0], 32)
+    D.add("t", [0.0, 1.0], 16)
+    D.generate_collocation_points(256)
+
+    def f_model(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        return tdq.grad(u, t) - 0.01 * tdq.grad(tdq.grad(u, x), x)
+
+    m = tdq.CollocationSolverND(verbose=False)
+    path = tmp_path / "m.jsonl"
+    m.compile([2, 16, 16, 1], f_model, D, [dirichletBC(D, 0.0, "x", "upper")], device="cpu",
+              metrics_path=str(path), log_every=5)
+    m.fit(tf_iter=10, newton_iter=5)
+    m.metrics.close()
+    recs = read_jsonl(path)
+    adam = [r for r in recs if r["phase"] == "adam"]
+    assert [r["epoch"] for r in adam] == [5, 10]
+    assert set(adam[-1]["terms"]) == {t.name for t in m.program().terms}
+    assert adam[-1]["pts_per_s"] > 0 and math.isfinite(adam[-1]["loss"])
+    assert any(r["phase"] == "lbfgs" for r in recs)
+    assert np.isclose(adam[-1]["loss"], m.losses[9]["Total Loss"], rtol=1e-6)
