@@ -55,12 +55,20 @@ def build(args):
 
 def main(argv=None):
     args = parser(__doc__.splitlines()[0], iters=10000, newton=10000).parse_args(argv)
+    import time
     model, Domain = build(args)
-    model.fit(tf_iter=args.iters, newton_iter=args.newton)
+    t0 = time.perf_counter()
+    model.fit(tf_iter=args.iters)
+    t1 = time.perf_counter()
+    if args.newton:
+        model.fit(newton_iter=args.newton)
+    t2 = time.perf_counter()
     x, t, U = ac_data()
     err, X_star, u_pred, f_pred = l2_on_data_grid(model, x, t, U)
     res = report("AC-SA", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"]),
-                           "backend": model.active_backend}, args.quiet)
+                           "min_loss_adam": float(model.min_loss["adam"]),
+                           "min_loss_lbfgs": float(model.min_loss["l-bfgs"]),
+                           "adam_s": t1 - t0, "lbfgs_s": t2 - t1, "backend": model.active_backend}, args.quiet)
     if args.plot:
         tdq.plotting.plot_solution_domain1D(model, [x, t], ub=np.array([1.0, 1.0]), lb=np.array([-1.0, 0.0]),
                                             Exact_u=U)
