@@ -226,6 +226,7 @@ class CollocationSolverND:
                     pairs.append((su, sl))
                     for fn in bc.deriv_model:
                         prog.register_callable(fn, su)
+                        prog.register_callable(fn, sl)
                 prog.add_term(Term(name, "periodic", pairs=pairs, fns=list(bc.deriv_model), lam=lam,
                                    scale=rep_scale))
             elif bc.isNeumann:

@@ -21,6 +21,11 @@ Loss definitions (SURVEY.md §2.5 "Exact numerics to match"):
                           type 2 lam*mean(f^2); one lambda per residual (B11 fixed).
 Adaptive periodic / Neumann terms, which the reference rejects (B13), take per-point weights.
 
+Mixed plans: when some callables need derivatives beyond the HIP kernels' order-2 envelope (e.g. the
+periodic u_xxx, u_xxxx of AC-baseline on 2 x 201 boundary points) the segments that only need
+order <= 2 (the collocation points) still run on the HIP kernels, and the few high-order segments
+run through the differentiable torch jet engine; the loss then composes both with autograd.
+
 Data parallel: the collocation segment is this rank's shard; residual means divide by the global
 count and every replicated term is scaled by ``1/world``, so per-rank losses sum to the global one.
 """
@@ -40,10 +45,18 @@ class Segment:
         self.name = name
         self.X = X
         self.offset = 0
+        self.part = 0     # 0: X_all (main plan); 1: X_hi (high-order plan, mixed mode)
 
     @property
     def n(self):
         return self.X.shape[0]
+
+
+class JetParts:
+    """Jets of a mixed program: ``lo`` over ``X_all`` (main plan), ``hi`` over ``X_hi``."""
+
+    def __init__(self, lo, hi):
+        self.lo, self.hi = lo, hi
 
 
 class Term:
@@ -73,8 +86,10 @@ class LossProgram:
         self.terms = []
         self.callables = []   # (fn, segment names, extra_args)
         self.plan = None
+        self.plan_hi = None   # mixed mode: plan of the high-order segments (torch jet engine)
         self.backend = None
         self.X_all = None
+        self.X_hi = None
         self.reasons = []
         self.fused_op = None
 
@@ -93,18 +108,27 @@ class LossProgram:
         self.callables.append((fn, seg_idx, extra_args))
 
     def finalize(self):
-        off = 0
-        for s in self.segments:
-            s.offset = off
-            off += s.n
-        self.X_all = torch.cat([s.X for s in self.segments], dim=0).contiguous() if self.segments \
-            else torch.zeros(0, self.d_in, device=self.device)
         self._plan()
+        parts = ([s for s in self.segments if s.part == 0], [s for s in self.segments if s.part == 1])
+        for segs in parts:
+            off = 0
+            for s in segs:
+                s.offset = off
+                off += s.n
+        cat = lambda segs: torch.cat([s.X for s in segs], dim=0).contiguous() if segs \
+            else torch.zeros(0, self.d_in, device=self.device)
+        self.X_all = cat(parts[0])
+        self.X_hi = cat(parts[1]) if parts[1] else None
+
+    @property
+    def mixed(self):
+        return self.plan_hi is not None
 
     def _plan(self):
         from ..models.networks import TanhMLP
         from ..ops import jet_mlp
         requests, jetable = set(), True
+        seg_req = {}
         reasons = []
         if not isinstance(self.net, TanhMLP):
             jetable = False
@@ -117,10 +141,31 @@ class LossProgram:
             net64 = _Float64View(self.net)
             req, ok, why, _ = autodiff.record_callable(fn, net64, probe, extra_args=extra)
             requests |= req
+            seg_req.setdefault(si, set()).update(req)
             if not ok:
                 jetable = False
                 reasons.extend(why)
         backend = self.requested_backend
+        for s in self.segments:
+            s.part = 0
+        if backend in ("auto", "hip") and jetable:
+            plan = JetPlan(requests, self.d_in)
+            ok, why = jet_mlp.hip_eligible(self.net, plan, self.device)
+            if not ok and plan.order > 2:
+                lo_req, hi_req, hi = self._split_by_order(seg_req)
+                if hi and lo_req is not None:
+                    ok_lo, why_lo = jet_mlp.hip_eligible(self.net, JetPlan(lo_req, self.d_in), self.device)
+                    n_hi = sum(self.segments[i].n for i in hi)
+                    n_lo = sum(sg.n for sg in self.segments) - n_hi
+                    if ok_lo and n_lo >= n_hi:
+                        for i in hi:
+                            self.segments[i].part = 1
+                        self.plan = JetPlan(lo_req, self.d_in)
+                        self.plan_hi = JetPlan(hi_req, self.d_in)
+                        self.backend = "hip"
+                        self.reasons = reasons + [f"mixed: order-{self.plan_hi.order} segments "
+                                                  f"{[self.segments[i].name for i in sorted(hi)]} on the torch jet"]
+                        return
         if backend == "auto":
             if not jetable:
                 backend = "autograd"
@@ -142,15 +187,46 @@ class LossProgram:
         self.backend = backend
         self.reasons = reasons
 
+    def _split_by_order(self, seg_req):
+        """Partition segments by the order their callables need: (lo requests, hi requests, hi
+        segment indices); segments without callables only need the value stream."""
+        lo, hi_req, hi = {()}, set(), set()
+        for si, req in seg_req.items():
+            if any(len(m) > 2 for m in req):
+                hi.add(si)
+                hi_req |= req
+            else:
+                lo |= req
+        return lo, hi_req, hi
+
     # ---------------------------------------------------------------- evaluation -----
     def seg_view(self, J, si):
         s = self.segments[si]
+        if isinstance(J, JetParts):
+            src, plan = (J.hi, self.plan_hi) if s.part == 1 else (J.lo, self.plan)
+            return jet_dict(src[:, s.offset:s.offset + s.n], plan)
         return jet_dict(J[:, s.offset:s.offset + s.n], self.plan)
 
-    def jet(self, params, X=None):
+    def jet(self, params, X=None, plan=None):
         from ..ops import jet_mlp
+        from ..jet import jet_forward
+        if X is None and self.mixed:
+            lo = jet_mlp.jet_eval(self.X_all, self.net, params, self.plan, self.backend, self.precision) \
+                if self.X_all.shape[0] else None
+            hi = jet_forward(self.X_hi, self.net.weights(params), self.plan_hi)
+            return JetParts(lo, hi)
         X = self.X_all if X is None else X
+        if plan is not None and plan is self.plan_hi:
+            return jet_forward(X, self.net.weights(params), plan)
         return jet_mlp.jet_eval(X, self.net, params, self.plan, self.backend, self.precision)
+
+    def plan_for(self, fn):
+        """Plan that serves callable ``fn`` (the high-order one if ``fn`` runs on a hi segment)."""
+        if self.mixed:
+            for f, si, _ in self.callables:
+                if f is fn and self.segments[si].part == 1:
+                    return self.plan_hi
+        return self.plan
 
     def call(self, fn, si, extra=(), J=None, X=None):
         """Evaluate a user callable on segment ``si`` (or explicit points ``X``)."""
@@ -159,7 +235,7 @@ class LossProgram:
             cols = [Xs[:, j:j + 1].detach().clone().requires_grad_(True) for j in range(self.d_in)]
             return fn(getattr(self, "_cur_net", self.net), *extra, *cols)
         Xs = self.segments[si].X if X is None else X
-        jd = self.seg_view(J, si) if X is None else jet_dict(J, self.plan)
+        jd = self.seg_view(J, si) if X is None else jet_dict(J, self.plan_for(fn))
         cols = [Xs[:, j:j + 1] for j in range(self.d_in)]
         ctx = autodiff.JetContext(cols, jd)
         with autodiff.use(ctx):
@@ -169,6 +245,8 @@ class LossProgram:
         if self.backend == "autograd":
             return getattr(self, "_cur_net", self.net)(self.segments[si].X)
         s = self.segments[si]
+        if isinstance(J, JetParts):
+            J = J.hi if s.part == 1 else J.lo
         return J[0, s.offset:s.offset + s.n]
 
     def evaluate(self, params=None, lambdas=None, extras=None):
@@ -261,7 +339,7 @@ class LossProgram:
         import os
         from .. import fusion
         self.fused_op = None
-        if self.backend != "hip" or os.environ.get("TDQ_FUSED_LOSS", "1") == "0":
+        if self.backend != "hip" or self.mixed or os.environ.get("TDQ_FUSED_LOSS", "1") == "0":
             return False
         fl = fusion.build(self, lambdas)
         if fl is None:
@@ -286,9 +364,10 @@ class LossProgram:
                     o = fn(_ParamView(self.net, params), *extra, *cols)
             else:
                 with torch.no_grad():
-                    J = self.jet(params if params is not None else self.net.flat, X=Xc)
+                    plan = self.plan_for(fn)
+                    J = self.jet(params if params is not None else self.net.flat, X=Xc, plan=plan)
                     cols = [Xc[:, j:j + 1] for j in range(self.d_in)]
-                    ctx = autodiff.JetContext(cols, jet_dict(J, self.plan))
+                    ctx = autodiff.JetContext(cols, jet_dict(J, plan))
                     with autodiff.use(ctx):
                         o = fn(ctx.proxy(), *extra, *cols)
             o = o if isinstance(o, (tuple, list)) else (o,)

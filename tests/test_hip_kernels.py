@@ -209,3 +209,52 @@ def test_solver_hip_matches_jet_backend(prec):
     b.fit(tf_iter=20)
     la, lb = a.losses[-1]["Total Loss"], b.losses[-1]["Total Loss"]
     assert abs(la - lb) / abs(lb) < 1e-3 * tl, (la, lb)
+
+
+def test_mixed_plan_high_order_periodic():
+    """AC-baseline-style program: the residual (order 2) runs on the HIP kernels, the periodic
+    u_xxx / u_xxxx boundary segments on the torch jet engine; loss, gradient and a short fit agree
+    with the all-torch jet program."""
+    import math
+    import numpy as np
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.boundaries import DomainND, IC, periodicBC
+
+    def build(backend):
+        tdq.set_seed(0)
+        D = DomainND(["x", "t"], time_var="t")
+        D.add("x", [-1.0, 1.0], 512)
+        D.add("t", [0.0, 1.0], 201)
+        D.generate_collocation_points(3000)
+
+        def deriv_model(u_model, x, t):
+            u = u_model(torch.cat([x, t], 1))
+            u_x = tdq.grad(u, x)
+            u_xx = tdq.grad(u_x, x)
+            u_xxx = tdq.grad(u_xx, x)
+            return u, u_x, u_xxx, tdq.grad(u_xxx, x)
+
+        def f_model(u_model, x, t):
+            u = u_model(torch.cat([x, t], 1))
+            u_xx = tdq.grad(tdq.grad(u, x), x)
+            return tdq.grad(u, t) - 0.0001 * u_xx + 5.0 * u ** 3 - 5.0 * u
+
+        m = tdq.CollocationSolverND(verbose=False)
+        m.compile([2, 128, 128, 128, 128, 1], f_model, D,
+                  [IC(D, [lambda x: x ** 2 * np.cos(math.pi * x)], var=[["x"]]), periodicBC(D, ["x"], [deriv_model])],
+                  backend=backend, device="cuda", precision="fp32")
+        return m
+
+    a, b = build("auto"), build("jet")
+    pa = a.program()
+    assert a.active_backend == "hip" and pa.mixed and pa.plan_hi.order == 4 and pa.plan.order == 2
+    la, ga = a.grad()
+    lb, gb = b.grad()
+    assert abs(la.item() - lb.item()) / abs(lb.item()) < 1e-5
+    for x, y in zip(ga, gb):
+        assert ((x - y).norm() / y.norm().clamp_min(1e-12)).item() < 1e-4
+    a.fit(tf_iter=10)
+    b.fit(tf_iter=10)
+    assert abs(a.losses[-1]["Total Loss"] - b.losses[-1]["Total Loss"]) / b.losses[-1]["Total Loss"] < 1e-3
+    u, f = a.predict(np.random.rand(100, 2))
+    assert np.isfinite(u).all() and np.isfinite(f).all()
