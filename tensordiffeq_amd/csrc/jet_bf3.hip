@@ -5,11 +5,10 @@
 // A-operand images: img[layer-1][o][kb][hl][lane] = 8 bf16 (hl 0 = hi, 1 = lo)
 //   element j of lane (p, g): row 16o + p, k = 8g + j -> feature 32kb + (j<4 ? 4g+j : 16+4g+j-4)
 //   transposed = 1 (forward):  A[row = out][k = in]  ;  0 (backward): A[row = in][k = out]
-__global__ void __launch_bounds__(256) pack_bf3_kernel(const float* __restrict__ P, bf16x8* __restrict__ img,
-                                                       NetDims d, int WT, int transposed) {
+__device__ __forceinline__ void pack_frag(const float* __restrict__ P, bf16x8* __restrict__ img, const NetDims& d,
+                                          int WT, int transposed, int e) {
   const int KB = WT / 2;
-  const int total = (d.n_hidden - 1) * WT * KB * 64;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+  {
     const int lane = e & 63, frag = e >> 6;
     const int kb = frag % KB, o = (frag / KB) % WT, layer = frag / (KB * WT) + 1;
     const int p = lane & 15, g = lane >> 4, row = 16 * o + p;
@@ -30,10 +29,9 @@ __global__ void __launch_bounds__(256) pack_bf3_kernel(const float* __restrict__
 }
 
 // zero-padded fp32 aux image (layout: jet_bf3.h aux_*)
-__global__ void __launch_bounds__(256) pack_aux_kernel(const float* __restrict__ P, float* __restrict__ aux,
-                                                       NetDims d, int W) {
-  const int total = aux_floats(d, W);
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+__device__ __forceinline__ void pack_aux(const float* __restrict__ P, float* __restrict__ aux, const NetDims& d,
+                                         int W, int e) {
+  {
     float v = 0.f;
     if (e < aux_b0(d, W)) {  // K0 [d_in][W]
       const int j = e / W, f = e - j * W;
@@ -55,6 +53,22 @@ __global__ void __launch_bounds__(256) pack_aux_kernel(const float* __restrict__
   }
 }
 
+// one launch per step: forward A image ([out][in]), backward A image ([in][out]) and aux image
+__global__ void __launch_bounds__(256) pack_all_kernel(const float* __restrict__ P, bf16x8* __restrict__ fimg,
+                                                       bf16x8* __restrict__ bimg, float* __restrict__ aux, NetDims d,
+                                                       int WT) {
+  const int nf = (d.n_hidden - 1) * WT * (WT / 2) * 64;
+  const int total = 2 * nf + aux_floats(d, 16 * WT);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    if (e < nf)
+      pack_frag(P, fimg, d, WT, 1, e);
+    else if (e < 2 * nf)
+      pack_frag(P, bimg, d, WT, 0, e - nf);
+    else
+      pack_aux(P, aux, d, 16 * WT, e - 2 * nf);
+  }
+}
+
 namespace {
 
 int64_t img_floats(int WT, int n_hidden) {  // hi/lo A images, in floats
@@ -63,16 +77,11 @@ int64_t img_floats(int WT, int n_hidden) {  // hi/lo A images, in floats
 
 int64_t aux_alloc(int d_in, int n_hidden, int W) { return ((int64_t)(d_in + n_hidden + 4) * W + 4 + 3) / 4 * 4; }
 
-int launch_pack(const float* P, bf16x8* img, float* aux, NetDims d, int WT, int transposed, hipStream_t st) {
-  const int total = (d.n_hidden - 1) * WT * (WT / 2) * 64;
-  if (total > 0) {
-    int blocks = (total + 255) / 256;
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(pack_bf3_kernel, dim3(blocks), dim3(256), 0, st, P, img, d, WT, transposed);
-    TDQ_CHECK_LAUNCH();
-  }
-  const int na = aux_floats(d, 16 * WT);
-  hipLaunchKernelGGL(pack_aux_kernel, dim3((na + 255) / 256), dim3(256), 0, st, P, aux, d, 16 * WT);
+int launch_pack(const float* P, bf16x8* fimg, bf16x8* bimg, float* aux, NetDims d, int WT, hipStream_t st) {
+  const int total = 2 * (d.n_hidden - 1) * WT * (WT / 2) * 64 + aux_floats(d, 16 * WT);
+  int blocks = (total + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(pack_all_kernel, dim3(blocks), dim3(256), 0, st, P, fimg, bimg, aux, d, WT);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -94,22 +103,23 @@ int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
 
 extern "C" {
 
-// saved post-activations Hs + forward A image + aux image, in floats (-1: unsupported)
+// scratch = saved post-activations Hs | forward A image | backward A image | aux image (floats;
+// -1: unsupported).  The forward packs all three images in one launch; the backward reuses them.
 int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int S) {
   const int WT = width_tiles(width);
   if (WT < 2) return -1;
   const int64_t nwg = (N + 63) / 64;
-  return (int64_t)n_hidden * nwg * S * 4 * WT * 256 + img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT);
+  return (int64_t)n_hidden * nwg * S * 4 * WT * 256 + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT);
 }
 
-// per-workgroup gradient slabs + reduction partials + backward A image + aux image, in floats
+// per-workgroup gradient slabs + reduction partials, in floats
 int64_t tdq_jet_bf3_slab_floats(int N, int d_in, int width, int d_out, int n_hidden) {
   const int WT = width_tiles(width);
   if (WT < 2) return -1;
   const int64_t nwg = (N + 63) / 64;
   const int64_t P = param_count(d_in, width, d_out, n_hidden);
   const int64_t chunks = nwg < 32 ? nwg : 32;
-  return (nwg * P + chunks * P + 3) / 4 * 4 + img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT);
+  return nwg * P + chunks * P;
 }
 
 int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
@@ -124,8 +134,9 @@ int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, in
   const int64_t nwg = (N + 63) / 64;
   float* Hs = scratch;
   float* img = scratch + (int64_t)n_hidden * nwg * S * 4 * WT * 256;
-  float* aux = img + img_floats(WT, n_hidden);
-  int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), aux, d, WT, 1, st);
+  float* bimg = img + img_floats(WT, n_hidden);
+  float* aux = bimg + img_floats(WT, n_hidden);
+  int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
   if (rc) return rc;
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st};
   return dispatch(true, WT, S, nso, a);
@@ -144,13 +155,13 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
   const int chunks = nwg < 32 ? nwg : 32;
   float* slab = work;
-  float* img = work + ((size_t)nwg * Ptot + (size_t)chunks * Ptot + 3) / 4 * 4;
-  float* aux = img + img_floats(WT, n_hidden);
-  int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), aux, d, WT, 0, st);
-  if (rc) return rc;
+  // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
+  const float* img = Hs + (int64_t)n_hidden * nwg * S * 4 * WT * 256 + img_floats(WT, n_hidden);
+  const float* aux = img + img_floats(WT, n_hidden);
+  (void)P;
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), dJ, nullptr, const_cast<float*>(Hs), slab, N, Ptot, d,
             sp, st};
-  rc = dispatch(false, WT, S, nso, a);
+  int rc = dispatch(false, WT, S, nso, a);
   if (rc) return rc;
   return tdq_slab_reduce(work, grad, nwg, Ptot, chunks, stream);
 }

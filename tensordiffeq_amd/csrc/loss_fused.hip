@@ -258,7 +258,7 @@ extern "C" {
 int tdq_loss_fused(const int* code, const float* consts, const void* outs, const void* groups,
                    const void* ptrs, int n_groups, int n_terms, int n_scal, int S, int d_in, int N,
                    const float* J, const float* X, float* dJ, float* partials, int n_blocks, int max_regs,
-                   float* losses, float* total, float* dscal, void* stream) {
+                   float* losses, float* total, float* dscal, int with_total, void* stream) {
   LFMeta meta{n_groups, n_terms, n_scal, S, d_in, N};
   if (meta.n_groups < 1 || meta.n_groups > LF_MAX_GROUPS || meta.n_terms > LF_MAX_TERMS ||
       meta.n_scal > LF_MAX_SCAL)
@@ -280,8 +280,10 @@ int tdq_loss_fused(const int* code, const float* consts, const void* outs, const
   hipLaunchKernelGGL(loss_reduce_kernel, dim3(ns), dim3(256), 0, st, partials, n_blocks, meta.n_terms,
                      meta.n_scal, losses, total, dscal);
   TDQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, losses, meta.n_terms, total);
-  TDQ_CHECK_LAUNCH();
+  if (with_total) {  // the Adam step's bookkeeping kernel (tdq_step_book) sums the terms itself
+    hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, losses, meta.n_terms, total);
+    TDQ_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -9,6 +9,11 @@
 //   is replayable inside a captured HIP graph.  float4 vector path + scalar tail per group.
 // tdq_best_track: snapshot the flat parameters when the step's loss improves (two tiny
 //   kernels: copy-if-improved, then the scalar update, so no block races on best_loss).
+// tdq_step_book: ONE single-thread kernel per step for all scalar bookkeeping - history row
+//   [loss, terms...] at the device epoch, best-loss / best-epoch update and the "improved" flag,
+//   every Adam step counter += 1, epoch += 1.  The Adam kernel then snapshots theta into the
+//   best-weights buffer (before its update) when the flag is set, so best tracking costs no
+//   extra launch.
 #include "common.h"
 
 #define TDQ_MAX_GROUPS 16
@@ -37,7 +42,9 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 }
 
 __global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const double* __restrict__ tptr,
-                                                          float lr, float b1, float b2, float eps) {
+                                                          float lr, float b1, float b2, float eps,
+                                                          const int* __restrict__ improved, float* __restrict__ snap) {
+  const bool do_snap = snap != nullptr && *improved != 0;  // group 0 only
   const double t = *tptr;
   const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
   const int64_t total = args.start[args.ngroups];
@@ -53,6 +60,7 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const do
     const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
     if (aligned && e0 + 4 <= gr.n) {
       f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
+      if (do_snap && gi == 0) *reinterpret_cast<f32x4*>(snap + e0) = p;
       const f32x4 g = *reinterpret_cast<const f32x4*>(gr.g + e0);
       f32x4 m = *reinterpret_cast<const f32x4*>(gr.m + e0);
       f32x4 v = *reinterpret_cast<const f32x4*>(gr.v + e0);
@@ -68,7 +76,10 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const do
     } else {
       for (int c = 0; c < 4; ++c) {
         const int64_t e = e0 + c;
-        if (e < gr.n) adam_elem(gr.p[e], sg * gr.g[e], gr.m[e], gr.v[e], b1, b2, eps, lr_t);
+        if (e < gr.n) {
+          if (do_snap && gi == 0) snap[e] = gr.p[e];
+          adam_elem(gr.p[e], sg * gr.g[e], gr.m[e], gr.v[e], b1, b2, eps, lr_t);
+        }
       }
     }
   }
@@ -93,12 +104,58 @@ __global__ void best_scalar_kernel(const float* __restrict__ loss, float* __rest
   }
 }
 
+#define TDQ_MAX_COUNTERS 8
+struct Counters {
+  double* c[TDQ_MAX_COUNTERS];
+  int n;
+};
+
+__global__ void step_book_kernel(float* __restrict__ loss, const float* __restrict__ terms, int n_terms, int sum_terms,
+                                 float* __restrict__ hist, int64_t hist_rows, int64_t* __restrict__ epoch,
+                                 float* __restrict__ best_loss, int64_t* __restrict__ best_epoch,
+                                 int* __restrict__ improved, Counters cnt) {
+  float lv = *loss;
+  if (sum_terms) {  // fused loss: total = sum of the (all-reduced) terms, in term order
+    lv = 0.f;
+    for (int t = 0; t < n_terms; ++t) lv += terms[t];
+    *loss = lv;
+  }
+  const int64_t ep = *epoch;
+  if (ep >= 0 && ep < hist_rows) {
+    float* row = hist + ep * (1 + n_terms);
+    row[0] = lv;
+    for (int t = 0; t < n_terms; ++t) row[1 + t] = terms[t];
+  }
+  const int imp = lv < *best_loss;  // NaN never improves
+  if (imp) {
+    *best_loss = lv;
+    *best_epoch = ep;
+  }
+  *improved = imp;
+  for (int i = 0; i < cnt.n; ++i) *cnt.c[i] += 1.0;
+  *epoch = ep + 1;
+}
+
 extern "C" {
 
-int tdq_abi_version() { return 5; }
+int tdq_abi_version() { return 6; }
 
+int tdq_step_book(float* loss, const float* terms, int n_terms, int sum_terms, float* hist, int64_t hist_rows,
+                  int64_t* epoch, float* best_loss, int64_t* best_epoch, int* improved, double* const* counters,
+                  int ncnt, void* stream) {
+  if (ncnt < 0 || ncnt > TDQ_MAX_COUNTERS) return (int)hipErrorInvalidValue;
+  Counters c;
+  c.n = ncnt;
+  for (int i = 0; i < TDQ_MAX_COUNTERS; ++i) c.c[i] = i < ncnt ? counters[i] : nullptr;
+  hipLaunchKernelGGL(step_book_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), loss, terms,
+                     n_terms, sum_terms, hist, hist_rows, epoch, best_loss, best_epoch, improved, c);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// improved / snap: optional (nullptr) best-weights snapshot of group 0 before its update
 int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, float b1, float b2,
-                   float eps, void* stream) {
+                   float eps, const int* improved, float* snap, void* stream) {
   if (ngroups <= 0 || ngroups > TDQ_MAX_GROUPS) return (int)hipErrorInvalidValue;
   AdamArgs args;
   const AdamGroup* src = reinterpret_cast<const AdamGroup*>(groups);
@@ -118,7 +175,7 @@ int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, f
   int64_t blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), args, t, lr, b1, b2, eps);
+                     reinterpret_cast<hipStream_t>(stream), args, t, lr, b1, b2, eps, improved, snap);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -43,8 +43,11 @@ class _Bucket:
         for n in self.sizes:
             out.append(buf[off:off + n])
             off += n
-        scal = [buf[off + i] for i in range(self.n_scalars)]
-        return out, scal
+        return out, buf[off:off + self.n_scalars]   # scal[0] = loss, scal[1:] = terms (contiguous)
+
+
+def _term_list(terms):
+    return list(terms.unbind()) if torch.is_tensor(terms) else list(terms)
 
 
 class ParamGroup:
@@ -130,11 +133,12 @@ class AdamEngine:
                            else ("zero", 0))
         return src
 
-    def _phase_a_fused(self, fop):
+    def _phase_a_fused(self, fop, for_step=False):
         from .ops import jet_hip
         prog = self.program
         J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
-        total, losses, dJ, dlam, dscal = fop(J)
+        # inside an optimizer step the bookkeeping kernel (fused.step_book) sums the terms
+        total, losses, dJ, dlam, dscal = fop(J, with_total=not for_step)
         gflat = jet_hip.backward_raw(saved, dJ)
         if getattr(self, "_fsrc", None) is None:
             self._fsrc = self._fused_map(fop)
@@ -154,13 +158,15 @@ class AdamEngine:
                 grads.append(dscal[k].view_as(w))
             else:
                 grads.append(torch.zeros_like(w))
-        terms = [losses[k] for k in range(len(self.term_names))]
-        return total, grads, terms
+        return total, grads, losses   # losses: contiguous per-term vector
 
-    def _phase_a(self):
+    def _phase_a(self, for_step=False):
+        """Loss, gradients (wrt every group tensor) and per-term losses.  ``for_step=True`` (the
+        optimizer step paths only): the fused loss leaves the total to ``_phase_b``."""
         fop = getattr(self.program, "fused_op", None)
+        self._sum_terms = fop is not None and for_step
         if fop is not None:
-            return self._phase_a_fused(fop)
+            return self._phase_a_fused(fop, for_step)
         alias = [t.detach().requires_grad_(True) for t in self.wrt]
         loss, vals = self.program.evaluate(**self.bind(alias))
         grads = torch.autograd.grad(loss, alias, allow_unused=True)
@@ -173,6 +179,7 @@ class AdamEngine:
             return loss, grads, terms
         red_idx = self.red_idx
         red = [grads[i] for i in red_idx]
+        terms = _term_list(terms)
         bucket = _Bucket(red, 1 + len(terms))
         buf = bucket.pack(red, [loss] + terms)
         self.dist.all_reduce_(buf)
@@ -183,23 +190,28 @@ class AdamEngine:
         return scal[0], grads, scal[1:]
 
     def _phase_b(self, loss, grads, terms):
+        """History row, best tracking, step counters and epoch in one bookkeeping launch
+        (``fused.step_book``), then one Adam launch per group; group 0's launch also snapshots
+        the best weights (before the update) when the step improved the loss."""
         st = self.state
-        fused.best_track(loss, st["best_loss"], self.flat, st["best_flat"], st["best_epoch"],
-                         st["epoch"])
-        row = torch.stack([loss.float()] + [t.float() for t in terms])
-        st["hist"].index_copy_(0, st["epoch"].reshape(1), row.unsqueeze(0))
+        if "improved" not in st:
+            st["improved"] = torch.zeros((), dtype=torch.int32, device=self.device)
+        tv = terms if torch.is_tensor(terms) else (
+            torch.stack([t.float().reshape(()) for t in terms]) if len(terms)
+            else torch.zeros(0, device=self.device))
+        fused.step_book(loss, tv.reshape(-1).float().contiguous(), st, self.counters,
+                        sum_terms=getattr(self, "_sum_terms", False))
         off = 0
-        for grp, opt, t, mom in zip(self.groups, self.opts, self.counters, self.moments):
+        for gi, (grp, opt, t, mom) in enumerate(zip(self.groups, self.opts, self.counters, self.moments)):
             n = len(grp.tensors)
-            t.add_(1.0)
             items = [(p, g, m, v, grp.sign) for p, g, (m, v) in zip(grp.tensors, grads[off:off + n], mom)]
-            fused.adam_multi(items, t, opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon)
+            snap = (st["best_flat"], st["improved"]) if gi == 0 and grp.tensors[0] is self.flat else None
+            fused.adam_multi(items, t, opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon, snapshot=snap)
             off += n
-        st["epoch"].add_(1)
         return loss
 
     def _eager_step(self):
-        loss, grads, terms = self._phase_a()
+        loss, grads, terms = self._phase_a(for_step=True)
         loss, grads, terms = self._reduce(loss, grads, terms)
         return self._phase_b(loss, grads, terms)
 
@@ -223,9 +235,10 @@ class AdamEngine:
         else:
             ga = torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga, pool=pool):
-                loss, grads, terms = self._phase_a()
+                loss, grads, terms = self._phase_a(for_step=True)
                 red_idx = self.red_idx
                 red = [grads[i] for i in red_idx]
+                terms = _term_list(terms)
                 self._bucket = _Bucket(red, 1 + len(terms))
                 self._bucket_buf = self._bucket.pack(red, [loss] + terms)
                 self._grads_static = grads

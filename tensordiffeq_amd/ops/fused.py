@@ -6,6 +6,9 @@
                 counter, so the launch is graph-capturable.
 ``best_track``  device-side "keep the best weights" (reference fit.py:51-55 stored an alias of
                 the live model, B8): copies the flat buffer to the snapshot iff loss < best.
+``step_book``   the per-step scalar bookkeeping in one single-thread launch (history row,
+                best loss/epoch + "improved" flag, every Adam step counter, epoch); the snapshot
+                of the best weights then rides on the Adam launch (``adam_multi(snapshot=...)``).
 """
 from __future__ import annotations
 
@@ -29,8 +32,10 @@ def _native(t):
     return t.is_cuda and _lib.available()
 
 
-def adam_multi(groups, t, lr, b1, b2, eps):
-    """groups: list of (param, grad, m, v, sign).  ``t``: float64 device step counter (already +1)."""
+def adam_multi(groups, t, lr, b1, b2, eps, snapshot=None):
+    """groups: list of (param, grad, m, v, sign).  ``t``: float64 device step counter (already +1).
+    ``snapshot=(best, improved)``: copy group 0's parameters into ``best`` before the update when
+    the int32 device flag ``improved`` is set."""
     if not groups:
         return
     if _native(groups[0][0]) and all(x.dtype == torch.float32 and x.is_contiguous()
@@ -38,19 +43,60 @@ def adam_multi(groups, t, lr, b1, b2, eps):
         lib = _lib.load()
         for lo in range(0, len(groups), _MAX_GROUPS):
             chunk = groups[lo:lo + _MAX_GROUPS]
+            snap = snapshot if lo == 0 else None
             arr = (_Group * len(chunk))()
             for i, (p, g, m, v, sign) in enumerate(chunk):
                 arr[i] = _Group(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
                                 float(sign), 0.0)
             rc = lib.tdq_adam_multi(ctypes.cast(arr, ctypes.c_void_p), len(chunk), _lib.ptr(t),
                                     float(lr), float(b1), float(b2), float(eps),
+                                    _lib.ptr(snap[1]) if snap else None, _lib.ptr(snap[0]) if snap else None,
                                     _lib.stream_ptr(p.device))
             _lib.check(rc, "tdq_adam_multi")
         return
     _lib.require_on_gpu() if groups[0][0].is_cuda else None
     with torch.no_grad():
+        if snapshot is not None:
+            best, improved = snapshot
+            best.copy_(torch.where(improved.bool(), groups[0][0], best))
         for (p, g, m, v, sign) in groups:
             torch_update(p, g, m, v, t, lr, b1, b2, eps, sign)
+
+
+def step_book(loss, terms, state, counters, sum_terms=False):
+    """Per-step bookkeeping on device (see module doc).  ``terms``: contiguous float32 vector.
+    ``sum_terms``: the loss buffer is (over)written with the sum of ``terms`` first (fused loss)."""
+    hist = state["hist"]
+    if _native(hist):
+        lib = _lib.load()
+        arr = (ctypes.c_void_p * max(1, len(counters)))(*[c.data_ptr() for c in counters])
+        rc = lib.tdq_step_book(_lib.ptr(loss), _lib.ptr(terms) if terms.numel() else None, int(terms.numel()),
+                               int(bool(sum_terms)),
+                               _lib.ptr(hist), int(hist.shape[0]), _lib.ptr(state["epoch"]),
+                               _lib.ptr(state["best_loss"]), _lib.ptr(state["best_epoch"]),
+                               _lib.ptr(state["improved"]), ctypes.cast(arr, ctypes.c_void_p), len(counters),
+                               _lib.stream_ptr(hist.device))
+        _lib.check(rc, "tdq_step_book")
+        return
+    if hist.is_cuda:
+        _lib.require_on_gpu()
+    with torch.no_grad():
+        ep = state["epoch"]
+        if sum_terms:
+            s = torch.zeros((), device=terms.device)
+            for t in terms.reshape(-1):
+                s = s + t
+            loss.copy_(s.reshape(loss.shape))
+        lv = loss.reshape(()).float()
+        row = torch.cat([lv.reshape(1), terms.reshape(-1).float()])
+        hist.index_copy_(0, ep.reshape(1), row.unsqueeze(0))
+        imp = lv < state["best_loss"]
+        state["improved"].copy_(imp.to(state["improved"].dtype))
+        state["best_epoch"].copy_(torch.where(imp, ep, state["best_epoch"]))
+        state["best_loss"].copy_(torch.where(imp, lv, state["best_loss"]))
+        for c in counters:
+            c.add_(1.0)
+        ep.add_(1)
 
 
 def best_track(loss, best_loss, flat, best_flat, best_epoch, epoch):

@@ -258,3 +258,44 @@ def test_mixed_plan_high_order_periodic():
     assert abs(a.losses[-1]["Total Loss"] - b.losses[-1]["Total Loss"]) / b.losses[-1]["Total Loss"] < 1e-3
     u, f = a.predict(np.random.rand(100, 2))
     assert np.isfinite(u).all() and np.isfinite(f).all()
+
+
+def test_step_book_and_adam_snapshot_match_torch():
+    """Native bookkeeping (history row, best loss/epoch, counters, epoch, summed total) and the
+    Adam-launch best-weights snapshot equal the torch fallback, over improving and non-improving steps."""
+    from tensordiffeq_amd.ops import fused
+
+    def run(device):
+        torch.manual_seed(0)
+        st = {"hist": torch.full((8, 4), float("nan"), device=device),
+              "epoch": torch.zeros((), dtype=torch.int64, device=device),
+              "best_loss": torch.full((), float("inf"), device=device),
+              "best_epoch": torch.full((), -1, dtype=torch.int64, device=device),
+              "improved": torch.zeros((), dtype=torch.int32, device=device),
+              "best_flat": torch.zeros(1001, device=device)}
+        cnt = [torch.zeros((), dtype=torch.float64, device=device) for _ in range(2)]
+        gen = torch.Generator().manual_seed(0)
+        p = torch.randn(1001, generator=gen).to(device)
+        m, v = torch.zeros_like(p), torch.zeros_like(p)
+        snaps = []
+        for step, terms in enumerate(([1.0, 2.0, 3.0], [0.5, 0.5, 0.5], [4.0, 0.0, 0.0], [0.1, 0.2, 0.3])):
+            tv = torch.tensor(terms, device=device)
+            loss = torch.zeros((), device=device)
+            fused.step_book(loss, tv, st, cnt, sum_terms=True)   # CPU tensors take the torch fallback
+            g = torch.randn(1001, generator=gen).to(device)
+            fused.adam_multi([(p, g, m, v, 1.0)], cnt[0], 0.005, 0.99, 0.999, 1e-7,
+                             snapshot=(st["best_flat"], st["improved"]))
+            snaps.append(st["best_flat"].clone())
+        return st, cnt, p, snaps
+
+    a = run("cuda")
+    b = run("cpu")
+    sa, sb = a[0], b[0]
+    assert torch.allclose(sa["hist"][:4].cpu(), sb["hist"][:4], equal_nan=True)
+    assert int(sa["epoch"]) == int(sb["epoch"]) == 4
+    assert float(sa["best_loss"]) == pytest.approx(float(sb["best_loss"])) == pytest.approx(0.6)
+    assert int(sa["best_epoch"]) == int(sb["best_epoch"]) == 3
+    assert [float(c) for c in a[1]] == [4.0, 4.0]
+    for x, y in zip(a[3], b[3]):
+        assert torch.allclose(x.cpu(), y, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(a[2].cpu(), b[2], rtol=1e-5, atol=1e-6)
