@@ -525,10 +525,11 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // (4 rows x 2 groups 8 rows apart, 8 words each) on 8 disjoint bank windows: conflict-free.
   constexpr int RS = 144;
   constexpr int IMG = 64 * RS;
-  // dK tile ownership: WT >= 4 -> wave w owns tile rows {w, w+4, ..} x all columns;
-  // WT = 2 -> one tile (w>>1, w&1) per wave
-  constexpr int NR = WT >= 4 ? WT / 4 : 1;
-  constexpr int NC = WT >= 4 ? WT : 1;
+  // dK tile ownership: the WT x WT output tiles split into 2 x 2 quadrants, wave w owns quadrant
+  // (w >> 1, w & 1): (WT/2)^2 tiles from WT/2 A and WT/2 B fragments per k-block (a 2 x 8 strip
+  // per wave would need 2 + 8 fragment loads for the same 16 tiles at WT = 8)
+  constexpr int NR = WT / 2;
+  constexpr int NC = WT / 2;
   constexpr int U1 = (4 * IMG) / 2;           // images, in floats
   constexpr int U2 = 4 * S * WT * 256;        // per-wave zb fragment stage (bf16 hi/lo)
   constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
@@ -548,8 +549,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const int Lh = d.n_hidden;
   float* gs = slab + (size_t)wg * Ptot;
   bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * 2 * 64 * 2);
-  auto dw_row = [](int wv, int r) { return WT >= 4 ? wv + 4 * r : (wv >> 1); };
-  auto dw_col = [](int wv, int c) { return WT >= 4 ? c : (wv & 1); };
+  auto dw_row = [](int wv, int r) { return (WT / 2) * (wv >> 1) + r; };
+  auto dw_col = [](int wv, int c) { return (WT / 2) * (wv & 1) + c; };
   // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
   const int tr_row = 8 * g + ((l & 15) >> 2), tr_col = 4 * (l & 3);
   const int swz = (g & 1) << 6;  // bit 3 of every row this lane's transposed reads touch
