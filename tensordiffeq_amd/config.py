@@ -14,6 +14,8 @@ metrics_path           TDQ_METRICS                 JSONL metrics file (rank-suff
 graphs                 TDQ_NO_GRAPH=1 disables     HIP-graph capture of the training step
 fused_loss             TDQ_FUSED_LOSS=0 disables   single-kernel loss program
 allow_torch_fallback   TDQ_ALLOW_TORCH_FALLBACK    1: let GPU runs fall back to torch ops
+lbfgs                  TDQ_LBFGS                   auto (device on GPU, host on CPU) | device
+                                                   (GPU-resident kernels, graph-replayed) | host
 =====================  ==========================  =========================================
 """
 from __future__ import annotations
@@ -40,6 +42,7 @@ class SolverConfig:
     graphs: bool = True
     fused_loss: bool = True
     allow_torch_fallback: bool = False
+    lbfgs: str = "auto"
 
     @classmethod
     def from_env(cls, **overrides):
@@ -55,6 +58,7 @@ class SolverConfig:
             "graphs": not _env_bool("TDQ_NO_GRAPH", False),
             "fused_loss": _env_bool("TDQ_FUSED_LOSS", True),
             "allow_torch_fallback": _env_bool("TDQ_ALLOW_TORCH_FALLBACK", False),
+            "lbfgs": e.get("TDQ_LBFGS", cls.lbfgs),
         }
         vals.update({k: v for k, v in overrides.items() if v is not None})
         cfg = cls(**vals)
@@ -68,6 +72,8 @@ class SolverConfig:
             raise ValueError(f"precision {self.precision!r}")
         if self.log_every < 1:
             raise ValueError("log_every must be >= 1")
+        if self.lbfgs not in ("auto", "device", "host"):
+            raise ValueError(f"lbfgs {self.lbfgs!r}")
 
     def apply_process_env(self):
         """Push the process-wide switches that the kernels / engines read."""

@@ -516,7 +516,7 @@ template <int WT, int S, int NSO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
-                   int Ptot, NetDims d, JetSpec sp) {
+                   int Ptot, NetDims d, JetSpec sp, int rev) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int W = 16 * WT;
   constexpr int KB = WT / 2;
@@ -541,7 +541,9 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wg = blockIdx.x, nwg = gridDim.x;
+  // rev: tiles in reverse dispatch order - the forward wrote the highest tiles last, so theirs are
+  // the saved activations still resident in the 256 MiB Infinity Cache when the backward starts
+  const int nwg = gridDim.x, wg = rev ? nwg - 1 - (int)blockIdx.x : (int)blockIdx.x;
   const int n = wg * 64 + w * 16 + p;
   const bool valid = n < N;
   const int nc = valid ? n : N - 1;
@@ -773,6 +775,15 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 // ------------------------------------------------------------------------------------------
 inline size_t fwd_bf3_lds(int WT, int S) { return (size_t)4 * S * WT * 1024; }
 
+// backward tile order: reverse (default) or dispatch order (TDQ_BWD_ORDER=forward, for A/B runs)
+inline int bwd_reverse_order() {
+  static const int rev = [] {
+    const char* e = getenv("TDQ_BWD_ORDER");
+    return (e != nullptr && e[0] == 'f') ? 0 : 1;
+  }();
+  return rev;
+}
+
 inline size_t bwd_bf3_lds(int WT, int S) {
   const int W = 16 * WT;
   const size_t u1 = (size_t)(4 * 64 * 144) / 2, u2 = (size_t)4 * S * WT * 256;
@@ -821,7 +832,7 @@ int launch_bwd_bf3(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
-                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp);
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order());
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -116,10 +116,9 @@ int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int
 int64_t tdq_jet_bf3_slab_floats(int N, int d_in, int width, int d_out, int n_hidden) {
   const int WT = width_tiles(width);
   if (WT < 2) return -1;
-  const int64_t nwg = (N + 63) / 64;
-  const int64_t P = param_count(d_in, width, d_out, n_hidden);
-  const int64_t chunks = nwg < 32 ? nwg : 32;
-  return nwg * P + chunks * P;
+  const int nwg = (N + 63) / 64;
+  const int64_t P = slab_stride(param_count(d_in, width, d_out, n_hidden));
+  return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
 
 int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
@@ -153,14 +152,15 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nwg = (N + 63) / 64;
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
-  const int chunks = nwg < 32 ? nwg : 32;
+  const int chunks = slab_chunks(nwg);
   float* slab = work;
   // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
   const float* img = Hs + (int64_t)n_hidden * nwg * S * 4 * WT * 256 + img_floats(WT, n_hidden);
   const float* aux = img + img_floats(WT, n_hidden);
   (void)P;
-  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), dJ, nullptr, const_cast<float*>(Hs), slab, N, Ptot, d,
-            sp, st};
+  // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
+  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), dJ, nullptr, const_cast<float*>(Hs), slab, N,
+            slab_stride(Ptot), d, sp, st};
   int rc = dispatch(false, WT, S, nso, a);
   if (rc) return rc;
   return tdq_slab_reduce(work, grad, nwg, Ptot, chunks, stream);

@@ -80,4 +80,12 @@ static inline int spec_nso(int S, const int* spec) {
   return nso;
 }
 
-extern "C" int tdq_slab_reduce(float* work, float* grad, int nwg, int Ptot, int chunks, void* stream);
+// per-workgroup gradient slab row stride: parameter count rounded up to 4 floats, so every slab
+// row is 16-byte aligned for the float4 reduction
+static inline int slab_stride(int P) { return (P + 3) & ~3; }
+
+// workgroup-chunk count of the first reduction pass
+static inline int slab_chunks(int nwg) { return nwg < 16 ? nwg : 16; }
+
+// slabs [nwg][slab_stride(P)] at work, partials [chunks][slab_stride(P)] right after -> grad[P]
+extern "C" int tdq_slab_reduce(float* work, float* grad, int nwg, int P, int chunks, void* stream);

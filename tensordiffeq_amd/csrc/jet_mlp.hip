@@ -593,32 +593,45 @@ jet_bwd_kernel(const float* __restrict__ X, const float* __restrict__ P, const f
   }
 }
 
-// deterministic slab reduction: pass 1 sums chunks of workgroups, pass 2 sums the chunks
+// deterministic slab reduction (fixed summation order): pass 1 sums chunks of workgroups, one
+// float4 column per thread with four independent 16-byte loads in flight; pass 2 sums the chunks
 __global__ void __launch_bounds__(256) slab_reduce1(const float* __restrict__ slab, float* __restrict__ part,
-                                                    int nwg, int Ptot, int chunks) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+                                                    int nwg, int Pst, int chunks) {
+  const int q = blockIdx.x * 256 + threadIdx.x;  // float4 column
   const int c = blockIdx.y;
-  if (k >= Ptot) return;
+  if (4 * q >= Pst) return;
   const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab) + q;
+  const size_t row = (size_t)(Pst >> 2);
+  f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();
   int wgi = lo;
   for (; wgi + 3 < hi; wgi += 4) {
-    a0 += slab[(size_t)wgi * Ptot + k];
-    a1 += slab[(size_t)(wgi + 1) * Ptot + k];
-    a2 += slab[(size_t)(wgi + 2) * Ptot + k];
-    a3 += slab[(size_t)(wgi + 3) * Ptot + k];
+    a0 += s4[(size_t)wgi * row];
+    a1 += s4[(size_t)(wgi + 1) * row];
+    a2 += s4[(size_t)(wgi + 2) * row];
+    a3 += s4[(size_t)(wgi + 3) * row];
   }
-  for (; wgi < hi; ++wgi) a0 += slab[(size_t)wgi * Ptot + k];
-  part[(size_t)c * Ptot + k] = (a0 + a1) + (a2 + a3);
+  for (; wgi < hi; ++wgi) a0 += s4[(size_t)wgi * row];
+  reinterpret_cast<f32x4*>(part)[(size_t)c * row + q] = (a0 + a1) + (a2 + a3);
 }
 
-__global__ void __launch_bounds__(256) slab_reduce2(const float* __restrict__ part, float* __restrict__ grad,
-                                                    int Ptot, int chunks) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= Ptot) return;
-  float a = 0.f;
-  for (int c = 0; c < chunks; ++c) a += part[(size_t)c * Ptot + k];
-  grad[k] = a;
+__global__ void __launch_bounds__(256) slab_reduce2(const float* __restrict__ part, float* __restrict__ grad, int P,
+                                                    int Pst, int chunks) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (4 * q >= P) return;
+  const f32x4* p4 = reinterpret_cast<const f32x4*>(part) + q;
+  const size_t row = (size_t)(Pst >> 2);
+  f32x4 a0 = zero4(), a1 = zero4();
+  int c = 0;
+  for (; c + 1 < chunks; c += 2) {
+    a0 += p4[(size_t)c * row];
+    a1 += p4[(size_t)(c + 1) * row];
+  }
+  if (c < chunks) a0 += p4[(size_t)c * row];
+  const f32x4 a = a0 + a1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (4 * q + e < P) grad[4 * q + e] = a[e];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -728,11 +741,11 @@ int64_t tdq_jet_scratch_floats(int N, int width, int n_hidden, int S, int unused
 int64_t tdq_jet_slab_floats(int N, int d_in, int width, int d_out, int n_hidden) {
   const int WT = width_tiles(width);
   if (WT < 0) return -1;
-  const int64_t nwg = (N + 63) / 64;
-  const int64_t P = param_count(d_in, width, d_out, n_hidden);
-  const int64_t chunks = nwg < 32 ? nwg : 32;
+  const int nwg = (N + 63) / 64;
+  const int64_t P = slab_stride(param_count(d_in, width, d_out, n_hidden));
+  const int64_t chunks = slab_chunks(nwg);
   const int64_t W = 16 * WT;
-  return nwg * P + chunks * P + (int64_t)(n_hidden > 1 ? n_hidden - 1 : 0) * W * W;
+  return (int64_t)nwg * P + chunks * P + (int64_t)(n_hidden > 1 ? n_hidden - 1 : 0) * W * W;
 }
 
 int tdq_jet_fwd(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
@@ -763,29 +776,31 @@ int tdq_jet_bwd(const float* X, const float* P, const float* dJ, const float* Zs
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nwg = (N + 63) / 64;
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
-  const int chunks = nwg < 32 ? nwg : 32;
+  const int Pst = slab_stride(Ptot);
+  const int chunks = slab_chunks(nwg);
   float* slab = work;
-  float* part = work + (size_t)nwg * Ptot;
-  float* Kp = part + (size_t)chunks * Ptot;
+  float* part = work + (size_t)nwg * Pst;
+  float* Kp = part + (size_t)chunks * Pst;
   int rc = launch_pad(P, Kp, d, 16 * WT, 0, st);
   if (rc) return rc;
   {
-    auto run = [&]() -> int { TDQ_DISPATCH(launch_bwd, X, P, Kp, dJ, Zs, slab, N, Ptot, d, sp, st) };
+    auto run = [&]() -> int { TDQ_DISPATCH(launch_bwd, X, P, Kp, dJ, Zs, slab, N, Pst, d, sp, st) };
     rc = run();
   }
   if (rc) return rc;
   return tdq_slab_reduce(work, grad, nwg, Ptot, chunks, stream);
 }
 
-// slabs [nwg][Ptot] at work, partials [chunks][Ptot] right after them -> grad[Ptot]
-int tdq_slab_reduce(float* work, float* grad, int nwg, int Ptot, int chunks, void* stream) {
+int tdq_slab_reduce(float* work, float* grad, int nwg, int P, int chunks, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int Pst = slab_stride(P);
+  const int nq = Pst / 4;
   float* slab = work;
-  float* part = work + (size_t)nwg * Ptot;
-  dim3 g1((Ptot + 255) / 256, chunks);
-  hipLaunchKernelGGL(slab_reduce1, g1, dim3(256), 0, st, slab, part, nwg, Ptot, chunks);
+  float* part = work + (size_t)nwg * Pst;
+  dim3 g1((nq + 255) / 256, chunks);
+  hipLaunchKernelGGL(slab_reduce1, g1, dim3(256), 0, st, slab, part, nwg, Pst, chunks);
   TDQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce2, dim3((Ptot + 255) / 256), dim3(256), 0, st, part, grad, Ptot, chunks);
+  hipLaunchKernelGGL(slab_reduce2, dim3((nq + 255) / 256), dim3(256), 0, st, part, grad, P, Pst, chunks);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

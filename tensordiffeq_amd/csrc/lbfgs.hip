@@ -1,0 +1,448 @@
+// Device-resident L-BFGS for gfx950.
+//
+// The reference runs the lua-port L-BFGS on the host (tensordiffeq/optimizers.py:107-308): a
+// two-loop recursion of ~200 tiny TF ops over <= 50 history pairs, several device->host syncs and
+// a numpy weight round-trip per iteration.  Here one iteration is five small kernels that live in
+// the same HIP graph as the loss/gradient evaluation, and the host reads nothing until it polls
+// the "active" flag every few dozen iterations:
+//
+//   lbfgs_dots   grid (chunks, m + 1): every dot product the iteration needs in ONE pass over the
+//                history ring - per slot i: s_i.g, y_i.g, s_i.y, y_i.y, s.y_i - and for the new pair
+//                s.y, y.y, s.g, y.g plus |g|_1 (s = t d, y = g - g_old formed on the fly); fp64
+//                partial sums per chunk;
+//   lbfgs_logic  one workgroup: reduces the partials in fixed order, runs the post-evaluation tests
+//                (NaN, best iterate, maxIter / maxEval, tolFun / tolX / |f - f_old|), the curvature
+//                test y.s > 1e-10 with ring push (H0 = y.s / y.y), keeps S^T Y and Y^T Y current by
+//                one new row + column per push, and turns the compact representation of Byrd,
+//                Nocedal & Schnabel (1994) into per-slot coefficients with two k x k triangular
+//                solves (one lane per history pair, R and Y^T Y in LDS);
+//   lbfgs_dir    elementwise: stores the pushed pair into the ring, d = cG g + sum_i (cS_i s_i +
+//                cY_i y_i), g_old = g, best-weights snapshot, partials of g.d and |d|_1;
+//   lbfgs_step   one workgroup: descent test g.d > -tolX, step t = min(1, 1/|g|_1) on the first
+//                iteration else the fixed learning rate (0.8, reference fit.py:67), f_old = f;
+//   lbfgs_axpy   x += t d (launched in front of the next evaluation).
+//
+// All scalar state is fp64 in one small device array (layout LB_* below, mirrored by
+// tensordiffeq_amd/optimizers/lbfgs_device.py).  Once a stopping test fires every kernel is a
+// no-op, so graph replays past convergence change nothing.
+#include "common.h"
+
+#define LB_MAXM 64
+#define LB_NF 5
+
+enum {
+  LB_ACTIVE = 0,  // 1 while iterating
+  LB_NITER,       // reference nIter
+  LB_FEVAL,       // reference currentFuncEval (the initial evaluation included)
+  LB_K,           // valid history pairs
+  LB_HEAD,        // ring slot of the oldest pair
+  LB_PUSHED,      // the current iteration pushed a pair ...
+  LB_SLOT,        // ... into this slot
+  LB_BEST,        // snapshot x into best_x in the next lbfgs_dir
+  LB_F,           // loss at the current x
+  LB_FOLD,        // loss before the last step
+  LB_MINLOSS,     // best loss so far
+  LB_BESTEP,      // epoch of the best loss (-1 = initial point)
+  LB_HDIAG,       // H0 scale y.s / y.y
+  LB_T,           // step length of the current direction
+  LB_DT1,         // |d|_1 * t
+  LB_G1,          // |g|_1 at the current x
+  LB_REASON,      // why the run stopped (0 = running)
+  LB_GTD,         // g.d of the current direction
+  LB_NST = 24
+};
+
+enum { LB_R_RUN = 0, LB_R_TOLFUN0 = 1, LB_R_NAN = 2, LB_R_MAXITER = 3, LB_R_TOL = 4, LB_R_GTD = 5 };
+
+struct LbCfg {
+  int p;            // parameters
+  int m;            // history size (<= LB_MAXM)
+  int max_iter;
+  int nchunks;      // lbfgs_dots chunks
+  int nblk;         // lbfgs_dir blocks
+  int fhist_len;    // length of the loss history buffer (0: none)
+  double max_eval;  // 1.25 max_iter (reference optimizers.py:113)
+  double lr;        // fixed step (0.8)
+  double tol_fun;
+  double tol_x;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// 256-thread block sum of NV doubles; the result is valid in thread 0
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = wave_sum(v[q]);
+  if (l == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[w * NV + q] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = ((red[q] + red[NV + q]) + red[2 * NV + q]) + red[3 * NV + q];
+}
+
+__device__ __forceinline__ bool slot_valid(int i, int head, int k, int m) { return ((i - head + m) % m) < k; }
+
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lbfgs_dots_kernel(const float* __restrict__ fg, const float* __restrict__ g_old,
+                                                         const float* __restrict__ d, const float* __restrict__ S,
+                                                         const float* __restrict__ Y, const double* __restrict__ st,
+                                                         double* __restrict__ part, LbCfg c) {
+  __shared__ double red[4 * LB_NF];
+  const int i = blockIdx.y, ch = blockIdx.x;
+  const int lo = (int)(((long long)c.p * ch) / c.nchunks), hi = (int)(((long long)c.p * (ch + 1)) / c.nchunks);
+  const float tf = (float)st[LB_T];
+  const int k = (int)st[LB_K], head = (int)st[LB_HEAD];
+  const bool run = st[LB_ACTIVE] != 0.0 && (i == c.m || slot_valid(i, head, k, c.m));
+  double a[LB_NF] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (run) {
+    if (i == c.m) {
+      for (int j = lo + (int)threadIdx.x; j < hi; j += 256) {
+        const float g = fg[j];
+        const float s = tf * d[j], y = g - g_old[j];
+        a[0] += (double)s * y;
+        a[1] += (double)y * y;
+        a[2] += (double)s * g;
+        a[3] += (double)y * g;
+        a[4] += fabs((double)g);
+      }
+    } else {
+      const float* Si = S + (size_t)i * c.p;
+      const float* Yi = Y + (size_t)i * c.p;
+      for (int j = lo + (int)threadIdx.x; j < hi; j += 256) {
+        const float g = fg[j];
+        const float s = tf * d[j], y = g - g_old[j];
+        const double si = Si[j], yi = Yi[j];
+        a[0] += si * g;
+        a[1] += yi * g;
+        a[2] += si * y;
+        a[3] += yi * y;
+        a[4] += (double)s * yi;
+      }
+    }
+  }
+  block_sum<LB_NF>(a, red);
+  if (threadIdx.x == 0) {
+    double* o = part + ((size_t)ch * (c.m + 1) + i) * LB_NF;
+#pragma unroll
+    for (int q = 0; q < LB_NF; ++q) o[q] = a[q];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dynamic LDS (doubles): dots[(m+1)*5] | Rc[m*m] | YYc[m*m] | aC[64] | bC[64] | uS[64] | pS[64]
+__global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restrict__ fg, const double* __restrict__ part,
+                                                          double* __restrict__ st, double* __restrict__ SY,
+                                                          double* __restrict__ YY, double* __restrict__ coef,
+                                                          float* __restrict__ fhist, LbCfg c) {
+  extern __shared__ __attribute__((aligned(16))) double lb_lds[];
+  __shared__ int flag[6];  // go, n_iter, pushed, slot, k, head
+  const int tid = threadIdx.x, m = c.m;
+  double* dots = lb_lds;
+  double* Rc = dots + (m + 1) * LB_NF;
+  double* YYc = Rc + m * m;
+  double* aC = YYc + m * m;
+  double* bC = aC + 64;
+  double* uS = bC + 64;
+  double* pS = uS + 64;
+  if (st[LB_ACTIVE] == 0.0) {
+    if (tid == 0) st[LB_BEST] = 0.0;
+    return;
+  }
+  // 1. reduce the chunk partials (fixed order: deterministic)
+  for (int v = tid; v < (m + 1) * LB_NF; v += 256) {
+    double a0 = 0.0, a1 = 0.0;
+    int ch = 0;
+    for (; ch + 1 < c.nchunks; ch += 2) {
+      a0 += part[(size_t)ch * (m + 1) * LB_NF + v];
+      a1 += part[(size_t)(ch + 1) * (m + 1) * LB_NF + v];
+    }
+    if (ch < c.nchunks) a0 += part[(size_t)ch * (m + 1) * LB_NF + v];
+    dots[v] = a0 + a1;
+  }
+  __syncthreads();
+  // 2. post-evaluation tests of the previous step (reference optimizers.py:241-296, with the
+  //    B9 fixes of eager_lbfgs), then the curvature test and ring push (optimizers.py:168-185)
+  if (tid == 0) {
+    const double* sc = dots + m * LB_NF;  // s.y, y.y, s.g, y.g, |g|_1
+    const double f = (double)fg[c.p];
+    int n_iter = (int)st[LB_NITER];
+    int best = 0, done = 0, reason = LB_R_RUN;
+    double minloss = st[LB_MINLOSS];
+    st[LB_G1] = sc[4];
+    if (n_iter == 0) {
+      if (fhist != nullptr && c.fhist_len > 0) fhist[0] = (float)f;
+      if (isfinite(f)) {
+        best = 1;
+        minloss = f;
+        st[LB_BESTEP] = -1.0;
+      }
+      if (sc[4] <= c.tol_fun) {
+        done = 1;
+        reason = LB_R_TOLFUN0;
+      }
+    } else {
+      const double fe = st[LB_FEVAL] + 1.0;
+      st[LB_FEVAL] = fe;
+      if (fhist != nullptr && n_iter < c.fhist_len) fhist[n_iter] = (float)f;
+      if (isnan(f)) {
+        done = 1;
+        reason = LB_R_NAN;
+      } else {
+        if (f < minloss) {
+          best = 1;
+          minloss = f;
+          st[LB_BESTEP] = (double)(n_iter - 1);
+        }
+        if (n_iter >= c.max_iter || fe >= c.max_eval) {
+          done = 1;
+          reason = LB_R_MAXITER;
+        } else if (sc[4] <= c.tol_fun || st[LB_DT1] <= c.tol_x || fabs(f - st[LB_FOLD]) < c.tol_x) {
+          done = 1;
+          reason = LB_R_TOL;
+        }
+      }
+    }
+    st[LB_F] = f;
+    st[LB_MINLOSS] = minloss;
+    st[LB_BEST] = (double)best;
+    int pushed = 0, slot = -1;
+    int k = (int)st[LB_K], head = (int)st[LB_HEAD];
+    if (done) {
+      st[LB_ACTIVE] = 0.0;
+      st[LB_REASON] = (double)reason;
+    } else {
+      n_iter += 1;
+      st[LB_NITER] = (double)n_iter;
+      if (n_iter > 1) {
+        const double ys = sc[0], yy = sc[1];
+        if (ys > 1e-10) {
+          if (k == m) {
+            slot = head;
+            head = (head + 1) % m;
+          } else {
+            slot = (head + k) % m;
+            k += 1;
+          }
+          st[LB_K] = (double)k;
+          st[LB_HEAD] = (double)head;
+          st[LB_HDIAG] = ys / yy;
+          SY[slot * m + slot] = ys;
+          YY[slot * m + slot] = yy;
+          pushed = 1;
+        }
+      }
+    }
+    st[LB_PUSHED] = (double)pushed;
+    st[LB_SLOT] = (double)slot;
+    flag[0] = !done;
+    flag[1] = n_iter;
+    flag[2] = pushed;
+    flag[3] = slot;
+    flag[4] = k;
+    flag[5] = head;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const int n_iter = flag[1], pushed = flag[2], slot = flag[3], k = flag[4], head = flag[5];
+  const double gam = n_iter == 1 ? 1.0 : st[LB_HDIAG];
+  if (n_iter == 1 || k == 0) {  // d = -H0 g (first iteration: H0 = I)
+    for (int v = tid; v < 2 * m; v += 256) coef[v] = 0.0;
+    if (tid == 0) coef[2 * m] = -gam;
+    return;
+  }
+  // 3. new row / column of S^T Y and Y^T Y (physical slot indices; every other valid slot was
+  //    valid before the push, so its dots are current)
+  if (pushed && tid < m && tid != slot && slot_valid(tid, head, k, m)) {
+    const double* dj = dots + tid * LB_NF;
+    SY[slot * m + tid] = dj[4];  // s_new . y_j
+    SY[tid * m + slot] = dj[2];  // s_j . y_new
+    YY[tid * m + slot] = dj[3];
+    YY[slot * m + tid] = dj[3];
+  }
+  __syncthreads();
+  // 4. chronological k x k blocks and right-hand sides into LDS
+  for (int e = tid; e < k * k; e += 256) {
+    const int a = e / k, b = e - a * k;
+    const int ia = (head + a) % m, ib = (head + b) % m;
+    Rc[a * m + b] = a <= b ? SY[ia * m + ib] : 0.0;
+    YYc[a * m + b] = YY[ia * m + ib];
+  }
+  if (tid < k) {
+    const int ij = (head + tid) % m;
+    const bool nw = pushed && ij == slot;
+    aC[tid] = nw ? dots[m * LB_NF + 2] : dots[ij * LB_NF + 0];  // s_j . g
+    bC[tid] = nw ? dots[m * LB_NF + 3] : dots[ij * LB_NF + 1];  // y_j . g
+  }
+  __syncthreads();
+  // 5. compact product on wave 0 (lane j = chronological pair j):
+  //    R u = S^T g ; rhs = D u + gam Y^T Y u - gam Y^T g ; R^T p1 = rhs ;
+  //    H g = gam g + S p1 - gam Y u   ->   d = -H g
+  if (tid < 64) {
+    const int j = tid;
+    double r = j < k ? aC[j] : 0.0, u = 0.0;
+    for (int q = k - 1; q >= 0; --q) {  // back substitution
+      const double uq = __shfl(r, q, 64) / Rc[q * m + q];
+      if (j == q) u = uq;
+      if (j < q) r -= Rc[j * m + q] * uq;
+    }
+    uS[j] = j < k ? u : 0.0;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int j = tid;
+    double rhs = 0.0;
+    if (j < k) {
+      double yu = 0.0;
+      for (int q = 0; q < k; ++q) yu += YYc[j * m + q] * uS[q];
+      rhs = Rc[j * m + j] * uS[j] + gam * yu - gam * bC[j];
+    }
+    double rr = rhs, p1 = 0.0;
+    for (int q = 0; q < k; ++q) {  // forward substitution with R^T
+      const double pq = __shfl(rr, q, 64) / Rc[q * m + q];
+      if (j == q) p1 = pq;
+      if (j > q && j < k) rr -= Rc[q * m + j] * pq;
+    }
+    pS[j] = j < k ? p1 : 0.0;
+  }
+  __syncthreads();
+  for (int v = tid; v < m; v += 256) {  // per PHYSICAL slot
+    const int cidx = (v - head + m) % m;
+    const bool in = cidx < k;
+    coef[v] = in ? -pS[cidx] : 0.0;
+    coef[m + v] = in ? gam * uS[cidx] : 0.0;
+  }
+  if (tid == 0) coef[2 * m] = -gam;
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lbfgs_dir_kernel(const float* __restrict__ x, const float* __restrict__ fg,
+                                                        float* __restrict__ g_old, float* __restrict__ d,
+                                                        float* __restrict__ S, float* __restrict__ Y,
+                                                        float* __restrict__ best_x, const double* __restrict__ st,
+                                                        const double* __restrict__ coef, double* __restrict__ part2,
+                                                        LbCfg c) {
+  __shared__ double red[8];
+  const bool best = st[LB_BEST] != 0.0, active = st[LB_ACTIVE] != 0.0;
+  const int n_iter = (int)st[LB_NITER], pushed = (int)st[LB_PUSHED], slot = (int)st[LB_SLOT];
+  const int k = (int)st[LB_K], head = (int)st[LB_HEAD], m = c.m;
+  const float tf = (float)st[LB_T];
+  const double cG = coef[2 * m];
+  double acc[2] = {0.0, 0.0};
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < c.p; j += gridDim.x * 256) {
+    if (best) best_x[j] = x[j];
+    if (!active) continue;
+    const float g = fg[j];
+    double dn = cG * g;
+    if (n_iter > 1) {
+      const float s = tf * d[j], y = g - g_old[j];
+      if (pushed) {
+        S[(size_t)slot * c.p + j] = s;
+        Y[(size_t)slot * c.p + j] = y;
+      }
+      for (int q = 0; q < k; ++q) {
+        const int i = (head + q) % m;
+        const bool nw = pushed && i == slot;
+        const double si = nw ? (double)s : (double)S[(size_t)i * c.p + j];
+        const double yi = nw ? (double)y : (double)Y[(size_t)i * c.p + j];
+        dn += coef[i] * si + coef[m + i] * yi;
+      }
+    }
+    const float df = (float)dn;
+    g_old[j] = g;
+    d[j] = df;
+    acc[0] += (double)g * df;
+    acc[1] += fabs((double)df);
+  }
+  block_sum<2>(acc, red);
+  if (threadIdx.x == 0) {
+    part2[2 * blockIdx.x] = acc[0];
+    part2[2 * blockIdx.x + 1] = acc[1];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lbfgs_step_kernel(const double* __restrict__ part2, double* __restrict__ st,
+                                                         LbCfg c) {
+  __shared__ double red[8];
+  if (st[LB_ACTIVE] == 0.0) return;
+  double acc[2] = {0.0, 0.0};
+  for (int b = threadIdx.x; b < c.nblk; b += 256) {
+    acc[0] += part2[2 * b];
+    acc[1] += part2[2 * b + 1];
+  }
+  block_sum<2>(acc, red);
+  if (threadIdx.x == 0) {
+    const double gtd = acc[0];
+    st[LB_GTD] = gtd;
+    if (gtd > -c.tol_x) {  // cannot make progress along d (reference optimizers.py:224)
+      st[LB_ACTIVE] = 0.0;
+      st[LB_REASON] = (double)LB_R_GTD;
+      return;
+    }
+    const double t = ((int)st[LB_NITER] == 1) ? fmin(1.0, 1.0 / st[LB_G1]) : c.lr;
+    st[LB_T] = t;
+    st[LB_DT1] = acc[1] * t;
+    st[LB_FOLD] = st[LB_F];
+  }
+}
+
+__global__ void __launch_bounds__(256) lbfgs_axpy_kernel(float* __restrict__ x, const float* __restrict__ d,
+                                                         const double* __restrict__ st, int p) {
+  if (st[LB_ACTIVE] == 0.0) return;
+  const float tf = (float)st[LB_T];
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < p; j += gridDim.x * 256) x[j] = fmaf(tf, d[j], x[j]);
+}
+
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+int tdq_lbfgs_nst() { return LB_NST; }
+
+// After an evaluation at x (fg = [g | f]): dots -> logic -> dir -> step.
+//   part: nchunks * (m + 1) * 5 doubles, part2: 2 * nblk doubles, SY / YY: m * m doubles,
+//   coef: 2 m + 1 doubles, S / Y: m * p floats, fhist: fhist_len floats (or null).
+int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
+                     double* st, double* SY, double* YY, double* coef, double* part, double* part2, float* fhist,
+                     int p, int m, int max_iter, int nchunks, int nblk, int fhist_len, double max_eval, double lr,
+                     double tol_fun, double tol_x, void* stream) {
+  if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
+  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m + 4 * 64) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgs_logic_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(((LB_MAXM + 1) * LB_NF + 2 * LB_MAXM * LB_MAXM + 4 * 64) * sizeof(double)));
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(lbfgs_dots_kernel, dim3(nchunks, m + 1), dim3(256), 0, s, fg, g_old, d, S, Y, st, part, c);
+  TDQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lbfgs_logic_kernel, dim3(1), dim3(256), lds, s, fg, part, st, SY, YY, coef, fhist, c);
+  TDQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lbfgs_dir_kernel, dim3(nblk), dim3(256), 0, s, x, fg, g_old, d, S, Y, best_x, st, coef, part2,
+                     c);
+  TDQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lbfgs_step_kernel, dim3(1), dim3(256), 0, s, part2, st, c);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// x += t d (a no-op once the run has stopped)
+int tdq_lbfgs_axpy(float* x, const float* d, const double* st, int p, int nblk, void* stream) {
+  if (p <= 0 || nblk < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(lbfgs_axpy_kernel, dim3(nblk), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, d, st, p);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -318,6 +318,11 @@ class LossGradEngine:
         buf = torch.cat([g.reshape(-1), loss.detach().reshape(1)])
         return buf
 
+    def evaluate_fg(self):
+        """``[grad | loss]`` at the CURRENT flat parameters (nothing copied in, not all-reduced):
+        the objective of the device L-BFGS, captured inside its HIP graph."""
+        return self._body()
+
     def __call__(self, x):
         with torch.no_grad():
             self.flat.copy_(x)

@@ -411,6 +411,14 @@ class CollocationSolverND:
             terms = {t.name: v for t, v in zip(self.program().terms, row[1:])}
         self.metrics.log(phase, ep, loss, terms)
 
+    def _use_device_lbfgs(self):
+        """Device-resident L-BFGS (``optimizers/lbfgs_device.py``) by default on a GPU; the
+        host-driven port elsewhere.  ``TDQ_LBFGS`` / ``SolverConfig.lbfgs`` overrides."""
+        impl = getattr(getattr(self, "config", None), "lbfgs", "auto")
+        if impl == "auto":
+            return self.device.type == "cuda"
+        return impl == "device"
+
     def _fit_lbfgs(self, newton_iter, newton_eager):
         ctx = self.dist_ctx
         if self.verbose and ctx.rank == 0:
@@ -427,7 +435,29 @@ class CollocationSolverND:
                 bar.set_postfix(loss=f)
                 bar.refresh()
 
-        if newton_eager:
+        if newton_eager and self._use_device_lbfgs():
+            from ..fit import _use_graphs
+            from ..optimizers import lbfgs_device
+
+            def on_poll(opt):
+                it = opt.n_iter
+                f = float(opt.st[lbfgs_device.F])
+                if self.metrics is not None:
+                    self.metrics.log("lbfgs", it, f)
+                bar.n = min(it, newton_iter)
+                bar.set_postfix(loss=f)
+                bar.refresh()
+
+            opt = lbfgs_device.minimize(eng.evaluate_fg, flat.data, newton_iter, lr=0.8,
+                                        all_reduce=ctx.all_reduce_ if ctx.is_distributed else None,
+                                        use_graph=_use_graphs(self.device),
+                                        poll_every=max(1, min(int(self.log_every), 64)), on_poll=on_poll)
+            with torch.no_grad():
+                flat.copy_(opt.best_x)
+            self.min_loss["l-bfgs"] = opt.min_loss
+            self.best_epoch["l-bfgs"] = opt.best_epoch
+            self.lbfgs_state = opt
+        elif newton_eager:
             x, _, _, best_w, min_loss, best_epoch = eager_lbfgs(
                 eng, flat.detach().clone(), maxIter=newton_iter, learningRate=0.8, on_eval=on_eval)
             with torch.no_grad():

@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lock = threading.Lock()
 _lib = None
@@ -32,7 +32,7 @@ class NativeUnavailable(RuntimeError):
 
 def _declare(lib):
     c = ctypes
-    P, I, F, L = c.c_void_p, c.c_int, c.c_float, c.c_int64
+    P, I, F, L, D = c.c_void_p, c.c_int, c.c_float, c.c_int64, c.c_double
     sig = {
         "tdq_abi_version": (I, []),
         "tdq_jet_fwd": (I, [P, P, P, P, I, I, I, I, I, I, P, P]),
@@ -48,6 +48,9 @@ def _declare(lib):
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
         "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, I, P]),
         "tdq_loss_meta_sizes": (I, [P]),
+        "tdq_lbfgs_nst": (I, []),
+        "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [P]),
+        "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
