@@ -212,6 +212,49 @@ __device__ __forceinline__ size_t hs_base(int layer, int nwg, int wg, int S, int
 }
 __device__ __forceinline__ int hs_off(int s, int t, int WT) { return (s * 4 * WT + t) * 256; }
 
+// layer 0 (input -> width, VALU; derivative streams are rows of K0): the post-activation streams of
+// feature tile t (forward).
+template <int WT, int S, int NSO>
+__device__ __forceinline__ void h0_jet(const JetSpec& sp, const float* __restrict__ aux, const NetDims& d,
+                                       const float* __restrict__ x, int t, int g, f32x4 (&h)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  const int f0 = 16 * t + 4 * g;
+  f32x4 z[S];
+  z[0] = *reinterpret_cast<const f32x4*>(aux + aux_b0(d, W) + f0);
+#pragma unroll
+  for (int j = 0; j < TDQ_MAXD; ++j)
+    if (j < d.d_in) z[0] += x[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+#pragma unroll
+  for (int s = 1; s < SO; ++s) z[s] = *reinterpret_cast<const f32x4*>(aux + sp.var[s] * W + f0);
+#pragma unroll
+  for (int s = SO; s < S; ++s) z[s] = zero4();
+  tanh_jet_f<S, NSO>(sp, z, h);
+}
+
+// Layer 0's derivative streams are functions of its value stream alone (z_a = a row of K0,
+// z_ab = 0): h_a = s1 K0[a], h_ab = -2 h s1 K0[a] K0[b], s1 = 1 - h^2.  With h0r set the forward
+// saves only the value stream of layer 0 and the backward rebuilds stream s here - 3/4 less
+// layer-0 saved-activation traffic (the step is bound by that traffic) for ~2 VALU ops per value.
+template <int WT, int S, int NSO>
+__device__ __forceinline__ f32x4 h0_stream(const JetSpec& sp, const float* __restrict__ aux, const f32x4& h, int t,
+                                           int g, int s) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  if (s == 0) return h;
+  const int f0 = 16 * t + 4 * g;
+  f32x4 r;
+  if (s < SO) {
+    const f32x4 k = *reinterpret_cast<const f32x4*>(aux + sp.var[s] * W + f0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = fmaf(-h[c], h[c], 1.f) * k[c];
+  } else {
+    const f32x4 ka = *reinterpret_cast<const f32x4*>(aux + sp.var[sp.ia[s]] * W + f0);
+    const f32x4 kb = *reinterpret_cast<const f32x4*>(aux + sp.var[sp.ib[s]] * W + f0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = (-2.f * h[c]) * fmaf(-h[c], h[c], 1.f) * (ka[c] * kb[c]);
+  }
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
@@ -290,7 +333,7 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
 template <int WT, int S, int NSO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
-                   float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp) {
+                   float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -304,8 +347,6 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // wave-private staging image of the next layer's B fragments: [s][kb][hl][lane][2 halves]
   bf16x4* stage = reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * 2 * 64 * 2);
   float* hlast = reinterpret_cast<float*>(stage);  // last layer: fp32 h image [s][t][lane][4]
-  const float* K0 = aux;
-  const float* b0 = aux + aux_b0(d, W);
   const float* Ko = aux + aux_ko(d, W);
 
   TDQ_TS(0);
@@ -315,25 +356,20 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 
   bf16x8 ah[S][KB], al[S][KB];
 
-  // ---- layer 0 (input -> width) on VALU: derivative streams are rows of K0 ----------------
+  // ---- layer 0 (input -> width) on VALU ---------------------------------------------------
   {
     float* H0 = Hs + hs_base(0, nwg, wg, S, w, WT, l);
+    const bool save_all = !h0r || Lh == 1;  // else the backward rebuilds streams >= 1 (h0_stream)
     bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
-      const int f0 = 16 * t + 4 * g;
-      f32x4 z[S], h[S];
-      z[0] = *reinterpret_cast<const f32x4*>(b0 + f0);
+      f32x4 h[S];
+      h0_jet<WT, S, NSO>(sp, aux, d, x, t, g, h);
+      *reinterpret_cast<f32x4*>(H0 + hs_off(0, t, WT)) = h[0];
+      if (save_all) {
 #pragma unroll
-      for (int j = 0; j < TDQ_MAXD; ++j)
-        if (j < d.d_in) z[0] += x[j] * *reinterpret_cast<const f32x4*>(K0 + j * W + f0);
-#pragma unroll
-      for (int s = 1; s < SO; ++s) z[s] = *reinterpret_cast<const f32x4*>(K0 + sp.var[s] * W + f0);
-#pragma unroll
-      for (int s = SO; s < S; ++s) z[s] = zero4();
-      tanh_jet_f<S, NSO>(sp, z, h);
-#pragma unroll
-      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(H0 + hs_off(s, t, WT)) = h[s];
+        for (int s = 1; s < S; ++s) *reinterpret_cast<f32x4*>(H0 + hs_off(s, t, WT)) = h[s];
+      }
       if (Lh == 1) {
 #pragma unroll
         for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
@@ -463,7 +499,7 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
                                              const bf16x8* __restrict__ Ki, const float* __restrict__ Hp,
                                              bf16x4* stage, float* accBslot, float* accK0,
                                              const float* __restrict__ xrow, const JetSpec& sp, const NetDims& d,
-                                             int w, int l, int p, int g) {
+                                             const float* __restrict__ aux, bool h0r, int w, int l, int p, int g) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
   bf16x8 wh[D], wl[D];
 #pragma unroll
@@ -471,9 +507,16 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
     wh[k] = Ki[k * 128];
     wl[k] = Ki[k * 128 + 64];
   }
+  // TO_FIRST && h0r: only layer 0's value stream is saved; the others are rebuilt (h0_stream)
+  const bool rec = TO_FIRST && h0r;
   f32x4 hr[2][S];
-  h_tile<S, WT>(hr[0], Hp, 0);
-  if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
+  if (rec) {
+    hr[0][0] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, 0, WT));
+    if (WT > 1) hr[1][0] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, 1, WT));
+  } else {
+    h_tile<S, WT>(hr[0], Hp, 0);
+    if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
+  }
   f32x4 accA[S], accB[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
@@ -499,9 +542,16 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
     if (o > 0) {
       const int t = o - 1;
       f32x4 h[S], zb[S];
+      if (rec) {
+        h[0] = hr[t & 1][0];
+        if (t + 2 < WT) hr[t & 1][0] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, t + 2, WT));
 #pragma unroll
-      for (int s = 0; s < S; ++s) h[s] = hr[t & 1][s];
-      if (t + 2 < WT) h_tile<S, WT>(hr[t & 1], Hp, t + 2);
+        for (int s = 1; s < S; ++s) h[s] = h0_stream<WT, S, NSO>(sp, aux, h[0], t, g, s);
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) h[s] = hr[t & 1][s];
+        if (t + 2 < WT) h_tile<S, WT>(hr[t & 1], Hp, t + 2);
+      }
       tanh_jet_b<S, NSO>(sp, h, accP, zb);
       if (TO_FIRST)
         first_layer_partials<WT, S, NSO>(sp, zb, xrow, d, t, w, p, g, accBslot, accK0);
@@ -516,7 +566,7 @@ template <int WT, int S, int NSO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
-                   int Ptot, NetDims d, JetSpec sp, int rev) {
+                   int Ptot, NetDims d, JetSpec sp, int rev, int h0r) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int W = 16 * WT;
   constexpr int KB = WT / 2;
@@ -647,6 +697,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   for (int i = Lh - 1; i >= 1; --i) {
     const int tsb = 2 + 8 * (Lh - 1 - i);
     const float* Hp = Hs + hs_base(i - 1, nwg, wg, S, w, WT, l);
+    // layer 0 under h0r: hp keeps the value stream, stream s is rebuilt from it (h0_stream)
+    const bool rec0 = h0r && i == 1;
     // h_{i-1} tiles of stream 0 for the dK images
     f32x4 hp[WT];
 #pragma unroll
@@ -674,7 +726,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
         for (int t = 0; t < WT; ++t) {
           bf16x4 hi, lo;
-          split4(hp[t], hi, lo);
+          split4(rec0 ? h0_stream<WT, S, NSO>(sp, aux, hp[t], t, g, s) : hp[t], hi, lo);
           const int off = row * RS + ((16 * t + 4 * g) ^ rsw);
           *reinterpret_cast<bf16x4*>(img + off) = hi;
           *reinterpret_cast<bf16x4*>(img + IMG + off) = lo;
@@ -682,7 +734,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
           *reinterpret_cast<bf16x4*>(img + 3 * IMG + off) = half8(zl[s][t >> 1], t & 1);
         }
       }
-      if (s + 1 < S) {  // next stream's h_{i-1} tiles fly while this stream's MFMAs run
+      if (s + 1 < S && !rec0) {  // next stream's h_{i-1} tiles fly while this stream's MFMAs run
 #pragma unroll
         for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(s + 1, t, WT));
       }
@@ -728,8 +780,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     // (d) hb_{i-1} = K_i zb_i, fused with the adjoint of tanh layer i-1
     const bf16x8* Ki = Kimg + (size_t)(i - 1) * (WT * KB) * 128 + l;
     if (i >= 2) {
-      bwd_hidden_d<WT, S, NSO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, w, l,
-                                      p, g);
+      bwd_hidden_d<WT, S, NSO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, aux,
+                                      h0r != 0, w, l, p, g);
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -738,7 +790,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
           zl[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
         }
     } else {
-      bwd_hidden_d<WT, S, NSO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, w, l, p, g);
+      bwd_hidden_d<WT, S, NSO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, aux, h0r != 0, w, l,
+                                     p, g);
     }
     TDQ_TS(tsb + 4);
   }
@@ -784,6 +837,16 @@ inline int bwd_reverse_order() {
   return rev;
 }
 
+// layer-0 activations recomputed in the backward (default) or saved by the forward
+// (TDQ_H0_RECOMPUTE=0, for A/B runs).  Read once per process: forward and backward always agree.
+inline int h0_recompute() {
+  static const int on = [] {
+    const char* e = getenv("TDQ_H0_RECOMPUTE");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 inline size_t bwd_bf3_lds(int WT, int S) {
   const int W = 16 * WT;
   const size_t u1 = (size_t)(4 * 64 * 144) / 2, u2 = (size_t)4 * S * WT * 256;
@@ -816,7 +879,7 @@ int launch_fwd_bf3(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
-                     a.Hs, a.N, a.d, a.sp);
+                     a.Hs, a.N, a.d, a.sp, h0_recompute());
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -832,7 +895,7 @@ int launch_bwd_bf3(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
-                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order());
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute());
   TDQ_CHECK_LAUNCH();
   return 0;
 }

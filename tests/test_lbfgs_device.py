@@ -108,7 +108,7 @@ def test_solver_device_lbfgs_matches_host(monkeypatch):
         assert math.isfinite(res[impl])
         if impl == "device":
             assert m.lbfgs_state.n_iter == 15
-            f_best = float(m.update_loss())
+            f_best = float(m.update_loss().detach())
             assert f_best == pytest.approx(m.min_loss["l-bfgs"], rel=1e-4)
     # identical algorithm; the device run also evaluates the last iterate
     assert res["device"] <= res["host"] * (1 + 1e-3)
