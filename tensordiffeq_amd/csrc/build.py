@@ -29,52 +29,58 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def _flags():
-    return ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics", "-fno-slp-vectorize",
-            "-Wno-unused-result", "-I", HERE]
+def _flags(defines=()):
+    return (["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+             "-Wno-unused-result", "-I", HERE] + [f"-D{m}" for m in defines])
 
 
-def _compile(src, force):
-    obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
+def _compile(src, force, build_dir=None, defines=()):
+    obj = os.path.join(build_dir or BUILD, os.path.basename(src).replace(".hip", ".o"))
     deps = [src] + glob.glob(os.path.join(HERE, "*.h"))
     if not force and os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj, False
-    cmd = [hipcc()] + _flags() + ["-c", src, "-o", obj]
+    cmd = [hipcc()] + _flags(defines) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
     return obj, True
 
 
-def build(force=False, jobs=None, verbose=True):
-    os.makedirs(BUILD, exist_ok=True)
+def build(force=False, jobs=None, verbose=True, variant=None, defines=()):
+    """Build ``csrc/libtdq_hip.so``; ``variant="x"`` with ``defines`` builds an A/B variant into
+    ``csrc/build_x/libtdq_hip.so`` instead (load it with ``TDQ_LIB_PATH``)."""
+    build_dir = os.path.join(HERE, f"build_{variant}") if variant else BUILD
+    out = os.path.join(build_dir, "libtdq_hip.so") if variant else OUT
+    os.makedirs(build_dir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(HERE, "*.hip")))
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force), srcs))
+        results = list(ex.map(lambda s: _compile(s, force, build_dir, defines), srcs))
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
-    if rebuilt or force or not os.path.exists(OUT) or any(
-            os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
-        tmp = OUT + ".tmp"
+    if rebuilt or force or not os.path.exists(out) or any(
+            os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        tmp = out + ".tmp"
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, OUT)
+        os.replace(tmp, out)
         if verbose:
-            print(f"built {OUT}")
+            print(f"built {out}")
     elif verbose:
-        print(f"{OUT} up to date")
-    return OUT
+        print(f"{out} up to date")
+    return out
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--variant", default=None, help="A/B build into csrc/build_<variant>/")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="preprocessor macro (variants)")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.j)
+    build(force=a.force, jobs=a.j, variant=a.variant, defines=a.defines)
 
 
 if __name__ == "__main__":

@@ -212,6 +212,15 @@ __device__ __forceinline__ size_t hs_base(int layer, int nwg, int wg, int S, int
 }
 __device__ __forceinline__ int hs_off(int s, int t, int WT) { return (s * 4 * WT + t) * 256; }
 
+// saved-activation store (forward); -DTDQ_NT_STORES builds the non-temporal variant for A/B runs
+__device__ __forceinline__ void hs_store(float* p, const f32x4& v) {
+#ifdef TDQ_NT_STORES
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#else
+  *reinterpret_cast<f32x4*>(p) = v;
+#endif
+}
+
 // layer 0 (input -> width, VALU; derivative streams are rows of K0): the post-activation streams of
 // feature tile t (forward).
 template <int WT, int S, int NSO>
@@ -303,7 +312,7 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       z[0] += biasP;
       tanh_jet_f<S, NSO>(sp, z, h);
 #pragma unroll
-      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(Hl + hs_off(s, t, WT)) = h[s];
+      for (int s = 0; s < S; ++s) hs_store(Hl + hs_off(s, t, WT), h[s]);
       if (LAST) {
 #pragma unroll
         for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
@@ -365,10 +374,10 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     for (int t = 0; t < WT; ++t) {
       f32x4 h[S];
       h0_jet<WT, S, NSO>(sp, aux, d, x, t, g, h);
-      *reinterpret_cast<f32x4*>(H0 + hs_off(0, t, WT)) = h[0];
+      hs_store(H0 + hs_off(0, t, WT), h[0]);
       if (save_all) {
 #pragma unroll
-        for (int s = 1; s < S; ++s) *reinterpret_cast<f32x4*>(H0 + hs_off(s, t, WT)) = h[s];
+        for (int s = 1; s < S; ++s) hs_store(H0 + hs_off(s, t, WT), h[s]);
       }
       if (Lh == 1) {
 #pragma unroll
