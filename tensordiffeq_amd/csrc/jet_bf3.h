@@ -212,12 +212,44 @@ __device__ __forceinline__ size_t hs_base(int layer, int nwg, int wg, int S, int
 }
 __device__ __forceinline__ int hs_off(int s, int t, int WT) { return (s * 4 * WT + t) * 256; }
 
-// saved-activation store (forward); -DTDQ_NT_STORES builds the non-temporal variant for A/B runs
+// Saved activations move with non-temporal stores (forward) and loads (backward): they are written
+// once, read after the whole forward + loss, and each read is too far from the next use of the
+// line for the caches to help, so allocating them only evicts the weight images and partials that
+// are reused.  A/B on MI355X (AC-SA step): plain 0.532 ms, nt stores 0.520, + nt loads 0.502;
+// keeping the first of the two backward reads of a hidden layer cached (the tanh-adjoint pass reads
+// the same lines right after) 0.494 vs 0.500; nt gradient-slab stores are slower (0.545 vs 0.520:
+// the reduction re-reads them at once).  -DTDQ_TEMPORAL_STORES / -DTDQ_TEMPORAL_LOADS /
+// -DTDQ_NT_C_LOADS / -DTDQ_NT_SLAB build the other variants (profiles/r1_v9_nontemporal_ab.txt).
 __device__ __forceinline__ void hs_store(float* p, const f32x4& v) {
-#ifdef TDQ_NT_STORES
-  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
-#else
+#ifdef TDQ_TEMPORAL_STORES
   *reinterpret_cast<f32x4*>(p) = v;
+#else
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#endif
+}
+
+__device__ __forceinline__ f32x4 hs_load(const float* p) {
+#ifdef TDQ_TEMPORAL_LOADS
+  return *reinterpret_cast<const f32x4*>(p);
+#else
+  return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+#endif
+}
+
+// the dK pass's read of h_{i-1} (the same lines are read again by the tanh-adjoint pass)
+__device__ __forceinline__ f32x4 hs_load_c(const float* p) {
+#ifdef TDQ_NT_C_LOADS
+  return hs_load(p);
+#else
+  return *reinterpret_cast<const f32x4*>(p);
+#endif
+}
+
+__device__ __forceinline__ void slab_store(float* p, float v) {
+#ifdef TDQ_NT_SLAB
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
 #endif
 }
 
@@ -451,7 +483,7 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 template <int S, int WT>
 __device__ __forceinline__ void h_tile(f32x4 (&h)[S], const float* __restrict__ Hl, int t) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) h[s] = *reinterpret_cast<const f32x4*>(Hl + hs_off(s, t, WT));
+  for (int s = 0; s < S; ++s) h[s] = hs_load(Hl + hs_off(s, t, WT));
 }
 
 // first-layer partials from zb_0 (fp32) of one feature tile: bias b0 and dK0[j][f] (one LDS slot
@@ -520,8 +552,8 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
   const bool rec = TO_FIRST && h0r;
   f32x4 hr[2][S];
   if (rec) {
-    hr[0][0] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, 0, WT));
-    if (WT > 1) hr[1][0] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, 1, WT));
+    hr[0][0] = hs_load(Hp + hs_off(0, 0, WT));
+    if (WT > 1) hr[1][0] = hs_load(Hp + hs_off(0, 1, WT));
   } else {
     h_tile<S, WT>(hr[0], Hp, 0);
     if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
@@ -553,7 +585,7 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
       f32x4 h[S], zb[S];
       if (rec) {
         h[0] = hr[t & 1][0];
-        if (t + 2 < WT) hr[t & 1][0] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, t + 2, WT));
+        if (t + 2 < WT) hr[t & 1][0] = hs_load(Hp + hs_off(0, t + 2, WT));
 #pragma unroll
         for (int s = 1; s < S; ++s) h[s] = h0_stream<WT, S, NSO>(sp, aux, h[0], t, g, s);
       } else {
@@ -711,7 +743,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     // h_{i-1} tiles of stream 0 for the dK images
     f32x4 hp[WT];
 #pragma unroll
-    for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(0, t, WT));
+    for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(0, t, WT));
     TDQ_TS(tsb);
 
     // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index
@@ -745,7 +777,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       }
       if (s + 1 < S && !rec0) {  // next stream's h_{i-1} tiles fly while this stream's MFMAs run
 #pragma unroll
-        for (int t = 0; t < WT; ++t) hp[t] = *reinterpret_cast<const f32x4*>(Hp + hs_off(s + 1, t, WT));
+        for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(s + 1, t, WT));
       }
       __syncthreads();
       if (s == 0) TDQ_TS(tsb + 1);
@@ -778,7 +810,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int in = 16 * dw_row(w, r) + 4 * g + c;
-            if (in < d.width && out < d.width) gs[ko + in * d.width + out] = dw[r][c2][c];
+            if (in < d.width && out < d.width) slab_store(gs + ko + in * d.width + out, dw[r][c2][c]);
           }
         }
     }
