@@ -100,6 +100,9 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
+                 f"'python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}'")
     dist = world > 1
     from tensordiffeq_amd.parallel import init_distributed, get_context
     ctx = init_distributed() if dist else get_context()

@@ -278,6 +278,8 @@ class CollocationSolverND:
 
     def program(self, batch=None):
         self._flat()  # wraps a user-assigned custom network
+        if self._state is not None:
+            self._train_state(self.device)  # re-validates the best snapshot against the network
         if self._programs.get("net") is not self.u_model:
             self._programs = {"net": self.u_model}
             self._engine = None
@@ -295,8 +297,20 @@ class CollocationSolverND:
 
     # ================================================================== state ===========
     def _train_state(self, device):
+        flat = self._flat()
+        st = self._state
+        if st is not None and (st["best_flat"].numel() != flat.numel() or st["best_flat"].device != flat.device):
+            # the network was replaced (load_model with other layer sizes, a custom u_model): the
+            # best-weights snapshot belongs to the old parameter vector - restart best tracking
+            # (epoch counter and loss history are kept); compiled engines are dropped with it
+            st["best_flat"] = flat.detach().clone()
+            st["best_loss"] = torch.full((), math.inf, dtype=torch.float32, device=flat.device)
+            st["best_epoch"] = torch.full((), -1, dtype=torch.int64, device=flat.device)
+            st.pop("improved", None)
+            self._programs = {}
+            self._engine = None
+            self._lbfgs_engine = None
         if self._state is None:
-            flat = self._flat()
             self._state = {
                 "best_loss": torch.full((), math.inf, dtype=torch.float32, device=device),
                 "best_flat": flat.detach().clone(),
@@ -354,13 +368,28 @@ class CollocationSolverND:
         return eng
 
     # ================================================================== fit =============
+    def minibatches(self, batch_sz):
+        """Per-rank minibatch ranges ``[(lo, hi), ...]`` (local shard indices) or ``[None]`` for
+        full batch.  The count comes from the SMALLEST shard (``N_f // world``), so every rank
+        runs the same number of steps - and therefore the same number of collectives - per
+        epoch even when ``N_f`` does not divide evenly; each step's residual denominator is
+        ``batch_sz * world`` on every rank."""
+        if batch_sz is None:
+            return [None]
+        batch_sz = int(batch_sz)
+        if batch_sz <= 0:
+            raise ValueError(f"batch_sz must be positive, got {batch_sz}")
+        ctx = self.dist_ctx
+        world = ctx.world if ctx.is_distributed else 1
+        n_min = self.N_f // world
+        if batch_sz >= n_min:
+            return [None]
+        nb = n_min // batch_sz
+        return [(i * batch_sz, (i + 1) * batch_sz) for i in range(nb)]
+
     def fit(self, tf_iter=0, newton_iter=0, batch_sz=None, newton_eager=True):
         ctx = self.dist_ctx
-        n_local = self.X_f_local.shape[0]
-        batches = [None]
-        if batch_sz is not None and batch_sz < n_local:
-            nb = max(1, n_local // int(batch_sz))
-            batches = [(i * batch_sz, (i + 1) * batch_sz) for i in range(nb)]
+        batches = self.minibatches(batch_sz)
         if self.verbose and ctx.rank == 0:
             print_screen(self)
         self.program()  # build / plan before timing-sensitive loops

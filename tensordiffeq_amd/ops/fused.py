@@ -38,6 +38,11 @@ def adam_multi(groups, t, lr, b1, b2, eps, snapshot=None):
     the int32 device flag ``improved`` is set."""
     if not groups:
         return
+    if snapshot is not None and snapshot[0].numel() != groups[0][0].numel():
+        # the kernel copies group 0's parameters into the snapshot buffer: a stale (smaller)
+        # snapshot would be an out-of-bounds device write
+        raise ValueError(f"best-weights snapshot has {snapshot[0].numel()} elements, parameters "
+                         f"{groups[0][0].numel()}")
     if _native(groups[0][0]) and all(x.dtype == torch.float32 and x.is_contiguous()
                                      for gr in groups for x in gr[:4]):
         lib = _lib.load()

@@ -47,7 +47,8 @@ class Adam:
 
     def state_for(self, p):
         st = self._state.get(id(p))
-        if st is None:
+        # keyed by id(): a freed tensor's id can be reused by a new one of another shape/device
+        if st is None or st[0].shape != p.shape or st[0].device != p.device:
             st = (torch.zeros_like(p), torch.zeros_like(p))
             self._state[id(p)] = st
         return st

@@ -81,3 +81,50 @@ def test_dp_gloo_matches_single_process():
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-4)
     assert torch.allclose(res["flat_after"], ref_flat, atol=1e-5)
     assert torch.allclose(res["flat_lbfgs"], ref_lbfgs, atol=1e-4)
+
+
+def _worker_batched(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(backend="gloo", device="cpu")
+    m = _build(True)          # N_f = 301 over 2 ranks: shards of 151 and 150 points
+    batches = m.minibatches(50)
+    m.fit(tf_iter=2, batch_sz=50)
+    q.put({"rank": rank, "n_local": m.X_f_local.shape[0], "batches": batches,
+           "epochs": int(m._state["epoch_host"]), "flat": m.u_model.flat.detach().clone(),
+           "lam": m.lambdas[0].detach().clone()})
+    ctx.barrier()
+    pdist.destroy()
+
+
+@pytest.mark.timeout(300)
+def test_dp_minibatch_uneven_shards():
+    """Uneven shards + batch_sz: every rank runs the same number of minibatch steps (one
+    all-reduce each), so the run completes and theta stays identical across ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_batched, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=280) for _ in range(2)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r["n_local"] for r in res] == [151, 150]
+    assert res[0]["batches"] == res[1]["batches"] == [(0, 50), (50, 100), (100, 150)]
+    assert res[0]["epochs"] == res[1]["epochs"] == 6
+    assert torch.equal(res[0]["flat"], res[1]["flat"])
+    assert res[0]["lam"].shape == (151, 1) and res[1]["lam"].shape == (150, 1)
+
+
+def test_minibatches_single_process():
+    m = _build(False)
+    assert m.minibatches(None) == [None]
+    assert m.minibatches(301) == [None]
+    assert m.minibatches(100) == [(0, 100), (100, 200), (200, 300)]
+    with pytest.raises(ValueError):
+        m.minibatches(0)

@@ -247,3 +247,24 @@ def test_tensordiffeq_alias():
     from tensordiffeq.boundaries import DomainND as D2
     assert CollocationSolverND is tdq.CollocationSolverND and D2 is DomainND
     assert tensordiffeq.utils.MSE is tdq.MSE
+
+
+def test_load_model_with_other_layer_sizes_resets_best_snapshot(tmp_path):
+    """After fit, load a checkpoint of a LARGER network and fit again: the best-weights
+    snapshot is rebuilt for the new parameter vector (the fused Adam copies the parameters into
+    it - a stale smaller snapshot would be an out-of-bounds write on a GPU)."""
+    big = tdq.CollocationSolverND(verbose=False)
+    D, bcs, f = burgers()
+    torch.manual_seed(1)
+    big.compile([2, 16, 16, 16, 1], f, D, bcs, backend="jet", device="cpu")
+    path = str(tmp_path / "big.npz")
+    big.save(path)
+    m = compiled("jet")
+    m.fit(tf_iter=3)
+    m.load_model(path)
+    assert m.u_model.flat.numel() == big.u_model.flat.numel()
+    m.fit(tf_iter=3)
+    st = m._state
+    assert st["best_flat"].numel() == m.u_model.flat.numel()
+    assert len(m.losses) == 6 and math.isfinite(m.min_loss["adam"])
+    assert 3 <= m.best_epoch["adam"] < 6   # best tracking restarted with the new network
