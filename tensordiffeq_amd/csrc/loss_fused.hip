@@ -255,10 +255,29 @@ __global__ void loss_total_kernel(const float* __restrict__ losses, int n_terms,
 extern "C" {
 
 // code: int4 per instruction; outs / groups / ptrs: device buffers of LFOut / LFGroup / LFPtrs
+// partials -> per-term losses and scalar gradients (+ the total when with_total); a separate entry
+// so a captured step can run it on a side stream, beside the jet backward
+int tdq_loss_reduce(const float* partials, int n_blocks, int n_terms, int n_scal, float* losses, float* total,
+                    float* dscal, int with_total, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int ns = n_terms + n_scal;
+  if (ns > 0) {
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(ns), dim3(256), 0, st, partials, n_blocks, n_terms, n_scal, losses,
+                       total, dscal);
+    TDQ_CHECK_LAUNCH();
+  }
+  if (with_total) {  // the Adam step's bookkeeping kernel (tdq_step_book) sums the terms itself
+    hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, losses, n_terms, total);
+    TDQ_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// do_reduce = 0: only the loss kernel (dJ, dlam, block partials); tdq_loss_reduce finishes
 int tdq_loss_fused(const int* code, const float* consts, const void* outs, const void* groups,
                    const void* ptrs, int n_groups, int n_terms, int n_scal, int S, int d_in, int N,
                    const float* J, const float* X, float* dJ, float* partials, int n_blocks, int max_regs,
-                   float* losses, float* total, float* dscal, int with_total, void* stream) {
+                   float* losses, float* total, float* dscal, int with_total, int do_reduce, void* stream) {
   LFMeta meta{n_groups, n_terms, n_scal, S, d_in, N};
   if (meta.n_groups < 1 || meta.n_groups > LF_MAX_GROUPS || meta.n_terms > LF_MAX_TERMS ||
       meta.n_scal > LF_MAX_SCAL)
@@ -276,15 +295,8 @@ int tdq_loss_fused(const int* code, const float* consts, const void* outs, const
                      reinterpret_cast<const LFGroup*>(groups), meta, reinterpret_cast<const LFPtrs*>(ptrs), J, X,
                      dJ, partials);
   TDQ_CHECK_LAUNCH();
-  const int ns = meta.n_terms + meta.n_scal;
-  hipLaunchKernelGGL(loss_reduce_kernel, dim3(ns), dim3(256), 0, st, partials, n_blocks, meta.n_terms,
-                     meta.n_scal, losses, total, dscal);
-  TDQ_CHECK_LAUNCH();
-  if (with_total) {  // the Adam step's bookkeeping kernel (tdq_step_book) sums the terms itself
-    hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, losses, meta.n_terms, total);
-    TDQ_CHECK_LAUNCH();
-  }
-  return 0;
+  if (!do_reduce) return 0;
+  return tdq_loss_reduce(partials, n_blocks, meta.n_terms, meta.n_scal, losses, total, dscal, with_total, stream);
 }
 
 int tdq_loss_meta_sizes(int* out) {

@@ -18,6 +18,8 @@
 
 #define TDQ_MAX_GROUPS 16
 
+// one tensor of the update with its optimizer's hyper-parameters and device step counter, so the
+// network (descent) and self-adaptive-weight (ascent) optimizers share one launch
 struct AdamGroup {
   float* p;
   const float* g;
@@ -25,7 +27,9 @@ struct AdamGroup {
   float* v;
   int64_t n;
   float sign;
+  float lr, b1, b2, eps;
   float pad;
+  const double* t;
 };
 
 struct AdamArgs {
@@ -41,12 +45,9 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = p - lr_t * m / (sqrtf(v) + eps);
 }
 
-__global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const double* __restrict__ tptr,
-                                                          float lr, float b1, float b2, float eps,
-                                                          const int* __restrict__ improved, float* __restrict__ snap) {
+__global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const int* __restrict__ improved,
+                                                          float* __restrict__ snap) {
   const bool do_snap = snap != nullptr && *improved != 0;  // group 0 only
-  const double t = *tptr;
-  const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
   const int64_t total = args.start[args.ngroups];
   for (int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x; slot < total;
        slot += (int64_t)gridDim.x * 256) {
@@ -56,7 +57,9 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const do
       if (q < args.ngroups && slot >= args.start[q]) gi = q;
     const AdamGroup gr = args.grp[gi];
     const int64_t e0 = (slot - args.start[gi]) * 4;
-    const float sg = gr.sign;
+    const float sg = gr.sign, b1 = gr.b1, b2 = gr.b2, eps = gr.eps;
+    const double t = *gr.t;  // bias-corrected step size from the group's device step counter
+    const float lr_t = (float)((double)gr.lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
     const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
     if (aligned && e0 + 4 <= gr.n) {
       f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
@@ -138,7 +141,7 @@ __global__ void step_book_kernel(float* __restrict__ loss, const float* __restri
 
 extern "C" {
 
-int tdq_abi_version() { return 7; }
+int tdq_abi_version() { return 8; }
 
 int tdq_step_book(float* loss, const float* terms, int n_terms, int sum_terms, float* hist, int64_t hist_rows,
                   int64_t* epoch, float* best_loss, int64_t* best_epoch, int* improved, double* const* counters,
@@ -153,9 +156,9 @@ int tdq_step_book(float* loss, const float* terms, int n_terms, int sum_terms, f
   return 0;
 }
 
-// improved / snap: optional (nullptr) best-weights snapshot of group 0 before its update
-int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, float b1, float b2,
-                   float eps, const int* improved, float* snap, void* stream) {
+// groups carry their own lr / b1 / b2 / eps / step-counter pointer.  improved / snap: optional
+// (nullptr) best-weights snapshot of group 0 before its update
+int tdq_adam_multi(const void* groups, int ngroups, const int* improved, float* snap, void* stream) {
   if (ngroups <= 0 || ngroups > TDQ_MAX_GROUPS) return (int)hipErrorInvalidValue;
   AdamArgs args;
   const AdamGroup* src = reinterpret_cast<const AdamGroup*>(groups);
@@ -166,7 +169,7 @@ int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, f
       args.grp[i] = src[i];
       args.start[i + 1] = args.start[i] + (src[i].n + 3) / 4;
     } else {
-      args.grp[i] = AdamGroup{nullptr, nullptr, nullptr, nullptr, 0, 1.f, 0.f};
+      args.grp[i] = AdamGroup{nullptr, nullptr, nullptr, nullptr, 0, 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, nullptr};
       if (i + 1 <= TDQ_MAX_GROUPS) args.start[i + 1] = args.start[i];
     }
   }
@@ -175,7 +178,7 @@ int tdq_adam_multi(const void* groups, int ngroups, const double* t, float lr, f
   int64_t blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), args, t, lr, b1, b2, eps, improved, snap);
+                     reinterpret_cast<hipStream_t>(stream), args, improved, snap);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

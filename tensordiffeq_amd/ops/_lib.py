@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lock = threading.Lock()
 _lib = None
@@ -43,10 +43,11 @@ def _declare(lib):
         "tdq_jet_bwd_bf3": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P]),
         "tdq_jet_bf3_scratch_floats": (L, [I, I, I, I, I]),
         "tdq_jet_bf3_slab_floats": (L, [I, I, I, I, I]),
-        "tdq_adam_multi": (I, [P, I, P, F, F, F, F, P, P, P]),
+        "tdq_adam_multi": (I, [P, I, P, P, P]),
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
-        "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, I, P]),
+        "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, I, I, P]),
+        "tdq_loss_reduce": (I, [P, I, I, I, P, P, P, I, P]),
         "tdq_loss_meta_sizes": (I, [P]),
         "tdq_lbfgs_nst": (I, []),
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [P]),

@@ -3,7 +3,8 @@
 ``adam_multi``  one launch updates every tensor of a step (flat theta, or all SA lambdas with
                 ``sign=-1`` for gradient ascent, reference fit.py:136-141) with the Keras Adam
                 formula; the bias-corrected step size is computed in-kernel from the device step
-                counter, so the launch is graph-capturable.
+                counter, so the launch is graph-capturable.  ``adam_multi_opts``: the same for
+                several optimizers (own counters / hyper-parameters) in ONE launch.
 ``best_track``  device-side "keep the best weights" (reference fit.py:51-55 stored an alias of
                 the live model, B8): copies the flat buffer to the snapshot iff loss < best.
 ``step_book``   the per-step scalar bookkeeping in one single-thread launch (history row,
@@ -25,7 +26,8 @@ _MAX_GROUPS = 16
 class _Group(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p),
                 ("v", ctypes.c_void_p), ("n", ctypes.c_int64), ("sign", ctypes.c_float),
-                ("pad", ctypes.c_float)]
+                ("lr", ctypes.c_float), ("b1", ctypes.c_float), ("b2", ctypes.c_float),
+                ("eps", ctypes.c_float), ("pad", ctypes.c_float), ("t", ctypes.c_void_p)]
 
 
 def _native(t):
@@ -33,38 +35,47 @@ def _native(t):
 
 
 def adam_multi(groups, t, lr, b1, b2, eps, snapshot=None):
-    """groups: list of (param, grad, m, v, sign).  ``t``: float64 device step counter (already +1).
-    ``snapshot=(best, improved)``: copy group 0's parameters into ``best`` before the update when
-    the int32 device flag ``improved`` is set."""
-    if not groups:
+    """groups: list of (param, grad, m, v, sign) sharing one optimizer.  ``t``: float64 device step
+    counter (already +1).  ``snapshot=(best, improved)``: copy group 0's parameters into ``best``
+    before the update when the int32 device flag ``improved`` is set."""
+    adam_multi_opts([(groups, t, lr, b1, b2, eps)], snapshot)
+
+
+def adam_multi_opts(opt_groups, snapshot=None):
+    """One launch for several optimizers: ``opt_groups`` = list of ``(groups, t, lr, b1, b2, eps)``
+    (e.g. Adam descent on theta and Adam ascent on the SA weights, each with its own step
+    counter and hyper-parameters).  ``snapshot`` applies to the first tensor of the first group."""
+    flat = [(p, g, m, v, sign, t, lr, b1, b2, eps)
+            for groups, t, lr, b1, b2, eps in opt_groups for (p, g, m, v, sign) in groups]
+    if not flat:
         return
-    if snapshot is not None and snapshot[0].numel() != groups[0][0].numel():
+    if snapshot is not None and snapshot[0].numel() != flat[0][0].numel():
         # the kernel copies group 0's parameters into the snapshot buffer: a stale (smaller)
         # snapshot would be an out-of-bounds device write
         raise ValueError(f"best-weights snapshot has {snapshot[0].numel()} elements, parameters "
-                         f"{groups[0][0].numel()}")
-    if _native(groups[0][0]) and all(x.dtype == torch.float32 and x.is_contiguous()
-                                     for gr in groups for x in gr[:4]):
+                         f"{flat[0][0].numel()}")
+    if _native(flat[0][0]) and all(x.dtype == torch.float32 and x.is_contiguous()
+                                   for gr in flat for x in gr[:4]):
         lib = _lib.load()
-        for lo in range(0, len(groups), _MAX_GROUPS):
-            chunk = groups[lo:lo + _MAX_GROUPS]
+        for lo in range(0, len(flat), _MAX_GROUPS):
+            chunk = flat[lo:lo + _MAX_GROUPS]
             snap = snapshot if lo == 0 else None
             arr = (_Group * len(chunk))()
-            for i, (p, g, m, v, sign) in enumerate(chunk):
+            for i, (p, g, m, v, sign, t, lr, b1, b2, eps) in enumerate(chunk):
                 arr[i] = _Group(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
-                                float(sign), 0.0)
-            rc = lib.tdq_adam_multi(ctypes.cast(arr, ctypes.c_void_p), len(chunk), _lib.ptr(t),
-                                    float(lr), float(b1), float(b2), float(eps),
+                                float(sign), float(lr), float(b1), float(b2), float(eps), 0.0,
+                                t.data_ptr())
+            rc = lib.tdq_adam_multi(ctypes.cast(arr, ctypes.c_void_p), len(chunk),
                                     _lib.ptr(snap[1]) if snap else None, _lib.ptr(snap[0]) if snap else None,
-                                    _lib.stream_ptr(p.device))
+                                    _lib.stream_ptr(flat[0][0].device))
             _lib.check(rc, "tdq_adam_multi")
         return
-    _lib.require_on_gpu() if groups[0][0].is_cuda else None
+    _lib.require_on_gpu() if flat[0][0].is_cuda else None
     with torch.no_grad():
         if snapshot is not None:
             best, improved = snapshot
-            best.copy_(torch.where(improved.bool(), groups[0][0], best))
-        for (p, g, m, v, sign) in groups:
+            best.copy_(torch.where(improved.bool(), flat[0][0], best))
+        for (p, g, m, v, sign, t, lr, b1, b2, eps) in flat:
             torch_update(p, g, m, v, t, lr, b1, b2, eps, sign)
 
 

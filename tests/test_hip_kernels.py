@@ -149,6 +149,34 @@ def test_adam_multi_matches_reference():
         assert torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
 
 
+def test_adam_multi_opts_two_optimizers_one_launch():
+    """theta descent and SA-weight ascent with their own counters / hyper-parameters in ONE launch,
+    plus the best-weights snapshot, against the torch reference update."""
+    from tensordiffeq_amd.ops import fused
+    from tensordiffeq_amd.optimizers.adam import torch_update
+    torch.manual_seed(1)
+    p1, g1 = torch.randn(50049, device="cuda"), torch.randn(50049, device="cuda")
+    p2, g2 = torch.randn(50513, device="cuda"), torch.randn(50513, device="cuda")
+    m1, v1, m2, v2 = (torch.zeros_like(x) for x in (p1, p1, p2, p2))
+    r1, r2 = (p1.clone(), m1.clone(), v1.clone()), (p2.clone(), m2.clone(), v2.clone())
+    t1 = torch.zeros((), dtype=torch.float64, device="cuda")
+    t2 = torch.full((), 7.0, dtype=torch.float64, device="cuda")  # counters need not agree
+    best = torch.zeros_like(p1)
+    improved = torch.ones((), dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        t1.add_(1)
+        t2.add_(1)
+        before = p1.clone()
+        fused.adam_multi_opts([([(p1, g1, m1, v1, 1.0)], t1, 0.005, 0.99, 0.999, 1e-7),
+                               ([(p2, g2, m2, v2, -1.0)], t2, 0.01, 0.9, 0.99, 1e-6)],
+                              snapshot=(best, improved))
+        assert torch.equal(best, before)
+        torch_update(r1[0], g1, r1[1], r1[2], t1, 0.005, 0.99, 0.999, 1e-7, 1.0)
+        torch_update(r2[0], g2, r2[1], r2[2], t2, 0.01, 0.9, 0.99, 1e-6, -1.0)
+    assert torch.allclose(p1, r1[0], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(p2, r2[0], rtol=1e-5, atol=1e-6)
+
+
 def test_best_track():
     from tensordiffeq_amd.ops import fused
     flat = torch.randn(1000, device="cuda")

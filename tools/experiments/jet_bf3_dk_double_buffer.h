@@ -1,0 +1,972 @@
+// Split-bf16 ("bf16x3") Taylor-jet tanh-MLP forward / backward kernels for gfx950 (MI355X, CDNA4).
+//
+// Same contract as jet_mlp.hip (stream jets J[s][n][q] of a tanh MLP and the flat parameter
+// gradient of <dJ, J>), re-tiled for the bf16 matrix cores: on gfx950 the exact-fp32 MFMA runs
+// at the fp32 VECTOR rate (64 FLOP/clk/SIMD) while v_mfma_f32_16x16x32_bf16 runs 16x faster.
+// Every GEMM operand is split x = hi + lo (two bf16, |x - hi - lo| <= 2^-17 |x|) and a product
+// is formed as ah*bh + ah*bl + al*bh with fp32 accumulation: 3 bf16 MFMAs per fp32-equivalent
+// product (5.3x the fp32-MFMA rate) at ~2^-16 relative error per product (the dropped al*bl
+// term), i.e. ~19 significant bits instead of bf16's 8.
+//
+// Layout (16x16x32 MFMA: lane l = (p = l&15, g = l>>4); A[p][8g+j], B[8g+j][p], D[4g+r][p]):
+//   * one workgroup = 4 waves x 16 points, one point per lane column, features in registers;
+//   * k-block kb of a layer covers features 32kb..32kb+31 in the PERMUTED order
+//       k = 8g + j  <->  feature 32kb + (j < 4 ? 4g + j : 16 + 4g + j - 4)
+//     so the fp32 accumulator tiles 2kb and 2kb+1 (lane holds rows 4g..4g+3 of each) ARE the
+//     B fragment of k-block kb after a hi/lo split - no lane movement between layers;
+//   * weights are pre-split into hi/lo A-fragment images in that permuted k order
+//     (pack_bf3_kernel: 16 B per lane per (layer, out tile, k-block)), streamed from L2 with a
+//     4-step register prefetch ring; biases / first and last layer come from a zero-padded
+//     fp32 "aux" image so that no load in a kernel needs a bounds guard (no exec branches);
+//   * streams are in JetPlan's canonical order - value, S1 first-order, NSO second-order - and
+//     NSO is a template parameter: the jet epilogues are branch-free straight-line code, the
+//     two first-order factors of a second-order stream are picked by uniform-index selects;
+//   * forward: the epilogue of output tile o-1 (bias, tanh jet, save, hi/lo split, stage) is
+//     issued in the same scheduling region as the MFMAs of tile o (double-buffered
+//     accumulators), so VALU work fills the MFMA shadow; it saves the POST-activation streams
+//     h (fp32).  The backward needs no tanh recompute: with s1 = 1 - h^2 and s2 z_a = -2 h h_a
+//       zb_ab = s1 hb_ab
+//       zb_a  = s1 hb_a - 2 h sum_{(a,b)} h_b hb_ab
+//       zb    = s1 hb - 2 h sum_{s>0} h_s hb_s - 2 sum_{(a,b)} h_a h_b hb_ab
+//   * dK = sum_points sum_streams h_prev zb^T reduces over POINTS: both operands go through
+//     [point][feature] bf16 LDS images read back transposed with ds_read_b64_tr_b16, so points
+//     land on the MFMA k index (8 consecutive points per lane); the next stream's h_prev tiles
+//     are in flight from HBM while the current stream's MFMAs run.
+// Reference behaviour: the nested tf.gradients of the PDE residual (SURVEY.md §2.2 K2-K8,
+// tensordiffeq/models.py:update_loss / utils.py:get_tf_model); jet_mlp.hip is the fp32 twin.
+#pragma once
+#include "jet_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// Optional per-phase timestamps (build with -DTDQ_PHASE_TIMING, tools/phase_timing.py): lane 0
+// of every wave stores s_memtime at numbered points into tdq_ts[(wg * 4 + wave) * 64 + k].
+#ifdef TDQ_PHASE_TIMING
+static __device__ unsigned long long* tdq_ts;  // per translation unit (no -fgpu-rdc)
+#define TDQ_TS(k)                                                                                 \
+  do {                                                                                            \
+    if ((threadIdx.x & 63) == 0)                                                                  \
+      tdq_ts[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TDQ_TS(k) \
+  do {            \
+  } while (0)
+#endif
+
+// aux image (fp32, zero padded to W = 16 WT features; TDQ_MAXO output columns):
+//   K0 [d_in][W] | b0 [W] | b_1..b_{Lh-1} [Lh-1][W] | Ko [W][4] | bo [4]
+__host__ __device__ inline int aux_b0(const NetDims& d, int W) { return d.d_in * W; }
+__host__ __device__ inline int aux_bh(const NetDims& d, int W) { return (d.d_in + 1) * W; }
+__host__ __device__ inline int aux_ko(const NetDims& d, int W) { return (d.d_in + d.n_hidden) * W; }
+__host__ __device__ inline int aux_bo(const NetDims& d, int W) { return (d.d_in + d.n_hidden + 4) * W; }
+__host__ __device__ inline int aux_floats(const NetDims& d, int W) { return (d.d_in + d.n_hidden + 4) * W + 4; }
+
+__device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// c += a * b  with a ~ ah + al, b ~ bh + bl  (al*bl dropped)
+__device__ __forceinline__ f32x4 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
+  c = mfma_bf(al, bh, c);
+  c = mfma_bf(ah, bl, c);
+  return mfma_bf(ah, bh, c);
+}
+
+// hi = rne_bf16(x), lo = rne_bf16(x - hi), two values per v_cvt_pk_bf16_f32
+__device__ __forceinline__ void split4(const f32x4 v, bf16x4& hi, bf16x4& lo) {
+  u32x2 H, L;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const f32x2 x = {v[2 * k], v[2 * k + 1]};
+    const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+    // scalar subtracts: packed f32 VALU (v_pk_add_f32) next to MFMAs costs extra issue cycles
+    const float r0 = v[2 * k] - __builtin_bit_cast(float, hb << 16);
+    const float r1 = v[2 * k + 1] - __builtin_bit_cast(float, hb & 0xffff0000u);
+    const f32x2 rl = {r0, r1};
+    H[k] = hb;
+    L[k] = __builtin_bit_cast(unsigned, __builtin_convertvector(rl, bf16x2));
+  }
+  hi = __builtin_bit_cast(bf16x4, H);
+  lo = __builtin_bit_cast(bf16x4, L);
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x4 half8(bf16x8 v, int hi_half) {
+  return hi_half ? __builtin_shufflevector(v, v, 4, 5, 6, 7) : __builtin_shufflevector(v, v, 0, 1, 2, 3);
+}
+
+// transposed LDS read (T10): lane 4q+c of each 16-lane group addresses row q, columns 4c..4c+3
+// of a 4 x 16 block; lane i of the group receives column i, rows 0..3.
+__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// tanh(z) and s1 = 1 - tanh(z)^2 without cancellation: e = exp(-2|z|),
+//   tanh|z| = (1 - e) / (1 + e)  (odd Taylor polynomial below 1/8),  s1 = 4 e / (1 + e)^2
+__device__ __forceinline__ void tanh_s1(float z, float& h, float& s1) {
+  const float az = fabsf(z);
+  const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * az);
+  const float r = __builtin_amdgcn_rcpf(1.f + e);
+  const float z2 = az * az;
+  const float poly = az * fmaf(z2, fmaf(z2, fmaf(z2, -0.053968254f, 0.13333334f), -0.33333334f), 1.f);
+  const float t = az < 0.125f ? poly : (1.f - e) * r;
+  h = __builtin_copysignf(t, z);
+  s1 = 4.f * e * (r * r);
+}
+
+// first-order stream `idx` (uniform, 1..S1) of a per-stream array.  Up to two candidates: a
+// select; more: the one-hot FMA over `sel` (LLVM turns a longer select chain over a register
+// array back into an indexed scratch load).
+template <int S, int S1, typename T>
+__device__ __forceinline__ T sel_first(const T (&v)[S], int idx, const float (&sel)[TDQ_MAXS]) {
+  if constexpr (S1 <= 2) {
+    T r = v[1];
+    if constexpr (S1 == 2) r = (idx == 2) ? v[2] : r;
+    return r;
+  } else {
+    T r = sel[1] * v[1];
+#pragma unroll
+    for (int q = 2; q <= S1; ++q) r += sel[q] * v[q];
+    return r;
+  }
+}
+
+// forward tanh jet of one feature tile: z -> h
+template <int S, int NSO>
+__device__ __forceinline__ void tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  f32x4 za[S], zb[S];
+#pragma unroll
+  for (int s = SO; s < S; ++s) {
+    za[s] = sel_first<S, S1>(z, sp.ia[s], sp.selA[s]);
+    zb[s] = sel_first<S, S1>(z, sp.ib[s], sp.selB[s]);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float hv, s1;
+    tanh_s1(z[0][c], hv, s1);
+    const float s2 = -2.f * hv * s1;
+    h[0][c] = hv;
+#pragma unroll
+    for (int s = 1; s < SO; ++s) h[s][c] = s1 * z[s][c];
+#pragma unroll
+    for (int s = SO; s < S; ++s) h[s][c] = fmaf(s2 * za[s][c], zb[s][c], s1 * z[s][c]);
+  }
+}
+
+// backward tanh jet of one feature tile from the saved post-activations h: hb -> zb
+template <int S, int NSO>
+__device__ __forceinline__ void tanh_jet_b(const JetSpec& sp, const f32x4 (&h)[S], const f32x4 (&hb)[S],
+                                           f32x4 (&zb)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float hc[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) hc[s] = h[s][c];
+    const float hv = hc[0];
+    const float s1 = fmaf(-hv, hv, 1.f);
+    const float m2h = -2.f * hv;
+    float zbv[S];
+    float sb1 = 0.f, sb2 = 0.f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) zbv[s] = s1 * hb[s][c];
+#pragma unroll
+    for (int s = 1; s < S; ++s) sb1 = fmaf(hc[s], hb[s][c], sb1);
+#pragma unroll
+    for (int s = SO; s < S; ++s) {
+      const float ha = sel_first<S, S1>(hc, sp.ia[s], sp.selA[s]), hq = sel_first<S, S1>(hc, sp.ib[s], sp.selB[s]);
+      const float hbs = hb[s][c];
+      sb2 = fmaf(ha * hq, hbs, sb2);
+      const float ga = m2h * hq * hbs, gb = m2h * ha * hbs;
+      if constexpr (S1 <= 2) {
+#pragma unroll
+        for (int q = 1; q < SO; ++q) {
+          zbv[q] += (sp.ia[s] == q) ? ga : 0.f;
+          zbv[q] += (sp.ib[s] == q) ? gb : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 1; q < SO; ++q) zbv[q] = fmaf(sp.selA[s][q], ga, fmaf(sp.selB[s][q], gb, zbv[q]));
+      }
+    }
+    zbv[0] = fmaf(m2h, sb1, fmaf(-2.f, sb2, zbv[0]));
+#pragma unroll
+    for (int s = 0; s < S; ++s) zb[s][c] = zbv[s];
+  }
+}
+
+// Hs (saved post-activations, fp32): [layer][wg][s][wave][tile][lane][4]
+__device__ __forceinline__ size_t hs_base(int layer, int nwg, int wg, int S, int w, int WT, int lane) {
+  return ((((size_t)layer * nwg + wg) * S * 4 + w) * WT) * 256 + (unsigned)(lane * 4);
+}
+__device__ __forceinline__ int hs_off(int s, int t, int WT) { return (s * 4 * WT + t) * 256; }
+
+// Saved activations move with non-temporal stores (forward) and loads (backward): they are written
+// once, read after the whole forward + loss, and each read is too far from the next use of the
+// line for the caches to help, so allocating them only evicts the weight images and partials that
+// are reused.  A/B on MI355X (AC-SA step): plain 0.532 ms, nt stores 0.520, + nt loads 0.502;
+// keeping the first of the two backward reads of a hidden layer cached (the tanh-adjoint pass reads
+// the same lines right after) 0.494 vs 0.500; nt gradient-slab stores are slower (0.545 vs 0.520:
+// the reduction re-reads them at once).  -DTDQ_TEMPORAL_STORES / -DTDQ_TEMPORAL_LOADS /
+// -DTDQ_NT_C_LOADS / -DTDQ_NT_SLAB build the other variants (profiles/r1_v9_nontemporal_ab.txt).
+__device__ __forceinline__ void hs_store(float* p, const f32x4& v) {
+#ifdef TDQ_TEMPORAL_STORES
+  *reinterpret_cast<f32x4*>(p) = v;
+#else
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#endif
+}
+
+__device__ __forceinline__ f32x4 hs_load(const float* p) {
+#ifdef TDQ_TEMPORAL_LOADS
+  return *reinterpret_cast<const f32x4*>(p);
+#else
+  return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+#endif
+}
+
+// the dK pass's read of h_{i-1} (the same lines are read again by the tanh-adjoint pass)
+__device__ __forceinline__ f32x4 hs_load_c(const float* p) {
+#ifdef TDQ_NT_C_LOADS
+  return hs_load(p);
+#else
+  return *reinterpret_cast<const f32x4*>(p);
+#endif
+}
+
+__device__ __forceinline__ void slab_store(float* p, float v) {
+#ifdef TDQ_NT_SLAB
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// layer 0 (input -> width, VALU; derivative streams are rows of K0): the post-activation streams of
+// feature tile t (forward).
+template <int WT, int S, int NSO>
+__device__ __forceinline__ void h0_jet(const JetSpec& sp, const float* __restrict__ aux, const NetDims& d,
+                                       const float* __restrict__ x, int t, int g, f32x4 (&h)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  const int f0 = 16 * t + 4 * g;
+  f32x4 z[S];
+  z[0] = *reinterpret_cast<const f32x4*>(aux + aux_b0(d, W) + f0);
+#pragma unroll
+  for (int j = 0; j < TDQ_MAXD; ++j)
+    if (j < d.d_in) z[0] += x[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+#pragma unroll
+  for (int s = 1; s < SO; ++s) z[s] = *reinterpret_cast<const f32x4*>(aux + sp.var[s] * W + f0);
+#pragma unroll
+  for (int s = SO; s < S; ++s) z[s] = zero4();
+  tanh_jet_f<S, NSO>(sp, z, h);
+}
+
+// Layer 0's derivative streams are functions of its value stream alone (z_a = a row of K0,
+// z_ab = 0): h_a = s1 K0[a], h_ab = -2 h s1 K0[a] K0[b], s1 = 1 - h^2.  With h0r set the forward
+// saves only the value stream of layer 0 and the backward rebuilds stream s here - 3/4 less
+// layer-0 saved-activation traffic (the step is bound by that traffic) for ~2 VALU ops per value.
+template <int WT, int S, int NSO>
+__device__ __forceinline__ f32x4 h0_stream(const JetSpec& sp, const float* __restrict__ aux, const f32x4& h, int t,
+                                           int g, int s) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  if (s == 0) return h;
+  const int f0 = 16 * t + 4 * g;
+  f32x4 r;
+  if (s < SO) {
+    const f32x4 k = *reinterpret_cast<const f32x4*>(aux + sp.var[s] * W + f0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = fmaf(-h[c], h[c], 1.f) * k[c];
+  } else {
+    const f32x4 ka = *reinterpret_cast<const f32x4*>(aux + sp.var[sp.ia[s]] * W + f0);
+    const f32x4 kb = *reinterpret_cast<const f32x4*>(aux + sp.var[sp.ib[s]] * W + f0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = (-2.f * h[c]) * fmaf(-h[c], h[c], 1.f) * (ka[c] * kb[c]);
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int WT, int S, int NSO, bool LAST>
+__device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)[S][WT / 2],
+                                           const bf16x8* __restrict__ Wi, const float* __restrict__ bi,
+                                           float* __restrict__ Hl, bf16x4* stage, float* hlast,
+                                           const JetSpec& sp, int l, int g) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
+  bf16x8 wh[D], wl[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    wh[k] = Wi[k * 128];
+    wl[k] = Wi[k * 128 + 64];
+  }
+  f32x4 accA[S], accB[S], biasA = zero4(), biasB = zero4();
+#pragma unroll
+  for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
+#pragma unroll
+  for (int o = 0; o <= WT; ++o) {
+    f32x4(&accC)[S] = (o & 1) ? accB : accA;
+    f32x4(&accP)[S] = (o & 1) ? accA : accB;
+    f32x4& biasC = (o & 1) ? biasB : biasA;
+    const f32x4& biasP = (o & 1) ? biasA : biasB;
+    if (o < WT) {  // MFMAs of output tile o
+      biasC = *reinterpret_cast<const f32x4*>(bi + 16 * o + 4 * g);
+#pragma unroll
+      for (int s = 0; s < S; ++s) accC[s] = zero4();
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const int st = o * KB + kb;
+        const bf16x8 Ah = wh[st % D], Al = wl[st % D];
+        if (st + D < NSTEP) {
+          wh[st % D] = Wi[(st + D) * 128];
+          wl[st % D] = Wi[(st + D) * 128 + 64];
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) accC[s] = mfma3(Ah, Al, ah[s][kb], al[s][kb], accC[s]);
+      }
+    }
+    if (o > 0) {  // epilogue of tile o-1 in the same scheduling region
+      const int t = o - 1;
+      f32x4 z[S], h[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) z[s] = accP[s];
+      z[0] += biasP;
+      tanh_jet_f<S, NSO>(sp, z, h);
+#pragma unroll
+      for (int s = 0; s < S; ++s) hs_store(Hl + hs_off(s, t, WT), h[s]);
+      if (LAST) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(h[s], hi, lo);
+          stage[(((s * KB + (t >> 1)) * 2 + 0) * 64 + l) * 2 + (t & 1)] = hi;
+          stage[(((s * KB + (t >> 1)) * 2 + 1) * 64 + l) * 2 + (t & 1)] = lo;
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (!LAST) {  // wave-private region: program order suffices
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        ah[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 0) * 64 + l) * 2]);
+        al[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
+      }
+  }
+}
+
+template <int WT, int S, int NSO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
+                   float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wg = blockIdx.x, nwg = gridDim.x;
+  const int n = wg * 64 + w * 16 + p;
+  const bool valid = n < N;
+  const int nc = valid ? n : N - 1;  // clamped: every load is in bounds, no exec branches
+  const int Lh = d.n_hidden;
+  // wave-private staging image of the next layer's B fragments: [s][kb][hl][lane][2 halves]
+  bf16x4* stage = reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * 2 * 64 * 2);
+  float* hlast = reinterpret_cast<float*>(stage);  // last layer: fp32 h image [s][t][lane][4]
+  const float* Ko = aux + aux_ko(d, W);
+
+  TDQ_TS(0);
+  float x[TDQ_MAXD];
+#pragma unroll
+  for (int j = 0; j < TDQ_MAXD; ++j) x[j] = j < d.d_in ? X[(size_t)nc * d.d_in + j] : 0.f;
+
+  bf16x8 ah[S][KB], al[S][KB];
+
+  // ---- layer 0 (input -> width) on VALU ---------------------------------------------------
+  {
+    float* H0 = Hs + hs_base(0, nwg, wg, S, w, WT, l);
+    const bool save_all = !h0r || Lh == 1;  // else the backward rebuilds streams >= 1 (h0_stream)
+    bf16x4 ph[S], pl[S];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      f32x4 h[S];
+      h0_jet<WT, S, NSO>(sp, aux, d, x, t, g, h);
+      hs_store(H0 + hs_off(0, t, WT), h[0]);
+      if (save_all) {
+#pragma unroll
+        for (int s = 1; s < S; ++s) hs_store(H0 + hs_off(s, t, WT), h[s]);
+      }
+      if (Lh == 1) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(h[s], hi, lo);
+          if (t & 1) {
+            ah[s][t >> 1] = cat8(ph[s], hi);
+            al[s][t >> 1] = cat8(pl[s], lo);
+          } else {
+            ph[s] = hi;
+            pl[s] = lo;
+          }
+        }
+      }
+    }
+  }
+
+  TDQ_TS(1);
+  // ---- hidden layers on bf16x3 MFMA --------------------------------------------------------
+  for (int i = 1; i < Lh - 1; ++i) {
+    fwd_hidden<WT, S, NSO, false>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
+                                  Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+    TDQ_TS(1 + i);
+  }
+  if (Lh >= 2) {
+    const int i = Lh - 1;
+    fwd_hidden<WT, S, NSO, true>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
+                                 Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+    TDQ_TS(1 + i);
+  }
+
+  // ---- output layer (width -> d_out): VALU dot over the staged fp32 h + cross-lane sum ----
+  float v[S][TDQ_MAXO];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = 0.f;
+#pragma unroll
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 kq = *reinterpret_cast<const f32x4*>(Ko + (16 * t + 4 * g + c) * 4);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const float hv = hlast[((s * WT + t) * 64 + l) * 4 + c];
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = fmaf(hv, kq[q], v[s][q]);
+      }
+    }
+  const f32x4 bo = *reinterpret_cast<const f32x4*>(aux + aux_bo(d, W));
+#pragma unroll
+  for (int q = 0; q < TDQ_MAXO; ++q) {
+    if (q >= d.d_out) break;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float r = col4_sum(v[s][q]);
+      if (s == 0) r += bo[q];
+      if (g == 0 && valid) J[((size_t)s * N + n) * d.d_out + q] = r;
+    }
+  }
+  TDQ_TS(15);
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+template <int S, int WT>
+__device__ __forceinline__ void h_tile(f32x4 (&h)[S], const float* __restrict__ Hl, int t) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) h[s] = hs_load(Hl + hs_off(s, t, WT));
+}
+
+// first-layer partials from zb_0 (fp32) of one feature tile: bias b0 and dK0[j][f] (one LDS slot
+// per wave, summed in fixed wave order later)
+template <int WT, int S, int NSO>
+__device__ __forceinline__ void first_layer_partials(const JetSpec& sp, const f32x4 (&zb)[S],
+                                                     const float* __restrict__ xrow, const NetDims& d, int t,
+                                                     int w, int p, int g, float* accB0, float* accK0) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  const int fo = 16 * t + 4 * g + (p >> 2);  // feature this lane stores after row16_sum4
+  {
+    const float r = row16_sum4(zb[0]);
+    if ((p & 3) == 0) accB0[w * W + fo] = r;
+  }
+  for (int j = 0; j < d.d_in; ++j) {
+    const float xj = xrow[j];
+    f32x4 v;  // scalar per component: packed f32 VALU beside MFMAs costs issue cycles
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float a = xj * zb[0][c];
+#pragma unroll
+      for (int s = 1; s < SO; ++s) a += (sp.var[s] == j) ? zb[s][c] : 0.f;
+      v[c] = a;
+    }
+    const float r = row16_sum4(v);
+    if ((p & 3) == 0) accK0[w * TDQ_MAXD * W + j * W + fo] = r;
+  }
+}
+
+// zb of one feature tile -> bias partial of its layer + hi/lo halves into the wave's fragment
+// stage ([s][kb][hl][lane][2 halves] bf16x4, the forward's staging layout)
+template <int WT, int S>
+__device__ __forceinline__ void zb_to_stage(const f32x4 (&zb)[S], const NetDims& d, int t, int w, int l, int p,
+                                            int g, float* accBslot, bf16x4* stage) {
+  constexpr int KB = WT / 2, W = 16 * WT;
+  {
+    const float r = row16_sum4(zb[0]);
+    if ((p & 3) == 0) accBslot[w * W + 16 * t + 4 * g + (p >> 2)] = r;
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    bf16x4 hi, lo;
+    split4(zb[s], hi, lo);
+    stage[(((s * KB + (t >> 1)) * 2 + 0) * 64 + l) * 2 + (t & 1)] = hi;
+    stage[(((s * KB + (t >> 1)) * 2 + 1) * 64 + l) * 2 + (t & 1)] = lo;
+  }
+}
+
+// (d) of hidden layer i: hb_{i-1} = K_i zb_i on bf16x3 MFMA; the epilogue of output tile o-1
+// (tanh-jet adjoint with the saved h_{i-1}, bias partials, split + stage - or, when i = 1, the
+// first-layer partials) runs in the scheduling region of tile o's MFMAs.
+template <int WT, int S, int NSO, bool TO_FIRST>
+__device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], const bf16x8 (&zl)[S][WT / 2],
+                                             const bf16x8* __restrict__ Ki, const float* __restrict__ Hp,
+                                             bf16x4* stage, float* accBslot, float* accK0,
+                                             const float* __restrict__ xrow, const JetSpec& sp, const NetDims& d,
+                                             const float* __restrict__ aux, bool h0r, int w, int l, int p, int g) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
+  bf16x8 wh[D], wl[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    wh[k] = Ki[k * 128];
+    wl[k] = Ki[k * 128 + 64];
+  }
+  // TO_FIRST && h0r: only layer 0's value stream is saved; the others are rebuilt (h0_stream)
+  const bool rec = TO_FIRST && h0r;
+  f32x4 hr[2][S];
+  if (rec) {
+    hr[0][0] = hs_load(Hp + hs_off(0, 0, WT));
+    if (WT > 1) hr[1][0] = hs_load(Hp + hs_off(0, 1, WT));
+  } else {
+    h_tile<S, WT>(hr[0], Hp, 0);
+    if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
+  }
+  f32x4 accA[S], accB[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
+#pragma unroll
+  for (int o = 0; o <= WT; ++o) {
+    f32x4(&accC)[S] = (o & 1) ? accB : accA;
+    f32x4(&accP)[S] = (o & 1) ? accA : accB;
+    if (o < WT) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) accC[s] = zero4();
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const int st = o * KB + kb;
+        const bf16x8 Ah = wh[st % D], Al = wl[st % D];
+        if (st + D < NSTEP) {
+          wh[st % D] = Ki[(st + D) * 128];
+          wl[st % D] = Ki[(st + D) * 128 + 64];
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) accC[s] = mfma3(Ah, Al, zh[s][kb], zl[s][kb], accC[s]);
+      }
+    }
+    if (o > 0) {
+      const int t = o - 1;
+      f32x4 h[S], zb[S];
+      if (rec) {
+        h[0] = hr[t & 1][0];
+        if (t + 2 < WT) hr[t & 1][0] = hs_load(Hp + hs_off(0, t + 2, WT));
+#pragma unroll
+        for (int s = 1; s < S; ++s) h[s] = h0_stream<WT, S, NSO>(sp, aux, h[0], t, g, s);
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) h[s] = hr[t & 1][s];
+        if (t + 2 < WT) h_tile<S, WT>(hr[t & 1], Hp, t + 2);
+      }
+      tanh_jet_b<S, NSO>(sp, h, accP, zb);
+      if (TO_FIRST)
+        first_layer_partials<WT, S, NSO>(sp, zb, xrow, d, t, w, p, g, accBslot, accK0);
+      else
+        zb_to_stage<WT, S>(zb, d, t, w, l, p, g, accBslot, stage);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int WT, int S, int NSO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
+                   const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
+                   int Ptot, NetDims d, JetSpec sp, int rev, int h0r) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int W = 16 * WT;
+  constexpr int KB = WT / 2;
+  // [point][feature] bf16 images (h hi/lo, zb hi/lo).  Row stride 144 bf16 = 72 words (= 8 mod 64)
+  // and the 64-column XOR on bit 3 of the row put the 8 rows of a transposed read's 32-lane half
+  // (4 rows x 2 groups 8 rows apart, 8 words each) on 8 disjoint bank windows: conflict-free.
+  constexpr int RS = 144;
+  constexpr int IMG = 64 * RS;
+  // dK tile ownership: the WT x WT output tiles split into 2 x 2 quadrants, wave w owns quadrant
+  // (w >> 1, w & 1): (WT/2)^2 tiles from WT/2 A and WT/2 B fragments per k-block (a 2 x 8 strip
+  // per wave would need 2 + 8 fragment loads for the same 16 tiles at WT = 8)
+  constexpr int NR = WT / 2;
+  constexpr int NC = WT / 2;
+  // LDS: two image sets (double-buffered over streams: stream s+1's images are written while
+  // stream s's MFMAs read the other set, one barrier per stream) in a union with the (d) pass's
+  // per-wave zb fragment stage, then the bias partials.  The output- and first-layer partials
+  // alias the union: they live while neither images nor stage do.
+  constexpr int U1 = (4 * IMG) / 2;           // one image set, in floats
+  constexpr int U2 = 4 * S * WT * 256;        // per-wave zb fragment stage (bf16 hi/lo)
+  constexpr int U = ((2 * U1 > U2 ? 2 * U1 : U2) + 3) / 4 * 4;
+  static_assert(4 * W * TDQ_MAXO + 4 * TDQ_MAXO + 4 * TDQ_MAXD * W <= U, "partials must fit the union");
+  __bf16* img = reinterpret_cast<__bf16*>(lds);
+  float* accB = lds + U;                      // [3: layer parity 0/1, layer 0][4][W]
+  float* accKo = lds;                         // [4][W * TDQ_MAXO]  (output phase; reduced before any image)
+  float* accBo = accKo + 4 * W * TDQ_MAXO;    // [4][TDQ_MAXO]
+  float* accK0 = accBo + 4 * TDQ_MAXO;        // [4][TDQ_MAXD * W]  (after the last image read)
+
+  const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // rev: tiles in reverse dispatch order - the forward wrote the highest tiles last, so theirs are
+  // the saved activations still resident in the 256 MiB Infinity Cache when the backward starts
+  const int nwg = gridDim.x, wg = rev ? nwg - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int n = wg * 64 + w * 16 + p;
+  const bool valid = n < N;
+  const int nc = valid ? n : N - 1;
+  const float vmask = valid ? 1.f : 0.f;  // zero adjoints for padding points: zb = 0 downstream
+  const int Lh = d.n_hidden;
+  float* gs = slab + (size_t)wg * Ptot;
+  bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * 2 * 64 * 2);
+  auto dw_row = [](int wv, int r) { return (WT / 2) * (wv >> 1) + r; };
+  auto dw_col = [](int wv, int c) { return (WT / 2) * (wv & 1) + c; };
+  // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
+  const int tr_row = 8 * g + ((l & 15) >> 2), tr_col = 4 * (l & 3);
+  const int swz = (g & 1) << 6;  // bit 3 of every row this lane's transposed reads touch
+  const float* xrow = X + (size_t)nc * d.d_in;  // padding points: zb = 0, x is irrelevant
+  TDQ_TS(0);
+
+  bf16x8 zh[S][KB], zl[S][KB];
+
+  // ---- output layer: hb = Ko ub ; dKo += h_last ub ; dbo += ub ; then the top tanh layer's
+  //      adjoint zb_{Lh-1} tile by tile (bias partials + B fragments, or first-layer partials)
+  {
+    const float* Ko = aux + aux_ko(d, W);
+    const float* Hl = Hs + hs_base(Lh - 1, nwg, wg, S, w, WT, l);
+    float* accBslot = Lh >= 2 ? accB + ((Lh - 1) & 1) * 4 * W : accB + 8 * W;
+    float ub[S][TDQ_MAXO];
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q)
+#pragma unroll
+      for (int s = 0; s < S; ++s) ub[s][q] = q < d.d_out ? vmask * dJ[((size_t)s * N + nc) * d.d_out + q] : 0.f;
+    constexpr int DH = WT < 3 ? WT : 3;  // H tiles in flight
+    f32x4 hr[DH][S];
+#pragma unroll
+    for (int k = 0; k < DH; ++k) h_tile<S, WT>(hr[k], Hl, k);
+    bf16x4 ph[S], pl[S];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      f32x4 h[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) h[s] = hr[t % DH][s];
+      if (t + DH < WT) h_tile<S, WT>(hr[t % DH], Hl, t + DH);
+      // hb = Ko ub over the zero-padded 4 output columns: no branches
+      f32x4 hbt[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) hbt[s] = zero4();
+      f32x4 kq[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kq[c] = *reinterpret_cast<const f32x4*>(Ko + (16 * t + 4 * g + c) * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q)
+#pragma unroll
+          for (int s = 0; s < S; ++s) hbt[s][c] = fmaf(kq[c][q], ub[s][q], hbt[s][c]);
+      // dKo[f][q] partials: sum over points of sum_s h_s ub_s
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) {
+        if (q >= d.d_out) break;
+        f32x4 part;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float a = 0.f;
+#pragma unroll
+          for (int s = 0; s < S; ++s) a = fmaf(ub[s][q], h[s][c], a);
+          part[c] = a;
+        }
+        const float r = row16_sum4(part);
+        if ((p & 3) == 0) accKo[w * W * TDQ_MAXO + (16 * t + 4 * g + (p >> 2)) * TDQ_MAXO + q] = r;
+      }
+      f32x4 zb[S];
+      tanh_jet_b<S, NSO>(sp, h, hbt, zb);
+      if (Lh >= 2) {
+        {
+          const float r = row16_sum4(zb[0]);
+          if ((p & 3) == 0) accBslot[w * W + 16 * t + 4 * g + (p >> 2)] = r;
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          bf16x4 hi, lo;
+          split4(zb[s], hi, lo);
+          if (t & 1) {
+            zh[s][t >> 1] = cat8(ph[s], hi);
+            zl[s][t >> 1] = cat8(pl[s], lo);
+          } else {
+            ph[s] = hi;
+            pl[s] = lo;
+          }
+        }
+      } else {
+        first_layer_partials<WT, S, NSO>(sp, zb, xrow, d, t, w, p, g, accBslot, accK0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q) {
+      if (q >= d.d_out) break;
+      const float v = row16_sum(ub[0][q]);
+      if (l == 0) accBo[w * TDQ_MAXO + q] = v;
+    }
+  }
+  // output-layer slab now: its partials alias the images (the first dK pass starts with a barrier)
+  __syncthreads();
+  if (w == 2) {
+    const int ko = off_layer(d, Lh);
+    for (int e = l; e < d.width * d.d_out; e += 64) {
+      const int f = e / d.d_out, q = e - f * d.d_out;
+      const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
+      gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
+    }
+    if (l < d.d_out)
+      gs[ko + d.width * d.d_out + l] =
+          ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
+  }
+  TDQ_TS(1);
+
+  // ---- hidden layers i = Lh-1 .. 1: zh/zl hold zb_i --------------------------------------
+  for (int i = Lh - 1; i >= 1; --i) {
+    const int tsb = 2 + 8 * (Lh - 1 - i);
+    const float* Hp = Hs + hs_base(i - 1, nwg, wg, S, w, WT, l);
+    // layer 0 under h0r: hp keeps the value stream, stream s is rebuilt from it (h0_stream)
+    const bool rec0 = h0r && i == 1;
+    // h_{i-1} tiles of stream 0 for the dK images
+    f32x4 hp[WT];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(0, t, WT));
+    TDQ_TS(tsb);
+
+    // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index.
+    //     Image sets alternate per stream: one barrier per stream (all waves done reading set
+    //     (s+1)&1 for stream s-1, and done writing set s&1), stream s+1's images and stream s+2's
+    //     h_{i-1} loads overlap stream s's MFMAs.
+    f32x4 dw[NR][NC];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dw[r][c] = zero4();
+    const int row = 16 * w + p;
+    const int rsw = ((row >> 3) & 1) << 6;
+    auto write_images = [&](int set, int sn, const f32x4 (&hsrc)[WT]) {
+      __bf16* im = img + set * (4 * IMG);
+#pragma unroll
+      for (int t = 0; t < WT; ++t) {
+        bf16x4 hi, lo;
+        split4(rec0 ? h0_stream<WT, S, NSO>(sp, aux, hsrc[t], t, g, sn) : hsrc[t], hi, lo);
+        const int off = row * RS + ((16 * t + 4 * g) ^ rsw);
+        *reinterpret_cast<bf16x4*>(im + off) = hi;
+        *reinterpret_cast<bf16x4*>(im + IMG + off) = lo;
+        *reinterpret_cast<bf16x4*>(im + 2 * IMG + off) = half8(zh[sn][t >> 1], t & 1);
+        *reinterpret_cast<bf16x4*>(im + 3 * IMG + off) = half8(zl[sn][t >> 1], t & 1);
+      }
+    };
+    __syncthreads();  // previous readers of the region (zb stage) done; bias partials landed
+    if (w == 0) {     // bias of layer i
+      const float* accBi = accB + (i & 1) * 4 * W;
+      const int bo = off_layer(d, i) + d.width * d.width;
+      for (int f = l; f < d.width; f += 64)
+        gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
+    }
+    write_images(0, 0, hp);
+    if (S > 1 && !rec0) {
+#pragma unroll
+      for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(1, t, WT));
+    }
+    __syncthreads();
+    TDQ_TS(tsb + 1);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s + 1 < S) {
+        write_images((s + 1) & 1, s + 1, hp);
+        if (s + 2 < S && !rec0) {
+#pragma unroll
+          for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(s + 2, t, WT));
+        }
+      }
+      const __bf16* im = img + (s & 1) * (4 * IMG);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {  // 64 points = 2 k-blocks of 32
+        bf16x8 Ah[NR], Al[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int off = (32 * kb + tr_row) * RS + ((16 * dw_row(w, r) + tr_col) ^ swz);
+          Ah[r] = cat8(tr_read(im + off), tr_read(im + off + 4 * RS));
+          Al[r] = cat8(tr_read(im + IMG + off), tr_read(im + IMG + off + 4 * RS));
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int off = (32 * kb + tr_row) * RS + ((16 * dw_col(w, c) + tr_col) ^ swz);
+          const bf16x8 Bh = cat8(tr_read(im + 2 * IMG + off), tr_read(im + 2 * IMG + off + 4 * RS));
+          const bf16x8 Bl = cat8(tr_read(im + 3 * IMG + off), tr_read(im + 3 * IMG + off + 4 * RS));
+#pragma unroll
+          for (int r = 0; r < NR; ++r) dw[r][c] = mfma3(Ah[r], Al[r], Bh, Bl, dw[r][c]);
+        }
+      }
+      __syncthreads();  // set s&1 read by every wave; set (s+1)&1 written by every wave
+    }
+    {
+      const int ko = off_layer(d, i);
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c2 = 0; c2 < NC; ++c2) {
+          const int out = 16 * dw_col(w, c2) + p;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int in = 16 * dw_row(w, r) + 4 * g + c;
+            if (in < d.width && out < d.width) slab_store(gs + ko + in * d.width + out, dw[r][c2][c]);
+          }
+        }
+    }
+    TDQ_TS(tsb + 2);
+    TDQ_TS(tsb + 3);
+
+    // (d) hb_{i-1} = K_i zb_i, fused with the adjoint of tanh layer i-1
+    const bf16x8* Ki = Kimg + (size_t)(i - 1) * (WT * KB) * 128 + l;
+    if (i >= 2) {
+      bwd_hidden_d<WT, S, NSO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, aux,
+                                      h0r != 0, w, l, p, g);
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {  // wave-private stage: program order suffices
+          zh[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 0) * 64 + l) * 2]);
+          zl[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
+        }
+    } else {
+      bwd_hidden_d<WT, S, NSO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, aux, h0r != 0, w, l,
+                                     p, g);
+    }
+    TDQ_TS(tsb + 4);
+  }
+
+  // ---- first-layer / output-layer slabs (partials of all waves are in LDS) ----------------
+  __syncthreads();
+  if (w == 0) {
+    const float* accB0 = accB + 8 * W;
+    const int bo = d.d_in * d.width;
+    for (int f = l; f < d.width; f += 64)
+      gs[bo + f] = ((accB0[f] + accB0[W + f]) + accB0[2 * W + f]) + accB0[3 * W + f];
+  } else if (w == 1) {
+    for (int e = l; e < d.d_in * d.width; e += 64) {
+      const int j = e / d.width, f = e - j * d.width;
+      const int k = j * W + f;
+      gs[e] = ((accK0[k] + accK0[TDQ_MAXD * W + k]) + accK0[2 * TDQ_MAXD * W + k]) + accK0[3 * TDQ_MAXD * W + k];
+    }
+  }
+  TDQ_TS(63);
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launch templates (instantiated per width class in jet_bf3_w{2,4,8}.hip)
+// ------------------------------------------------------------------------------------------
+inline size_t fwd_bf3_lds(int WT, int S) { return (size_t)4 * S * WT * 1024; }
+
+// backward tile order: reverse (default) or dispatch order (TDQ_BWD_ORDER=forward, for A/B runs)
+inline int bwd_reverse_order() {
+  static const int rev = [] {
+    const char* e = getenv("TDQ_BWD_ORDER");
+    return (e != nullptr && e[0] == 'f') ? 0 : 1;
+  }();
+  return rev;
+}
+
+// layer-0 activations recomputed in the backward (default) or saved by the forward
+// (TDQ_H0_RECOMPUTE=0, for A/B runs).  Read once per process: forward and backward always agree.
+inline int h0_recompute() {
+  static const int on = [] {
+    const char* e = getenv("TDQ_H0_RECOMPUTE");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
+inline size_t bwd_bf3_lds(int WT, int S) {
+  const int W = 16 * WT;
+  const size_t u1 = (size_t)(4 * 64 * 144) / 2, u2 = (size_t)4 * S * WT * 256;
+  const size_t u = ((2 * u1 > u2 ? 2 * u1 : u2) + 3) / 4 * 4;
+  return (u + 12 * W) * sizeof(float);
+}
+
+struct Bf3Args {
+  const float* X;
+  const float* aux;
+  const bf16x8* img;
+  const float* dJ;   // bwd
+  float* J;          // fwd
+  float* Hs;
+  float* slab;       // bwd
+  int N, Ptot;
+  NetDims d;
+  JetSpec sp;
+  hipStream_t st;
+};
+
+template <int WT, int S, int NSO>
+int launch_fwd_bf3(const Bf3Args& a) {
+  const int nwg = (a.N + 63) / 64;
+  const size_t lds = fwd_bf3_lds(WT, S);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_fwd_bf3_kernel<WT, S, NSO>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
+                     a.Hs, a.N, a.d, a.sp, h0_recompute());
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int WT, int S, int NSO>
+int launch_bwd_bf3(const Bf3Args& a) {
+  const int nwg = (a.N + 63) / 64;
+  const size_t lds = bwd_bf3_lds(WT, S);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_bwd_bf3_kernel<WT, S, NSO>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute());
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// per-width-class entry points (jet_bf3_w{2,4,8}.hip); return hipErrorInvalidValue when
+// (S, NSO) has no instantiation
+int bf3_fwd_w2(int S, int nso, const Bf3Args& a);
+int bf3_fwd_w4(int S, int nso, const Bf3Args& a);
+int bf3_fwd_w8(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w2(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w4(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w8(int S, int nso, const Bf3Args& a);
