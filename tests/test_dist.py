@@ -1,4 +1,4 @@
-"""Data parallelism without a cluster: gloo on CPU, world_size 2.
+"""Data parallelism without a cluster: gloo on CPU, world_size 2 and 4.
 
 Asserts that sharded DP (collocation points + SA weights split by rank, replicated BC terms
 scaled by 1/world, one flat all-reduce) reproduces the single-process full-batch loss,
@@ -55,7 +55,8 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_dp_gloo_matches_single_process():
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_gloo_matches_single_process(world):
     ref = _build(False)
     eng = ref._get_engine(None, 10)
     loss, grads, terms = eng._phase_a()
@@ -68,7 +69,7 @@ def test_dp_gloo_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=280)
@@ -128,3 +129,70 @@ def test_minibatches_single_process():
     assert m.minibatches(100) == [(0, 100), (100, 200), (200, 300)]
     with pytest.raises(ValueError):
         m.minibatches(0)
+
+
+def _discovery_problem():
+    import math
+    import numpy as np
+    x = np.linspace(-1, 1, 21)
+    t = np.linspace(0, 1, 9)
+    X, T = np.meshgrid(x, t)
+    xs, ts = X.reshape(-1, 1), T.reshape(-1, 1)            # 189 points: uneven shards
+    u = np.sin(math.pi * xs) * np.exp(-0.5 * ts)
+
+    def f_model(u_model, var, x, t):
+        uu = u_model(torch.cat([x, t], 1))
+        return tdq.grad(uu, t) - var[0] * tdq.grad(tdq.grad(uu, x), x)
+
+    return f_model, xs, ts, u
+
+
+def _build_discovery(dist):
+    import numpy as np
+    f_model, xs, ts, u = _discovery_problem()
+    torch.manual_seed(0)
+    var = [tdq.Variable(0.1)]
+    cw = np.linspace(0.5, 1.5, xs.shape[0]).reshape(-1, 1).astype(np.float32)
+    m = tdq.DiscoveryModel(verbose=False)
+    m.compile([2, 10, 10, 1], f_model, [xs, ts], u, var, col_weights=cw, backend="jet", device="cpu",
+              dist=dist)
+    return m, var
+
+
+def _worker_discovery(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(backend="gloo", device="cpu")
+    m, var = _build_discovery(True)
+    m.fit(tf_iter=4)
+    res = {"rank": rank, "flat": m.u_model.flat.detach().clone(), "var": float(var[0].detach()),
+           "cw": m.col_weights.detach().clone(), "lo": m._lo, "hi": m._hi}
+    q.put(res)
+    ctx.barrier()
+    pdist.destroy()
+
+
+@pytest.mark.timeout(300)
+def test_discovery_dp_gloo_matches_single_process():
+    """DiscoveryModel under DP: data points and their SA collocation weights sharded, network and
+    PDE coefficients all-reduced - same trajectory as the single-process full batch."""
+    ref, rvar = _build_discovery(False)
+    ref.fit(tf_iter=4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_discovery, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=280) for _ in range(2)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert torch.equal(res[0]["flat"], res[1]["flat"])
+    assert torch.allclose(res[0]["flat"], ref.u_model.flat.detach(), atol=1e-5)
+    assert res[0]["var"] == pytest.approx(float(rvar[0].detach()), rel=1e-4, abs=1e-7)
+    cw = torch.cat([r["cw"] for r in res])
+    assert torch.allclose(cw, ref.col_weights.detach(), atol=1e-5)
