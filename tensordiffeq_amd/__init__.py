@@ -22,7 +22,7 @@ networks = models.networks
 
 __version__ = "0.2.0"
 
-from . import config, metrics  # noqa: E402
+from . import config, metrics, profiling  # noqa: E402
 from .config import SolverConfig  # noqa: E402
 
 __all__ = ["models", "networks", "plotting", "utils", "helpers", "optimizers", "boundaries",

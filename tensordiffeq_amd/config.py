@@ -16,6 +16,8 @@ fused_loss             TDQ_FUSED_LOSS=0 disables   single-kernel loss program
 allow_torch_fallback   TDQ_ALLOW_TORCH_FALLBACK    1: let GPU runs fall back to torch ops
 lbfgs                  TDQ_LBFGS                   auto (device on GPU, host on CPU) | device
                                                    (GPU-resident kernels, graph-replayed) | host
+(profiling)            TDQ_PROFILE                 directory: every fit() runs under torch.profiler
+                                                   -> trace.json + kernels.txt (profiling.py)
 =====================  ==========================  =========================================
 """
 from __future__ import annotations

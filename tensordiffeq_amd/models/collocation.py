@@ -388,6 +388,11 @@ class CollocationSolverND:
         return [(i * batch_sz, (i + 1) * batch_sz) for i in range(nb)]
 
     def fit(self, tf_iter=0, newton_iter=0, batch_sz=None, newton_eager=True):
+        from ..profiling import maybe_profile
+        with maybe_profile(f"CollocationSolverND.fit(tf_iter={tf_iter}, newton_iter={newton_iter})"):
+            return self._fit(tf_iter, newton_iter, batch_sz, newton_eager)
+
+    def _fit(self, tf_iter, newton_iter, batch_sz, newton_eager):
         ctx = self.dist_ctx
         batches = self.minibatches(batch_sz)
         if self.verbose and ctx.rank == 0:

@@ -154,7 +154,9 @@ class DiscoveryModel:
         return self._get_engine(1).run(1)
 
     def fit(self, tf_iter):
-        self.train_loop(tf_iter)
+        from ..profiling import maybe_profile
+        with maybe_profile(f"DiscoveryModel.fit(tf_iter={tf_iter})"):
+            self.train_loop(tf_iter)
 
     def train_loop(self, tf_iter):
         ctx = self.dist_ctx

@@ -47,3 +47,17 @@ def test_metrics_jsonl(tmp_path):
     assert adam[-1]["pts_per_s"] > 0 and math.isfinite(adam[-1]["loss"])
     assert any(r["phase"] == "lbfgs" for r in recs)
     assert np.isclose(adam[-1]["loss"], m.losses[9]["Total Loss"], rtol=1e-6)
+
+
+def test_kernel_profile_writes_trace_and_table(tmp_path, monkeypatch):
+    """TDQ_PROFILE wraps fit() in torch.profiler: a Chrome trace and a kernel table per run."""
+    from tests.test_solver import compiled
+    monkeypatch.setenv("TDQ_PROFILE", str(tmp_path / "prof"))
+    m = compiled("jet")
+    m.fit(tf_iter=3)
+    trace = tmp_path / "prof" / "trace.json"
+    table = tmp_path / "prof" / "kernels.txt"
+    assert trace.exists() and trace.stat().st_size > 0
+    lines = table.read_text().splitlines()
+    assert lines[0].startswith("# CollocationSolverND.fit(tf_iter=3")
+    assert len(lines) > 3 and "%" in lines[2]

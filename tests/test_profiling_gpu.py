@@ -1,0 +1,18 @@
+"""Built-in profiler on the GPU: graph-replayed HIP kernels appear in the kernel table."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_profile_sees_graph_replayed_jet_kernels(tmp_path, monkeypatch):
+    import bench
+    monkeypatch.setenv("TDQ_PROFILE", str(tmp_path / "p"))
+    m = bench.build_problem(2048, 1, "hip", torch.device("cuda", 0), False)
+    m.fit(tf_iter=5)
+    text = (tmp_path / "p" / "kernels.txt").read_text()
+    assert text.splitlines()[1].startswith("# device kernels")
+    assert "jet_bwd_bf3_kernel" in text and "adam_multi_kernel" in text
+    assert os.path.getsize(tmp_path / "p" / "trace.json") > 0
