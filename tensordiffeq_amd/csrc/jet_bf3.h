@@ -614,6 +614,16 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // [point][feature] bf16 images (h hi/lo, zb hi/lo).  Row stride 144 bf16 = 72 words (= 8 mod 64)
   // and the 64-column XOR on bit 3 of the row put the 8 rows of a transposed read's 32-lane half
   // (4 rows x 2 groups 8 rows apart, 8 words each) on 8 disjoint bank windows: conflict-free.
+  // Inside each 16-column block the 4-column chunks are XOR-permuted by bits 2-3 of the row
+  // (chunk' = chunk ^ ((row >> 2) & 3)): a ds_write_b64 lane group (16 rows, one chunk, banks
+  // mod 32) then covers 32 distinct banks instead of 8 (4-way conflicts on every image store), and
+  // a transposed read still fetches each row's same 8-word window, each lane at its chunk's new
+  // place.
+#ifdef TDQ_NO_CHUNK_SWIZZLE
+  constexpr int CHUNK_SWZ = 0;
+#else
+  constexpr int CHUNK_SWZ = 1;
+#endif
   constexpr int RS = 144;
   constexpr int IMG = 64 * RS;
   // dK tile ownership: the WT x WT output tiles split into 2 x 2 quadrants, wave w owns quadrant
@@ -647,6 +657,10 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
   const int tr_row = 8 * g + ((l & 15) >> 2), tr_col = 4 * (l & 3);
   const int swz = (g & 1) << 6;  // bit 3 of every row this lane's transposed reads touch
+  // the chunk swizzle of the rows this lane reads: rows 8g + q (first read) and 8g + 4 + q
+  // (second read), q < 4, so (row >> 2) & 3 = 2g & 3 and (2g + 1) & 3
+  const int tr_col1 = CHUNK_SWZ ? 4 * ((l & 3) ^ ((2 * g) & 3)) : tr_col;
+  const int tr_col2 = CHUNK_SWZ ? 4 * ((l & 3) ^ ((2 * g + 1) & 3)) : tr_col;
   const float* xrow = X + (size_t)nc * d.d_in;  // padding points: zb = 0, x is irrelevant
   TDQ_TS(0);
 
@@ -764,11 +778,12 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       {
         const int row = 16 * w + p;
         const int rsw = ((row >> 3) & 1) << 6;
+        const int wch = CHUNK_SWZ ? (g ^ ((row >> 2) & 3)) : g;  // swizzled 4-column chunk
 #pragma unroll
         for (int t = 0; t < WT; ++t) {
           bf16x4 hi, lo;
           split4(rec0 ? h0_stream<WT, S, NSO>(sp, aux, hp[t], t, g, s) : hp[t], hi, lo);
-          const int off = row * RS + ((16 * t + 4 * g) ^ rsw);
+          const int off = row * RS + ((16 * t + 4 * wch) ^ rsw);
           *reinterpret_cast<bf16x4*>(img + off) = hi;
           *reinterpret_cast<bf16x4*>(img + IMG + off) = lo;
           *reinterpret_cast<bf16x4*>(img + 2 * IMG + off) = half8(zh[s][t >> 1], t & 1);
@@ -786,15 +801,17 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
         bf16x8 Ah[NR], Al[NR];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-          const int off = (32 * kb + tr_row) * RS + ((16 * dw_row(w, r) + tr_col) ^ swz);
-          Ah[r] = cat8(tr_read(img + off), tr_read(img + off + 4 * RS));
-          Al[r] = cat8(tr_read(img + IMG + off), tr_read(img + IMG + off + 4 * RS));
+          const int off = (32 * kb + tr_row) * RS + ((16 * dw_row(w, r) + tr_col1) ^ swz);
+          const int of2 = (32 * kb + tr_row + 4) * RS + ((16 * dw_row(w, r) + tr_col2) ^ swz);
+          Ah[r] = cat8(tr_read(img + off), tr_read(img + of2));
+          Al[r] = cat8(tr_read(img + IMG + off), tr_read(img + IMG + of2));
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          const int off = (32 * kb + tr_row) * RS + ((16 * dw_col(w, c) + tr_col) ^ swz);
-          const bf16x8 Bh = cat8(tr_read(img + 2 * IMG + off), tr_read(img + 2 * IMG + off + 4 * RS));
-          const bf16x8 Bl = cat8(tr_read(img + 3 * IMG + off), tr_read(img + 3 * IMG + off + 4 * RS));
+          const int off = (32 * kb + tr_row) * RS + ((16 * dw_col(w, c) + tr_col1) ^ swz);
+          const int of2 = (32 * kb + tr_row + 4) * RS + ((16 * dw_col(w, c) + tr_col2) ^ swz);
+          const bf16x8 Bh = cat8(tr_read(img + 2 * IMG + off), tr_read(img + 2 * IMG + of2));
+          const bf16x8 Bl = cat8(tr_read(img + 3 * IMG + off), tr_read(img + 3 * IMG + of2));
 #pragma unroll
           for (int r = 0; r < NR; ++r) dw[r][c] = mfma3(Ah[r], Al[r], Bh, Bl, dw[r][c]);
         }
