@@ -32,6 +32,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 METRIC = "collocation-pts/sec + L2 rel-error, Allen-Cahn SA-PINN @ 1/2/4/8 GPU"
+PRECISION_NOTES = {
+    "bf16x3": "bf16x3: split-bf16 MFMA (hi*hi+hi*lo+lo*hi), fp32 accumulate, fp32 elementwise/loss/optimizer",
+    "bf16": "bf16: bf16 activations x split-bf16 weights (hi*hi+lo*hi), fp32 accumulate, "
+            "fp32 elementwise/loss/optimizer",
+    "fp32": "fp32 MFMA",
+}
 
 
 def build_problem(n_per_gpu, world, backend, device, dist, precision=None):
@@ -95,8 +101,9 @@ def main(argv=None):
     ap.add_argument("--npts", type=int, default=50000, help="collocation points per GPU")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--no-l2", action="store_true")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"],
-                    help="GEMM precision of the HIP jet kernels (bf16x3 = split-bf16 MFMA, fp32 accumulate)")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp32"],
+                    help="GEMM precision of the HIP jet kernels (bf16x3 = split-bf16 MFMA, fp32 accumulate; "
+                         "bf16 = bf16 activations x split-bf16 weights)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -152,14 +159,12 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if (backend == "hip" and args.precision == "bf16x3") else "fp32",
+            "dtype": "bf16" if (backend == "hip" and args.precision != "fp32") else "fp32",
             "data": "synthetic (LHS collocation points, random Keras-init weights); L2 on data/AC.mat",
             "config": {"model": "Allen-Cahn SA-PINN tanh MLP [2,128,128,128,128,1]",
                        "global_batch": n_glob, "seq_len": None, "parallelism": f"dp{world}",
                        "points_per_gpu": args.npts, "backend": backend,
-                       "precision": (("bf16x3: split-bf16 MFMA (hi*hi+hi*lo+lo*hi), fp32 accumulate, "
-                                      "fp32 elementwise/loss/optimizer") if args.precision == "bf16x3"
-                                     else "fp32 MFMA") if backend == "hip" else "fp32",
+                       "precision": PRECISION_NOTES[args.precision] if backend == "hip" else "fp32",
                        "bc_points": "IC 512 (SA) + periodic 2x201 (u, u_x)"},
             "loss_after": loss,
             "l2_rel_error_after_steps": l2,

@@ -26,7 +26,7 @@ def parser(desc, iters=10000, newton=0, n_f=None):
     ap.add_argument("--n-f", type=int, default=n_f, help="collocation points (reference setting by default)")
     ap.add_argument("--device", default=None, help="cuda / cpu (default: cuda if available)")
     ap.add_argument("--backend", default="auto", help="auto | hip | jet | autograd")
-    ap.add_argument("--precision", default=None, help="bf16x3 | fp32 (HIP jet GEMMs)")
+    ap.add_argument("--precision", default=None, help="bf16x3 | bf16 | fp32 (HIP jet GEMMs)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--plot", action="store_true", help="draw the reference-style figures")
     ap.add_argument("--quiet", action="store_true")

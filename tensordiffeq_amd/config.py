@@ -6,7 +6,8 @@ environment overrides so that a run can be re-tuned without code changes.
 field                  env var                     meaning
 =====================  ==========================  =========================================
 backend                TDQ_BACKEND                 auto | hip | jet | autograd
-precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | fp32 (fp32 MFMA)
+precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 activations,
+                                                   split weights) | fp32 (fp32 MFMA)
 seed                   TDQ_SEED                    global seed applied at compile
 periodic_legacy        TDQ_PERIODIC_LEGACY         1: reference periodic-BC quirk (B12)
 log_every              TDQ_LOG_EVERY               progress / metrics cadence (steps)
@@ -70,7 +71,7 @@ class SolverConfig:
     def validate(self):
         if self.backend not in ("auto", "hip", "jet", "autograd"):
             raise ValueError(f"backend {self.backend!r}")
-        if self.precision not in ("bf16x3", "fp32"):
+        if self.precision not in ("bf16x3", "bf16", "fp32"):
             raise ValueError(f"precision {self.precision!r}")
         if self.log_every < 1:
             raise ValueError("log_every must be >= 1")

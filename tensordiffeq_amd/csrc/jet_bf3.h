@@ -79,6 +79,24 @@ __device__ __forceinline__ f32x4 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 b
   return mfma_bf(ah, bh, c);
 }
 
+// activation-operand products.  LO (precision "bf16x3"): activations split hi + lo like the weights,
+// 3 MFMAs per product.  !LO (precision "bf16"): activations rounded to bf16 once (8-bit mantissa),
+// weights still hi + lo: 2 MFMAs, half the activation fragments / staging / images, which is what
+// lets two workgroups share a CU.
+template <bool LO>
+__device__ __forceinline__ f32x4 mfma_w(bf16x8 ah, bf16x8 al, const bf16x8& bh, const bf16x8& bl, f32x4 c) {
+  c = mfma_bf(al, bh, c);
+  if constexpr (LO) c = mfma_bf(ah, bl, c);
+  return mfma_bf(ah, bh, c);
+}
+// dK products: both operands are activations (saved h, adjoint zb)
+template <bool LO>
+__device__ __forceinline__ f32x4 mfma_aa(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                         f32x4 c) {
+  if constexpr (LO) return mfma3(ah, al, bh, bl, c);
+  return mfma_bf(ah, bh, c);
+}
+
 // hi = rne_bf16(x), lo = rne_bf16(x - hi), two values per v_cvt_pk_bf16_f32
 __device__ __forceinline__ void split4(const f32x4 v, bf16x4& hi, bf16x4& lo) {
   u32x2 H, L;
@@ -95,6 +113,20 @@ __device__ __forceinline__ void split4(const f32x4 v, bf16x4& hi, bf16x4& lo) {
   }
   hi = __builtin_bit_cast(bf16x4, H);
   lo = __builtin_bit_cast(bf16x4, L);
+}
+
+// hi only (precision "bf16")
+__device__ __forceinline__ bf16x4 cvt_hi4(const f32x4 v) {
+  return __builtin_convertvector(v, bf16x4);
+}
+
+// split (LO) or round (!LO) one 4-element accumulator row
+template <bool LO>
+__device__ __forceinline__ void split_or_round(const f32x4 v, bf16x4& hi, bf16x4& lo) {
+  if constexpr (LO)
+    split4(v, hi, lo);
+  else
+    hi = cvt_hi4(v);
 }
 
 __device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
@@ -220,29 +252,54 @@ __device__ __forceinline__ int hs_off(int s, int t, int WT) { return (s * 4 * WT
 // the same lines right after) 0.494 vs 0.500; nt gradient-slab stores are slower (0.545 vs 0.520:
 // the reduction re-reads them at once).  -DTDQ_TEMPORAL_STORES / -DTDQ_TEMPORAL_LOADS /
 // -DTDQ_NT_C_LOADS / -DTDQ_NT_SLAB build the other variants (profiles/r1_v9_nontemporal_ab.txt).
-__device__ __forceinline__ void hs_store(float* p, const f32x4& v) {
+// Saved-activation regions and weight images are addressed through buffer resources: the lane
+// offset (lane * 16 bytes) is ONE VGPR shared by every access and the tile's uniform byte offset
+// goes to soffset / the immediate field.  Per-lane 64-bit pointers plus tile offsets beyond the
+// global instructions' 4 KiB immediate range cost a VGPR pair per distinct tile.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct Tl {
+  __amdgpu_buffer_rsrc_t r;
+  int v;
+};
+__device__ __forceinline__ Tl tl_make(const void* uniform_base, int lane) {
+  return Tl{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_base), 0, 0x7fffffff, 0x00020000), lane * 16};
+}
 #ifdef TDQ_TEMPORAL_STORES
-  *reinterpret_cast<f32x4*>(p) = v;
+#define TDQ_POL_ST 0
 #else
-  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#define TDQ_POL_ST 2  // nt
 #endif
-}
-
-__device__ __forceinline__ f32x4 hs_load(const float* p) {
 #ifdef TDQ_TEMPORAL_LOADS
-  return *reinterpret_cast<const f32x4*>(p);
+#define TDQ_POL_LD 0
 #else
-  return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+#define TDQ_POL_LD 2  // nt
+#endif
+// wave w's region of saved layer `layer` (uniform base; the lane offset lives in Tl::v)
+template <int WT>
+__device__ __forceinline__ Tl hs_region(const float* Hs, int layer, int nwg, int wg, int S, int w, int lane) {
+  return tl_make(Hs + hs_base(layer, nwg, wg, S, w, WT, 0), lane);
+}
+template <int WT>
+__device__ __forceinline__ void hs_store(const Tl& T, int s, int t, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_ST);
+}
+template <int WT>
+__device__ __forceinline__ f32x4 hs_load(const Tl& T, int s, int t) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_LD));
+}
+// the dK pass's read of h_{i-1} (the same lines are read again by the tanh-adjoint pass): cached
+template <int WT>
+__device__ __forceinline__ f32x4 hs_load_c(const Tl& T, int s, int t) {
+#ifdef TDQ_NT_C_LOADS
+  return hs_load<WT>(T, s, t);
+#else
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_off(s, t, WT) * 4, 0));
 #endif
 }
-
-// the dK pass's read of h_{i-1} (the same lines are read again by the tanh-adjoint pass)
-__device__ __forceinline__ f32x4 hs_load_c(const float* p) {
-#ifdef TDQ_NT_C_LOADS
-  return hs_load(p);
-#else
-  return *reinterpret_cast<const f32x4*>(p);
-#endif
+// hi / lo A fragment of step `st` of a layer's weight image (lo 64 lanes = 1 KiB later)
+__device__ __forceinline__ void img_frag(const Tl& I, int st, bf16x8& hi, bf16x8& lo) {
+  hi = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(I.r, I.v, st * 2048, 0));
+  lo = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(I.r, I.v, st * 2048 + 1024, 0));
 }
 
 __device__ __forceinline__ void slab_store(float* p, float v) {
@@ -299,18 +356,30 @@ __device__ __forceinline__ f32x4 h0_stream(const JetSpec& sp, const float* __res
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int WT, int S, int NSO, bool LAST>
-__device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)[S][WT / 2],
-                                           const bf16x8* __restrict__ Wi, const float* __restrict__ bi,
-                                           float* __restrict__ Hl, bf16x4* stage, float* hlast,
+// output layer (width -> d_out, VALU) of one feature tile of the last hidden layer, straight from
+// the epilogue registers: per-lane partial dots, summed across the 4 row groups at the end
+template <int S>
+__device__ __forceinline__ void out_dot(const f32x4 (&h)[S], const float* __restrict__ Ko, int t, int g,
+                                        float (&v)[S][TDQ_MAXO]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 kq = *reinterpret_cast<const f32x4*>(Ko + (16 * t + 4 * g + c) * 4);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = fmaf(h[s][c], kq[q], v[s][q]);
+  }
+}
+
+template <int WT, int S, int NSO, bool LO, bool LAST>
+__device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)[S][WT / 2], const Tl& Wi,
+                                           const float* __restrict__ bi, const Tl& Hl, bf16x4* stage,
+                                           const float* __restrict__ Ko, float (&vout)[S][TDQ_MAXO],
                                            const JetSpec& sp, int l, int g) {
-  constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
+  constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4, HL = LO ? 2 : 1;
   bf16x8 wh[D], wl[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    wh[k] = Wi[k * 128];
-    wl[k] = Wi[k * 128 + 64];
-  }
+  for (int k = 0; k < D; ++k) img_frag(Wi, k, wh[k], wl[k]);
   f32x4 accA[S], accB[S], biasA = zero4(), biasB = zero4();
 #pragma unroll
   for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
@@ -328,12 +397,9 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       for (int kb = 0; kb < KB; ++kb) {
         const int st = o * KB + kb;
         const bf16x8 Ah = wh[st % D], Al = wl[st % D];
-        if (st + D < NSTEP) {
-          wh[st % D] = Wi[(st + D) * 128];
-          wl[st % D] = Wi[(st + D) * 128 + 64];
-        }
+        if (st + D < NSTEP) img_frag(Wi, st + D, wh[st % D], wl[st % D]);
 #pragma unroll
-        for (int s = 0; s < S; ++s) accC[s] = mfma3(Ah, Al, ah[s][kb], al[s][kb], accC[s]);
+        for (int s = 0; s < S; ++s) accC[s] = mfma_w<LO>(Ah, Al, ah[s][kb], al[s][kb], accC[s]);
       }
     }
     if (o > 0) {  // epilogue of tile o-1 in the same scheduling region
@@ -344,17 +410,16 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       z[0] += biasP;
       tanh_jet_f<S, NSO>(sp, z, h);
 #pragma unroll
-      for (int s = 0; s < S; ++s) hs_store(Hl + hs_off(s, t, WT), h[s]);
+      for (int s = 0; s < S; ++s) hs_store<WT>(Hl, s, t, h[s]);
       if (LAST) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
+        out_dot<S>(h, Ko, t, g, vout);
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           bf16x4 hi, lo;
-          split4(h[s], hi, lo);
-          stage[(((s * KB + (t >> 1)) * 2 + 0) * 64 + l) * 2 + (t & 1)] = hi;
-          stage[(((s * KB + (t >> 1)) * 2 + 1) * 64 + l) * 2 + (t & 1)] = lo;
+          split_or_round<LO>(h[s], hi, lo);
+          stage[(((s * KB + (t >> 1)) * HL + 0) * 64 + l) * 2 + (t & 1)] = hi;
+          if constexpr (LO) stage[(((s * KB + (t >> 1)) * HL + 1) * 64 + l) * 2 + (t & 1)] = lo;
         }
       }
     }
@@ -365,14 +430,14 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
     for (int s = 0; s < S; ++s)
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        ah[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 0) * 64 + l) * 2]);
-        al[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
+        ah[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * HL + 0) * 64 + l) * 2]);
+        if constexpr (LO) al[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * HL + 1) * 64 + l) * 2]);
       }
   }
 }
 
-template <int WT, int S, int NSO>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <int WT, int S, int NSO, bool LO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LO ? 1 : 2, LO ? 1 : 2)))
 jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
                    float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
@@ -386,8 +451,8 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const int nc = valid ? n : N - 1;  // clamped: every load is in bounds, no exec branches
   const int Lh = d.n_hidden;
   // wave-private staging image of the next layer's B fragments: [s][kb][hl][lane][2 halves]
-  bf16x4* stage = reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * 2 * 64 * 2);
-  float* hlast = reinterpret_cast<float*>(stage);  // last layer: fp32 h image [s][t][lane][4]
+  constexpr int HL = LO ? 2 : 1;
+  bf16x4* stage = reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * HL * 64 * 2);
   const float* Ko = aux + aux_ko(d, W);
 
   TDQ_TS(0);
@@ -396,35 +461,39 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   for (int j = 0; j < TDQ_MAXD; ++j) x[j] = j < d.d_in ? X[(size_t)nc * d.d_in + j] : 0.f;
 
   bf16x8 ah[S][KB], al[S][KB];
+  float v[S][TDQ_MAXO];  // output-layer partial dots (last hidden layer's epilogue)
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = 0.f;
 
   // ---- layer 0 (input -> width) on VALU ---------------------------------------------------
   {
-    float* H0 = Hs + hs_base(0, nwg, wg, S, w, WT, l);
+    const Tl H0 = hs_region<WT>(Hs, 0, nwg, wg, S, w, l);
     const bool save_all = !h0r || Lh == 1;  // else the backward rebuilds streams >= 1 (h0_stream)
     bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
       f32x4 h[S];
       h0_jet<WT, S, NSO>(sp, aux, d, x, t, g, h);
-      hs_store(H0 + hs_off(0, t, WT), h[0]);
+      hs_store<WT>(H0, 0, t, h[0]);
       if (save_all) {
 #pragma unroll
-        for (int s = 1; s < S; ++s) hs_store(H0 + hs_off(s, t, WT), h[s]);
+        for (int s = 1; s < S; ++s) hs_store<WT>(H0, s, t, h[s]);
       }
       if (Lh == 1) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&hlast[((s * WT + t) * 64 + l) * 4]) = h[s];
+        out_dot<S>(h, Ko, t, g, v);
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           bf16x4 hi, lo;
-          split4(h[s], hi, lo);
+          split_or_round<LO>(h[s], hi, lo);
           if (t & 1) {
             ah[s][t >> 1] = cat8(ph[s], hi);
-            al[s][t >> 1] = cat8(pl[s], lo);
+            if constexpr (LO) al[s][t >> 1] = cat8(pl[s], lo);
           } else {
             ph[s] = hi;
-            pl[s] = lo;
+            if constexpr (LO) pl[s] = lo;
           }
         }
       }
@@ -434,35 +503,20 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   TDQ_TS(1);
   // ---- hidden layers on bf16x3 MFMA --------------------------------------------------------
   for (int i = 1; i < Lh - 1; ++i) {
-    fwd_hidden<WT, S, NSO, false>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
-                                  Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+    fwd_hidden<WT, S, NSO, LO, false>(ah, al, tl_make(Wimg + (size_t)(i - 1) * NSTEP * 128, l),
+                                      aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT>(Hs, i, nwg, wg, S, w, l), stage,
+                                      Ko, v, sp, l, g);
     TDQ_TS(1 + i);
   }
   if (Lh >= 2) {
     const int i = Lh - 1;
-    fwd_hidden<WT, S, NSO, true>(ah, al, Wimg + (size_t)(i - 1) * NSTEP * 128 + l, aux + aux_bh(d, W) + (i - 1) * W,
-                                 Hs + hs_base(i, nwg, wg, S, w, WT, l), stage, hlast, sp, l, g);
+    fwd_hidden<WT, S, NSO, LO, true>(ah, al, tl_make(Wimg + (size_t)(i - 1) * NSTEP * 128, l),
+                                     aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT>(Hs, i, nwg, wg, S, w, l), stage,
+                                     Ko, v, sp, l, g);
     TDQ_TS(1 + i);
   }
 
-  // ---- output layer (width -> d_out): VALU dot over the staged fp32 h + cross-lane sum ----
-  float v[S][TDQ_MAXO];
-#pragma unroll
-  for (int s = 0; s < S; ++s)
-#pragma unroll
-    for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = 0.f;
-#pragma unroll
-  for (int t = 0; t < WT; ++t)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const f32x4 kq = *reinterpret_cast<const f32x4*>(Ko + (16 * t + 4 * g + c) * 4);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const float hv = hlast[((s * WT + t) * 64 + l) * 4 + c];
-#pragma unroll
-        for (int q = 0; q < TDQ_MAXO; ++q) v[s][q] = fmaf(hv, kq[q], v[s][q]);
-      }
-    }
+  // ---- output layer (width -> d_out): cross-lane sum of the epilogue partial dots ---------
   const f32x4 bo = *reinterpret_cast<const f32x4*>(aux + aux_bo(d, W));
 #pragma unroll
   for (int q = 0; q < TDQ_MAXO; ++q) {
@@ -481,9 +535,9 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 // backward
 // ------------------------------------------------------------------------------------------
 template <int S, int WT>
-__device__ __forceinline__ void h_tile(f32x4 (&h)[S], const float* __restrict__ Hl, int t) {
+__device__ __forceinline__ void h_tile(f32x4 (&h)[S], const Tl& Hl, int t) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) h[s] = hs_load(Hl + hs_off(s, t, WT));
+  for (int s = 0; s < S; ++s) h[s] = hs_load<WT>(Hl, s, t);
 }
 
 // first-layer partials from zb_0 (fp32) of one feature tile: bias b0 and dK0[j][f] (one LDS slot
@@ -515,10 +569,10 @@ __device__ __forceinline__ void first_layer_partials(const JetSpec& sp, const f3
 
 // zb of one feature tile -> bias partial of its layer + hi/lo halves into the wave's fragment
 // stage ([s][kb][hl][lane][2 halves] bf16x4, the forward's staging layout)
-template <int WT, int S>
+template <int WT, int S, bool LO>
 __device__ __forceinline__ void zb_to_stage(const f32x4 (&zb)[S], const NetDims& d, int t, int w, int l, int p,
                                             int g, float* accBslot, bf16x4* stage) {
-  constexpr int KB = WT / 2, W = 16 * WT;
+  constexpr int KB = WT / 2, W = 16 * WT, HL = LO ? 2 : 1;
   {
     const float r = row16_sum4(zb[0]);
     if ((p & 3) == 0) accBslot[w * W + 16 * t + 4 * g + (p >> 2)] = r;
@@ -526,34 +580,31 @@ __device__ __forceinline__ void zb_to_stage(const f32x4 (&zb)[S], const NetDims&
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     bf16x4 hi, lo;
-    split4(zb[s], hi, lo);
-    stage[(((s * KB + (t >> 1)) * 2 + 0) * 64 + l) * 2 + (t & 1)] = hi;
-    stage[(((s * KB + (t >> 1)) * 2 + 1) * 64 + l) * 2 + (t & 1)] = lo;
+    split_or_round<LO>(zb[s], hi, lo);
+    stage[(((s * KB + (t >> 1)) * HL + 0) * 64 + l) * 2 + (t & 1)] = hi;
+    if constexpr (LO) stage[(((s * KB + (t >> 1)) * HL + 1) * 64 + l) * 2 + (t & 1)] = lo;
   }
 }
 
 // (d) of hidden layer i: hb_{i-1} = K_i zb_i on bf16x3 MFMA; the epilogue of output tile o-1
 // (tanh-jet adjoint with the saved h_{i-1}, bias partials, split + stage - or, when i = 1, the
 // first-layer partials) runs in the scheduling region of tile o's MFMAs.
-template <int WT, int S, int NSO, bool TO_FIRST>
+template <int WT, int S, int NSO, bool LO, bool TO_FIRST>
 __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], const bf16x8 (&zl)[S][WT / 2],
-                                             const bf16x8* __restrict__ Ki, const float* __restrict__ Hp,
+                                             const Tl& Ki, const Tl& Hp,
                                              bf16x4* stage, float* accBslot, float* accK0,
                                              const float* __restrict__ xrow, const JetSpec& sp, const NetDims& d,
                                              const float* __restrict__ aux, bool h0r, int w, int l, int p, int g) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
   bf16x8 wh[D], wl[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    wh[k] = Ki[k * 128];
-    wl[k] = Ki[k * 128 + 64];
-  }
+  for (int k = 0; k < D; ++k) img_frag(Ki, k, wh[k], wl[k]);
   // TO_FIRST && h0r: only layer 0's value stream is saved; the others are rebuilt (h0_stream)
   const bool rec = TO_FIRST && h0r;
   f32x4 hr[2][S];
   if (rec) {
-    hr[0][0] = hs_load(Hp + hs_off(0, 0, WT));
-    if (WT > 1) hr[1][0] = hs_load(Hp + hs_off(0, 1, WT));
+    hr[0][0] = hs_load<WT>(Hp, 0, 0);
+    if (WT > 1) hr[1][0] = hs_load<WT>(Hp, 0, 1);
   } else {
     h_tile<S, WT>(hr[0], Hp, 0);
     if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
@@ -572,12 +623,9 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
       for (int kb = 0; kb < KB; ++kb) {
         const int st = o * KB + kb;
         const bf16x8 Ah = wh[st % D], Al = wl[st % D];
-        if (st + D < NSTEP) {
-          wh[st % D] = Ki[(st + D) * 128];
-          wl[st % D] = Ki[(st + D) * 128 + 64];
-        }
+        if (st + D < NSTEP) img_frag(Ki, st + D, wh[st % D], wl[st % D]);
 #pragma unroll
-        for (int s = 0; s < S; ++s) accC[s] = mfma3(Ah, Al, zh[s][kb], zl[s][kb], accC[s]);
+        for (int s = 0; s < S; ++s) accC[s] = mfma_w<LO>(Ah, Al, zh[s][kb], zl[s][kb], accC[s]);
       }
     }
     if (o > 0) {
@@ -585,7 +633,7 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
       f32x4 h[S], zb[S];
       if (rec) {
         h[0] = hr[t & 1][0];
-        if (t + 2 < WT) hr[t & 1][0] = hs_load(Hp + hs_off(0, t + 2, WT));
+        if (t + 2 < WT) hr[t & 1][0] = hs_load<WT>(Hp, 0, t + 2);
 #pragma unroll
         for (int s = 1; s < S; ++s) h[s] = h0_stream<WT, S, NSO>(sp, aux, h[0], t, g, s);
       } else {
@@ -597,14 +645,14 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
       if (TO_FIRST)
         first_layer_partials<WT, S, NSO>(sp, zb, xrow, d, t, w, p, g, accBslot, accK0);
       else
-        zb_to_stage<WT, S>(zb, d, t, w, l, p, g, accBslot, stage);
+        zb_to_stage<WT, S, LO>(zb, d, t, w, l, p, g, accBslot, stage);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-template <int WT, int S, int NSO>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <int WT, int S, int NSO, bool LO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LO ? 1 : 2, LO ? 1 : 2)))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
                    int Ptot, NetDims d, JetSpec sp, int rev, int h0r) {
@@ -631,14 +679,20 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // per wave would need 2 + 8 fragment loads for the same 16 tiles at WT = 8)
   constexpr int NR = WT / 2;
   constexpr int NC = WT / 2;
-  constexpr int U1 = (4 * IMG) / 2;           // images, in floats
-  constexpr int U2 = 4 * S * WT * 256;        // per-wave zb fragment stage (bf16 hi/lo)
+  // images: h hi, (h lo,) zb hi, (zb lo) - the lo images only under LO
+  constexpr int HL = LO ? 2 : 1;
+  constexpr int IH = 0, IHL = IMG, IZ = HL * IMG, IZL = 3 * IMG;
+  constexpr int U1 = (2 * HL * IMG) / 2;      // images, in floats
+  constexpr int U2 = 2 * S * WT * 256 * HL;   // per-wave zb fragment stage (bf16 hi(/lo))
   constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
+  static_assert(4 * W * TDQ_MAXO + 4 * TDQ_MAXO + 4 * TDQ_MAXD * W <= U, "partials must fit the union");
   __bf16* img = reinterpret_cast<__bf16*>(lds);
-  float* accK0 = lds + U;                     // [4][TDQ_MAXD * W]
-  float* accB = accK0 + 4 * TDQ_MAXD * W;     // [3: layer parity 0/1, layer 0][4][W]
-  float* accKo = accB + 12 * W;               // [4][W * TDQ_MAXO]
+  float* accB = lds + U;                      // [3: layer parity 0/1, layer 0][4][W]
+  // output- and first-layer partials alias the image / stage union: they live while neither does
+  // (Ko is reduced right after the output phase, K0 after the last image read)
+  float* accKo = lds;                         // [4][W * TDQ_MAXO]
   float* accBo = accKo + 4 * W * TDQ_MAXO;    // [4][TDQ_MAXO]
+  float* accK0 = accBo + 4 * TDQ_MAXO;        // [4][TDQ_MAXD * W]
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -651,7 +705,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const float vmask = valid ? 1.f : 0.f;  // zero adjoints for padding points: zb = 0 downstream
   const int Lh = d.n_hidden;
   float* gs = slab + (size_t)wg * Ptot;
-  bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * 2 * 64 * 2);
+  bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * HL * 64 * 2);
   auto dw_row = [](int wv, int r) { return (WT / 2) * (wv >> 1) + r; };
   auto dw_col = [](int wv, int c) { return (WT / 2) * (wv & 1) + c; };
   // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
@@ -670,7 +724,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   //      adjoint zb_{Lh-1} tile by tile (bias partials + B fragments, or first-layer partials)
   {
     const float* Ko = aux + aux_ko(d, W);
-    const float* Hl = Hs + hs_base(Lh - 1, nwg, wg, S, w, WT, l);
+    const Tl Hl = hs_region<WT>(Hs, Lh - 1, nwg, wg, S, w, l);
     float* accBslot = Lh >= 2 ? accB + ((Lh - 1) & 1) * 4 * W : accB + 8 * W;
     float ub[S][TDQ_MAXO];
 #pragma unroll
@@ -726,13 +780,13 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           bf16x4 hi, lo;
-          split4(zb[s], hi, lo);
+          split_or_round<LO>(zb[s], hi, lo);
           if (t & 1) {
             zh[s][t >> 1] = cat8(ph[s], hi);
-            zl[s][t >> 1] = cat8(pl[s], lo);
+            if constexpr (LO) zl[s][t >> 1] = cat8(pl[s], lo);
           } else {
             ph[s] = hi;
-            pl[s] = lo;
+            if constexpr (LO) pl[s] = lo;
           }
         }
       } else {
@@ -746,18 +800,31 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       if (l == 0) accBo[w * TDQ_MAXO + q] = v;
     }
   }
+  // output-layer slab now: its partials alias the images (the first dK pass starts with a barrier)
+  __syncthreads();
+  if (w == 2) {
+    const int ko = off_layer(d, Lh);
+    for (int e = l; e < d.width * d.d_out; e += 64) {
+      const int f = e / d.d_out, q = e - f * d.d_out;
+      const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
+      gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
+    }
+    if (l < d.d_out)
+      gs[ko + d.width * d.d_out + l] =
+          ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
+  }
   TDQ_TS(1);
 
   // ---- hidden layers i = Lh-1 .. 1: zh/zl hold zb_i --------------------------------------
   for (int i = Lh - 1; i >= 1; --i) {
     const int tsb = 2 + 8 * (Lh - 1 - i);
-    const float* Hp = Hs + hs_base(i - 1, nwg, wg, S, w, WT, l);
+    const Tl Hp = hs_region<WT>(Hs, i - 1, nwg, wg, S, w, l);
     // layer 0 under h0r: hp keeps the value stream, stream s is rebuilt from it (h0_stream)
     const bool rec0 = h0r && i == 1;
     // h_{i-1} tiles of stream 0 for the dK images
     f32x4 hp[WT];
 #pragma unroll
-    for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(0, t, WT));
+    for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT>(Hp, 0, t);
     TDQ_TS(tsb);
 
     // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index
@@ -782,73 +849,99 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
         for (int t = 0; t < WT; ++t) {
           bf16x4 hi, lo;
-          split4(rec0 ? h0_stream<WT, S, NSO>(sp, aux, hp[t], t, g, s) : hp[t], hi, lo);
+          split_or_round<LO>(rec0 ? h0_stream<WT, S, NSO>(sp, aux, hp[t], t, g, s) : hp[t], hi, lo);
           const int off = row * RS + ((16 * t + 4 * wch) ^ rsw);
-          *reinterpret_cast<bf16x4*>(img + off) = hi;
-          *reinterpret_cast<bf16x4*>(img + IMG + off) = lo;
-          *reinterpret_cast<bf16x4*>(img + 2 * IMG + off) = half8(zh[s][t >> 1], t & 1);
-          *reinterpret_cast<bf16x4*>(img + 3 * IMG + off) = half8(zl[s][t >> 1], t & 1);
+          *reinterpret_cast<bf16x4*>(img + IH + off) = hi;
+          *reinterpret_cast<bf16x4*>(img + IZ + off) = half8(zh[s][t >> 1], t & 1);
+          if constexpr (LO) {
+            *reinterpret_cast<bf16x4*>(img + IHL + off) = lo;
+            *reinterpret_cast<bf16x4*>(img + IZL + off) = half8(zl[s][t >> 1], t & 1);
+          }
         }
       }
       if (s + 1 < S && !rec0) {  // next stream's h_{i-1} tiles fly while this stream's MFMAs run
 #pragma unroll
-        for (int t = 0; t < WT; ++t) hp[t] = hs_load_c(Hp + hs_off(s + 1, t, WT));
+        for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT>(Hp, s + 1, t);
       }
       __syncthreads();
       if (s == 0) TDQ_TS(tsb + 1);
+      // transposed-read bases of this wave's first row / column tile: the other tiles (+16 r / c
+      // columns) and the second k-block (+32 rows) are immediate offsets of these four addresses
+      // (adding 16 r never crosses the swizzled bit 6: the bases' low six bits + 16 (NR - 1) < 64)
+      const int ra1 = tr_row * RS + ((16 * dw_row(w, 0) + tr_col1) ^ swz);
+      const int ra2 = (tr_row + 4) * RS + ((16 * dw_row(w, 0) + tr_col2) ^ swz);
+      const int ca1 = tr_row * RS + ((16 * dw_col(w, 0) + tr_col1) ^ swz);
+      const int ca2 = (tr_row + 4) * RS + ((16 * dw_col(w, 0) + tr_col2) ^ swz);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {  // 64 points = 2 k-blocks of 32
         bf16x8 Ah[NR], Al[NR];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-          const int off = (32 * kb + tr_row) * RS + ((16 * dw_row(w, r) + tr_col1) ^ swz);
-          const int of2 = (32 * kb + tr_row + 4) * RS + ((16 * dw_row(w, r) + tr_col2) ^ swz);
-          Ah[r] = cat8(tr_read(img + off), tr_read(img + of2));
-          Al[r] = cat8(tr_read(img + IMG + off), tr_read(img + IMG + of2));
+          const int off = ra1 + 32 * kb * RS + 16 * r;
+          const int of2 = ra2 + 32 * kb * RS + 16 * r;
+          Ah[r] = cat8(tr_read(img + IH + off), tr_read(img + IH + of2));
+          if constexpr (LO) Al[r] = cat8(tr_read(img + IHL + off), tr_read(img + IHL + of2));
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          const int off = (32 * kb + tr_row) * RS + ((16 * dw_col(w, c) + tr_col1) ^ swz);
-          const int of2 = (32 * kb + tr_row + 4) * RS + ((16 * dw_col(w, c) + tr_col2) ^ swz);
-          const bf16x8 Bh = cat8(tr_read(img + 2 * IMG + off), tr_read(img + 2 * IMG + of2));
-          const bf16x8 Bl = cat8(tr_read(img + 3 * IMG + off), tr_read(img + 3 * IMG + of2));
+          const int off = ca1 + 32 * kb * RS + 16 * c;
+          const int of2 = ca2 + 32 * kb * RS + 16 * c;
+          const bf16x8 Bh = cat8(tr_read(img + IZ + off), tr_read(img + IZ + of2));
+          bf16x8 Bl;
+          if constexpr (LO) Bl = cat8(tr_read(img + IZL + off), tr_read(img + IZL + of2));
 #pragma unroll
-          for (int r = 0; r < NR; ++r) dw[r][c] = mfma3(Ah[r], Al[r], Bh, Bl, dw[r][c]);
+          for (int r = 0; r < NR; ++r) dw[r][c] = mfma_aa<LO>(Ah[r], Al[r], Bh, Bl, dw[r][c]);
         }
       }
     }
     {
-      const int ko = off_layer(d, i);
+      // dK_i rows / columns this wave owns.  Unpadded width: one lane offset + uniform (r, c2, c)
+      // offsets through a buffer resource (no per-store address VGPRs, no exec branches);
+      // padded width: guarded stores.
+      const int in0 = 16 * dw_row(w, 0) + 4 * g, out0 = 16 * dw_col(w, 0) + p;
+      float* gk = gs + off_layer(d, i);
+      if (d.width == W) {
+        const Tl G = tl_make(gk, 0);
+        const int voff = (in0 * W + out0) * 4;
 #pragma unroll
-      for (int r = 0; r < NR; ++r)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c2 = 0; c2 < NC; ++c2) {
-          const int out = 16 * dw_col(w, c2) + p;
+          for (int c2 = 0; c2 < NC; ++c2)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int in = 16 * dw_row(w, r) + 4 * g + c;
-            if (in < d.width && out < d.width) slab_store(gs + ko + in * d.width + out, dw[r][c2][c]);
-          }
-        }
+            for (int c = 0; c < 4; ++c) {
+              const float v = dw[r][c2][c];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), G.r, voff, ((16 * r + c) * W + 16 * c2) * 4, 0);
+            }
+      } else {
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int c2 = 0; c2 < NC; ++c2)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const int in = in0 + 16 * r + c, out = out0 + 16 * c2;
+              if (in < d.width && out < d.width) slab_store(gk + in * d.width + out, dw[r][c2][c]);
+            }
+      }
     }
     TDQ_TS(tsb + 2);
     __syncthreads();  // images consumed: the region becomes the zb fragment stage
     TDQ_TS(tsb + 3);
 
     // (d) hb_{i-1} = K_i zb_i, fused with the adjoint of tanh layer i-1
-    const bf16x8* Ki = Kimg + (size_t)(i - 1) * (WT * KB) * 128 + l;
+    const Tl Ki = tl_make(Kimg + (size_t)(i - 1) * (WT * KB) * 128, l);
     if (i >= 2) {
-      bwd_hidden_d<WT, S, NSO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, aux,
+      bwd_hidden_d<WT, S, NSO, LO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, aux,
                                       h0r != 0, w, l, p, g);
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {  // wave-private stage: program order suffices
-          zh[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 0) * 64 + l) * 2]);
-          zl[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * 2 + 1) * 64 + l) * 2]);
+          zh[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * HL + 0) * 64 + l) * 2]);
+          if constexpr (LO) zl[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * HL + 1) * 64 + l) * 2]);
         }
     } else {
-      bwd_hidden_d<WT, S, NSO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, aux, h0r != 0, w, l,
+      bwd_hidden_d<WT, S, NSO, LO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, aux, h0r != 0, w, l,
                                      p, g);
     }
     TDQ_TS(tsb + 4);
@@ -867,16 +960,6 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       const int k = j * W + f;
       gs[e] = ((accK0[k] + accK0[TDQ_MAXD * W + k]) + accK0[2 * TDQ_MAXD * W + k]) + accK0[3 * TDQ_MAXD * W + k];
     }
-  } else if (w == 2) {
-    const int ko = off_layer(d, Lh);
-    for (int e = l; e < d.width * d.d_out; e += 64) {
-      const int f = e / d.d_out, q = e - f * d.d_out;
-      const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
-      gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
-    }
-    if (l < d.d_out)
-      gs[ko + d.width * d.d_out + l] =
-          ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
   }
   TDQ_TS(63);
 }
@@ -884,7 +967,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 // ------------------------------------------------------------------------------------------
 // host-side launch templates (instantiated per width class in jet_bf3_w{2,4,8}.hip)
 // ------------------------------------------------------------------------------------------
-inline size_t fwd_bf3_lds(int WT, int S) { return (size_t)4 * S * WT * 1024; }
+inline size_t fwd_bf3_lds(int WT, int S, bool lo) { return (size_t)2 * S * WT * 1024 * (lo ? 2 : 1); }
 
 // backward tile order: reverse (default) or dispatch order (TDQ_BWD_ORDER=forward, for A/B runs)
 inline int bwd_reverse_order() {
@@ -905,11 +988,11 @@ inline int h0_recompute() {
   return on;
 }
 
-inline size_t bwd_bf3_lds(int WT, int S) {
-  const int W = 16 * WT;
-  const size_t u1 = (size_t)(4 * 64 * 144) / 2, u2 = (size_t)4 * S * WT * 256;
+inline size_t bwd_bf3_lds(int WT, int S, bool lo) {
+  const int W = 16 * WT, hl = lo ? 2 : 1;
+  const size_t u1 = (size_t)(2 * hl * 64 * 144) / 2, u2 = (size_t)2 * S * WT * 256 * hl;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
-  return (u + 4 * TDQ_MAXD * W + 12 * W + 4 * W * TDQ_MAXO + 4 * TDQ_MAXO) * sizeof(float);
+  return (u + 12 * W) * sizeof(float);
 }
 
 struct Bf3Args {
@@ -924,38 +1007,49 @@ struct Bf3Args {
   NetDims d;
   JetSpec sp;
   hipStream_t st;
+  int lo;            // 1: bf16x3 (activations hi + lo), 0: bf16 activations
 };
 
-template <int WT, int S, int NSO>
-int launch_fwd_bf3(const Bf3Args& a) {
+template <int WT, int S, int NSO, bool LO>
+int launch_fwd_bf3_lo(const Bf3Args& a) {
   const int nwg = (a.N + 63) / 64;
-  const size_t lds = fwd_bf3_lds(WT, S);
+  const size_t lds = fwd_bf3_lds(WT, S, LO);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_fwd_bf3_kernel<WT, S, NSO>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_fwd_bf3_kernel<WT, S, NSO, LO>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
+  hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
                      a.Hs, a.N, a.d, a.sp, h0_recompute());
   TDQ_CHECK_LAUNCH();
   return 0;
 }
 
 template <int WT, int S, int NSO>
-int launch_bwd_bf3(const Bf3Args& a) {
+int launch_fwd_bf3(const Bf3Args& a) {
+  return a.lo ? launch_fwd_bf3_lo<WT, S, NSO, true>(a) : launch_fwd_bf3_lo<WT, S, NSO, false>(a);
+}
+
+template <int WT, int S, int NSO, bool LO>
+int launch_bwd_bf3_lo(const Bf3Args& a) {
   const int nwg = (a.N + 63) / 64;
-  const size_t lds = bwd_bf3_lds(WT, S);
+  const size_t lds = bwd_bf3_lds(WT, S, LO);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_bwd_bf3_kernel<WT, S, NSO>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_bwd_bf3_kernel<WT, S, NSO, LO>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
+  hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
                      a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute());
   TDQ_CHECK_LAUNCH();
   return 0;
+}
+
+template <int WT, int S, int NSO>
+int launch_bwd_bf3(const Bf3Args& a) {
+  return a.lo ? launch_bwd_bf3_lo<WT, S, NSO, true>(a) : launch_bwd_bf3_lo<WT, S, NSO, false>(a);
 }
 
 // per-width-class entry points (jet_bf3_w{2,4,8}.hip); return hipErrorInvalidValue when

@@ -121,8 +121,9 @@ int64_t tdq_jet_bf3_slab_floats(int N, int d_in, int width, int d_out, int n_hid
   return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
 
+// lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16)
 int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
-                    int d_out, int n_hidden, int S, const int* spec, void* stream) {
+                    int d_out, int n_hidden, int S, const int* spec, int lo, void* stream) {
   if (N <= 0) return 0;
   const int WT = width_tiles(width);
   JetSpec sp;
@@ -137,12 +138,13 @@ int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, in
   float* aux = bimg + img_floats(WT, n_hidden);
   int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
   if (rc) return rc;
-  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st};
+  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo};
   return dispatch(true, WT, S, nso, a);
 }
 
 int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
-                    int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, void* stream) {
+                    int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo,
+                    void* stream) {
   if (N <= 0) return 0;
   const int WT = width_tiles(width);
   JetSpec sp;
@@ -160,7 +162,7 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
   (void)P;
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), dJ, nullptr, const_cast<float*>(Hs), slab, N,
-            slab_stride(Ptot), d, sp, st};
+            slab_stride(Ptot), d, sp, st, lo};
   int rc = dispatch(false, WT, S, nso, a);
   if (rc) return rc;
   return tdq_slab_reduce(work, grad, nwg, Ptot, chunks, stream);

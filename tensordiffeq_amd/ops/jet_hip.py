@@ -30,7 +30,7 @@ def stream_spec(plan):
 
 
 def _fns(lib, cfg):
-    if cfg["precision"] == "bf16x3":
+    if cfg["precision"] in ("bf16x3", "bf16"):
         return (lib.tdq_jet_fwd_bf3, lib.tdq_jet_bwd_bf3,
                 lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["d_in"], cfg["width"], cfg["n_hidden"], cfg["S"]),
                 lambda N: lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
@@ -39,10 +39,19 @@ def _fns(lib, cfg):
             lambda N: lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
 
 
+def _lo_args(cfg):
+    """Trailing kernel flag of the split-bf16 family: 1 = bf16x3, 0 = bf16 activations."""
+    if cfg["precision"] == "bf16x3":
+        return (1,)
+    if cfg["precision"] == "bf16":
+        return (0,)
+    return ()
+
+
 def forward_raw(X, P, net, plan, precision=None):
     """Autograd-free forward: returns ``(J, saved)`` where ``saved`` feeds :func:`backward_raw`.
 
-    ``precision``: ``"bf16x3"`` (csrc/jet_bf3.hip, saves post-activations) or ``"fp32"``
+    ``precision``: ``"bf16x3"`` / ``"bf16"`` (csrc/jet_bf3.hip, saves post-activations) or ``"fp32"``
     (csrc/jet_mlp.hip, saves pre-activations); the saved buffer only fits its own backward."""
     lib = _lib.load()
     cfg = hip_config(net, plan, precision)
@@ -58,7 +67,7 @@ def forward_raw(X, P, net, plan, precision=None):
         raise ValueError(f"jet kernels cannot serve {cfg}")
     scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
     rc = fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
-                         cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, _lib.stream_ptr(X.device))
+                         cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
     _lib.check(rc, f"tdq_jet_fwd[{cfg['precision']}]")
     return J, (X, P, scratch, cfg, spec, S)
 
@@ -76,7 +85,7 @@ def backward_raw(saved, dJ):
     spec_c = (ctypes.c_int * len(spec))(*spec)
     rc = bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
                          _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S,
-                         spec_c, _lib.stream_ptr(X.device))
+                         spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
     _lib.check(rc, f"tdq_jet_bwd[{cfg['precision']}]")
     return grad
 

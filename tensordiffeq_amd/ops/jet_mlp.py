@@ -29,13 +29,15 @@ from . import _lib
 
 MAX_S = 8
 PTS_PER_WG = 64
-PRECISIONS = ("bf16x3", "fp32")
+PRECISIONS = ("bf16x3", "bf16", "fp32")
 _precision = os.environ.get("TDQ_PRECISION", "bf16x3")
 
 
 def set_precision(p):
     """Default GEMM precision of the HIP jet kernels: ``"bf16x3"`` (split-bf16 MFMA, ~2^-16 relative
-    error per product, default) or ``"fp32"`` (exact-fp32 MFMA)."""
+    error per product, default), ``"bf16"`` (weights split hi + lo, activations rounded to bf16:
+    ~2^-9 relative error per activation, two MFMAs per product, two workgroups per CU) or
+    ``"fp32"`` (exact-fp32 MFMA)."""
     global _precision
     if p not in PRECISIONS:
         raise ValueError(f"precision must be one of {PRECISIONS}")
@@ -54,7 +56,7 @@ def hip_config(net, plan, precision=None):
     """Return the kernel geometry or raise ValueError if the kernels cannot serve it.
 
     ``precision`` (default: :func:`get_precision`) picks the kernel family; bf16x3 needs at least
-    two 16-feature tiles (width > 16) and falls back to fp32 below that."""
+    two 16-feature tiles (width > 16) and falls back to fp32 below that (so does bf16)."""
     sizes = net.layer_sizes
     d_in, d_out = sizes[0], sizes[-1]
     hidden = sizes[1:-1]
@@ -83,7 +85,7 @@ def hip_config(net, plan, precision=None):
     precision = precision or _precision
     if precision not in PRECISIONS:
         raise ValueError(f"precision {precision!r} not in {PRECISIONS}")
-    if precision == "bf16x3" and WT < 2:
+    if precision in ("bf16x3", "bf16") and WT < 2:
         precision = "fp32"
     return {"d_in": d_in, "d_out": d_out, "width": hidden[0], "WT": WT, "S": S,
             "n_hidden": len(hidden), "precision": precision}

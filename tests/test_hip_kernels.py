@@ -15,10 +15,11 @@ from tensordiffeq_amd.models.networks import TanhMLP
 pytestmark = pytest.mark.gpu
 
 # max error relative to each stream's scale (forward) / relative gradient norm (backward).
-# bf16x3: every GEMM product carries ~2^-16 relative error (split-bf16 MFMA, csrc/jet_bf3.hip).
-TOL_FWD = {"fp32": 2e-5, "bf16x3": 2e-4}
-TOL_BWD = {"fp32": 5e-5, "bf16x3": 5e-4}
-PRECS = ["fp32", "bf16x3"]
+# bf16x3: every GEMM product carries ~2^-16 relative error (split-bf16 MFMA, csrc/jet_bf3.hip);
+# bf16: activations rounded to bf16 (2^-9 relative) against split weights.
+TOL_FWD = {"fp32": 2e-5, "bf16x3": 2e-4, "bf16": 8e-2}
+TOL_BWD = {"fp32": 5e-5, "bf16x3": 5e-4, "bf16": 1e-2}
+PRECS = ["fp32", "bf16x3", "bf16"]
 
 CASES = [
     # layer_sizes, requests, N
@@ -229,7 +230,7 @@ def test_solver_hip_matches_jet_backend(prec):
     assert a.active_backend == "hip" and b.active_backend == "jet"
     la, ga = a.grad()
     lb, gb = b.grad()
-    tl = 1.0 if prec == "fp32" else 10.0
+    tl = {"fp32": 1.0, "bf16x3": 10.0, "bf16": 300.0}[prec]
     assert abs(la.item() - lb.item()) / abs(lb.item()) < 1e-5 * tl
     for x, y in zip(ga, gb):
         assert ((x - y).norm() / y.norm().clamp_min(1e-12)).item() < 1e-4 * tl
