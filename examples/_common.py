@@ -27,6 +27,7 @@ def parser(desc, iters=10000, newton=0, n_f=None):
     ap.add_argument("--device", default=None, help="cuda / cpu (default: cuda if available)")
     ap.add_argument("--backend", default="auto", help="auto | hip | jet | autograd")
     ap.add_argument("--precision", default=None, help="bf16x3 | bf16 | fp32 (HIP jet GEMMs)")
+    ap.add_argument("--newton-precision", default=None, help="jet precision of the L-BFGS phase (default: --precision)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--plot", action="store_true", help="draw the reference-style figures")
     ap.add_argument("--quiet", action="store_true")
@@ -34,7 +35,10 @@ def parser(desc, iters=10000, newton=0, n_f=None):
 
 
 def solver_kw(args):
-    return {"backend": args.backend, "device": args.device, "precision": args.precision}
+    kw = {"backend": args.backend, "device": args.device, "precision": args.precision}
+    if getattr(args, "newton_precision", None):
+        kw["newton_precision"] = args.newton_precision
+    return kw
 
 
 def ac_data():

@@ -8,6 +8,7 @@ field                  env var                     meaning
 backend                TDQ_BACKEND                 auto | hip | jet | autograd
 precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 activations,
                                                    split weights) | fp32 (fp32 MFMA)
+newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision)
 seed                   TDQ_SEED                    global seed applied at compile
 periodic_legacy        TDQ_PERIODIC_LEGACY         1: reference periodic-BC quirk (B12)
 log_every              TDQ_LOG_EVERY               progress / metrics cadence (steps)
@@ -38,6 +39,7 @@ def _env_bool(name, default):
 class SolverConfig:
     backend: str = "auto"
     precision: str = "bf16x3"
+    newton_precision: str | None = None
     seed: int | None = None
     periodic_legacy: bool = False
     log_every: int = 100
@@ -54,6 +56,7 @@ class SolverConfig:
         vals = {
             "backend": e.get("TDQ_BACKEND", cls.backend),
             "precision": e.get("TDQ_PRECISION", cls.precision),
+            "newton_precision": e.get("TDQ_NEWTON_PRECISION") or None,
             "seed": int(e["TDQ_SEED"]) if "TDQ_SEED" in e else None,
             "periodic_legacy": _env_bool("TDQ_PERIODIC_LEGACY", False),
             "log_every": int(e.get("TDQ_LOG_EVERY", cls.log_every)),
@@ -73,6 +76,8 @@ class SolverConfig:
             raise ValueError(f"backend {self.backend!r}")
         if self.precision not in ("bf16x3", "bf16", "fp32"):
             raise ValueError(f"precision {self.precision!r}")
+        if self.newton_precision not in (None, "bf16x3", "bf16", "fp32"):
+            raise ValueError(f"newton_precision {self.newton_precision!r}")
         if self.log_every < 1:
             raise ValueError("log_every must be >= 1")
         if self.lbfgs not in ("auto", "device", "host"):

@@ -83,12 +83,17 @@ class CollocationSolverND:
     def compile(self, layer_sizes, f_model, domain, bcs, Adaptive_type=0, dict_adaptive=None,
                 init_weights=None, g=None, dist=False, backend="auto", device=None,
                 periodic_legacy=False, seed=None, network=None, precision=None, metrics_path=None,
-                log_every=None):
+                log_every=None, newton_precision=None):
         from ..config import SolverConfig
         self.config = SolverConfig.from_env(backend=None if backend == "auto" else backend, precision=precision,
-                                            seed=seed, metrics_path=metrics_path, log_every=log_every)
+                                            seed=seed, metrics_path=metrics_path, log_every=log_every,
+                                            newton_precision=newton_precision)
         backend = self.config.backend
         precision = self.config.precision
+        # jet-GEMM precision of the L-BFGS phase (None: same as the Adam phase).  L-BFGS's
+        # curvature pairs need the accurate gradient; Adam tolerates bf16 activations
+        # (profiles/r2_v2_accuracy_mixed.jsonl)
+        self.newton_precision = self.config.newton_precision
         seed = self.config.seed
         periodic_legacy = periodic_legacy or self.config.periodic_legacy
         self.log_every = self.config.log_every
@@ -207,12 +212,12 @@ class CollocationSolverND:
         out = self.f_model(net, *cols)
         return len(out) if isinstance(out, (tuple, list)) else 1
 
-    def _build_program(self, batch=None):
+    def _build_program(self, batch=None, precision=None):
         ctx = self.dist_ctx
         world = ctx.world if ctx.is_distributed else 1
         rep_scale = 1.0 / world
         prog = LossProgram(self.u_model, len(self.domain.vars), self.device, backend=self.backend,
-                           precision=self.precision,
+                           precision=precision or self.precision,
                            world=world, weight_outside_sum=self.weight_outside_sum, g=self.g,
                            periodic_legacy=self.periodic_legacy)
         for i, bc in enumerate(self.bcs):
@@ -276,7 +281,7 @@ class CollocationSolverND:
         prog.finalize()
         return prog
 
-    def program(self, batch=None):
+    def program(self, batch=None, precision=None):
         self._flat()  # wraps a user-assigned custom network
         if self._state is not None:
             self._train_state(self.device)  # re-validates the best snapshot against the network
@@ -284,9 +289,11 @@ class CollocationSolverND:
             self._programs = {"net": self.u_model}
             self._engine = None
             self._lbfgs_engine = None
-        key = ("batch", batch)
+        if precision == self.precision:
+            precision = None
+        key = ("batch", batch) if precision is None else ("batch", batch, precision)
         if key not in self._programs:
-            prog = self._build_program(batch)
+            prog = self._build_program(batch, precision)
             prog.enable_fusion(self.lambdas)
             self._programs[key] = prog
         return self._programs[key]
@@ -352,7 +359,7 @@ class CollocationSolverND:
 
     def _get_lbfgs_engine(self):
         if self._lbfgs_engine is None:
-            self._lbfgs_engine = LossGradEngine(self, self.program(), self.lambdas)
+            self._lbfgs_engine = LossGradEngine(self, self.program(precision=self.newton_precision), self.lambdas)
         return self._lbfgs_engine
 
     def _get_engine(self, batch=None, n_hint=0):

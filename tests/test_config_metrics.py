@@ -22,6 +22,34 @@ def test_config_env_and_overrides(monkeypatch):
         SolverConfig.from_env(backend="cuda")
 
 
+def test_newton_precision_builds_separate_program(monkeypatch):
+    """Per-phase jet precision: the L-BFGS engine gets its own program (and kernel family)."""
+    from tensordiffeq_amd.boundaries import DomainND, dirichletBC
+    monkeypatch.setenv("TDQ_NEWTON_PRECISION", "bf16x3")
+    assert SolverConfig.from_env().newton_precision == "bf16x3"
+    with pytest.raises(ValueError):
+        SolverConfig.from_env(newton_precision="fp16")
+    monkeypatch.delenv("TDQ_NEWTON_PRECISION")
+    tdq.set_seed(0)
+    D = DomainND(["x", "t"], time_var="t")
+    D.add("x", [-1.0, 1.0], 32)
+    D.add("t", [0.0, 1.0], 16)
+    D.generate_collocation_points(128)
+
+    def f_model(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        return tdq.grad(u, t) - 0.01 * tdq.grad(tdq.grad(u, x), x)
+
+    m = tdq.CollocationSolverND(verbose=False)
+    m.compile([2, 16, 16, 1], f_model, D, [dirichletBC(D, 0.0, "x", "upper")], device="cpu",
+              precision="bf16", newton_precision="bf16x3")
+    assert m.program().precision == "bf16"
+    assert m._get_lbfgs_engine().program.precision == "bf16x3"
+    assert m.program(precision="bf16") is m.program()   # same-precision request -> same program
+    m.fit(tf_iter=3, newton_iter=3)
+    assert math.isfinite(m.losses[-1]["Total Loss"])
+
+
 def test_metrics_jsonl(tmp_path):
     from tensordiffeq_amd.boundaries import DomainND, dirichletBC
     tdq.set_seed(0)

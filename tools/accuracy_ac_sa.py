@@ -2,7 +2,8 @@
 
 Runs examples/AC-SA.py (Adam ``--iters`` + L-BFGS ``--newton``) for each requested precision and
 prints one JSON line per run: relative L2 on the AC.mat grid, final/min losses, wall time per
-phase.  Usage (GPU):  python tools/accuracy_ac_sa.py --iters 10000 --newton 10000 --prec bf16x3 fp32
+phase.  Usage (GPU):  python tools/accuracy_ac_sa.py --iters 10000 --newton 10000 --prec bf16x3 fp32 bf16+bf16x3
+(``a+b``: Adam phase in precision a, L-BFGS phase in b).
 """
 import argparse
 import json
@@ -24,9 +25,11 @@ def main():
     spec = importlib.util.spec_from_file_location("ac_sa", os.path.join(os.path.dirname(HERE), "examples", "AC-SA.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    for p in args.prec:
-        res = mod.main(["--iters", str(args.iters), "--newton", str(args.newton), "--precision", p,
-                        "--seed", str(args.seed), "--quiet"])
+    for p in args.prec:  # "adam+lbfgs" (e.g. bf16+bf16x3) picks a per-phase precision
+        pa, _, pn = p.partition("+")
+        extra = ["--newton-precision", pn] if pn else []
+        res = mod.main(["--iters", str(args.iters), "--newton", str(args.newton), "--precision", pa,
+                        "--seed", str(args.seed), "--quiet"] + extra)
         res["precision"] = p
         res["schedule"] = f"adam {args.iters} + lbfgs {args.newton}"
         print(json.dumps(res), flush=True)

@@ -72,22 +72,23 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="multiply iteration counts (smoke runs)")
     a = ap.parse_args()
     k = lambda n: str(max(1, int(n * a.scale)))
+    prec, _, newton_prec = a.precision.partition("+")  # "adam+lbfgs", e.g. bf16+bf16x3
+    pk = ["--precision", prec] + (["--newton-precision", newton_prec] if newton_prec else [])
     for w in a.which:
         if w == "burgers":
-            r, dt = timed(_example("burgers-new").main, ["--iters", k(10000), "--newton", k(10000), "--quiet",
-                                                         "--precision", a.precision])
+            r, dt = timed(_example("burgers-new").main, ["--iters", k(10000), "--newton", k(10000), "--quiet"] + pk)
             r.update(config="burgers [2,20x8,1] N_f 10k, adam 10k + lbfgs 10k", wall_s=dt)
         elif w == "helmholtz":
-            r, dt = timed(_example("steady-state").main, ["--iters", k(10000), "--newton", k(10000), "--quiet",
-                                                          "--precision", a.precision])
+            r, dt = timed(_example("steady-state").main, ["--iters", k(10000), "--newton", k(10000), "--quiet"] + pk)
             r.update(config="helmholtz-2d [2,50x4,1] N_f 10k, adam 10k + lbfgs 10k", wall_s=dt)
         elif w == "discovery":
-            r, dt = timed(_example("AC-discovery").main, ["--iters", k(10000), "--quiet", "--precision", a.precision])
+            r, dt = timed(_example("AC-discovery").main, ["--iters", k(10000), "--quiet", "--precision", prec])
             r.update(config="AC discovery [2,128x4,1] 102,912 data pts, adam 10k (SA col weights)", wall_s=dt)
         elif w == "poisson10m":
-            r = poisson_throughput(int(10_000_000 * min(1.0, a.scale)), int(k(50)), 3, a.precision)
+            r = poisson_throughput(int(10_000_000 * min(1.0, a.scale)), int(k(50)), 3, prec)
         else:
             raise SystemExit(f"unknown config {w}")
+        r["precision_arg"] = a.precision
         print(json.dumps(r), flush=True)
 
 
