@@ -274,26 +274,68 @@ __device__ __forceinline__ Tl tl_make(const void* uniform_base, int lane) {
 #else
 #define TDQ_POL_LD 2  // nt
 #endif
+// Precision "bf16" (!LO) saves the derivative streams (s >= 1) as bf16: the next layer's GEMM already
+// consumed them rounded to bf16, so the dK images are unchanged, and the tanh-jet adjoint sees the
+// same 2^-9 relative rounding the forward applied; the value stream stays fp32 (s1 = 1 - h^2 near
+// saturation needs it).  Per wave and layer: [t] fp32 value tiles, then [s-1][t] bf16 tiles with an
+// 8-byte lane stride.  -DTDQ_BF16_HS_FP32 keeps every stream fp32 (A/B).
+#ifdef TDQ_BF16_HS_FP32
+#define TDQ_HS_HALF(LO) false
+#else
+#define TDQ_HS_HALF(LO) (!(LO))
+#endif
+template <int WT, bool LO>
+__host__ __device__ constexpr int hs_wave_floats(int S) {
+  return TDQ_HS_HALF(LO) ? WT * (256 + (S - 1) * 128) : S * WT * 256;
+}
 // wave w's region of saved layer `layer` (uniform base; the lane offset lives in Tl::v)
-template <int WT>
+template <int WT, bool LO>
 __device__ __forceinline__ Tl hs_region(const float* Hs, int layer, int nwg, int wg, int S, int w, int lane) {
-  return tl_make(Hs + hs_base(layer, nwg, wg, S, w, WT, 0), lane);
+  if constexpr (TDQ_HS_HALF(LO))
+    return tl_make(Hs + (((size_t)layer * nwg + wg) * 4 + w) * hs_wave_floats<WT, LO>(S), lane);
+  else
+    return tl_make(Hs + hs_base(layer, nwg, wg, S, w, WT, 0), lane);
 }
-template <int WT>
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+template <int WT, bool LO>
 __device__ __forceinline__ void hs_store(const Tl& T, int s, int t, const f32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_ST);
+  if constexpr (TDQ_HS_HALF(LO)) {
+    if (s > 0) {
+      const bf16x4 b = __builtin_convertvector(v, bf16x4);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, b), T.r, T.v >> 1,
+                                            (WT * 256 + ((s - 1) * WT + t) * 128) * 4, TDQ_POL_ST);
+      return;
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, t * 256 * 4, TDQ_POL_ST);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_ST);
+  }
 }
-template <int WT>
+template <int WT, bool LO, int POL>
+__device__ __forceinline__ f32x4 hs_load_p(const Tl& T, int s, int t) {
+  if constexpr (TDQ_HS_HALF(LO)) {
+    if (s > 0) {
+      const u32x2v u = __builtin_amdgcn_raw_buffer_load_b64(T.r, T.v >> 1, (WT * 256 + ((s - 1) * WT + t) * 128) * 4, POL);
+      // bf16 -> fp32: the bf16 bits are the high half of the fp32 word
+      return f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+                   __uint_as_float(u[1] & 0xffff0000u)};
+    }
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, t * 256 * 4, POL));
+  } else {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_off(s, t, WT) * 4, POL));
+  }
+}
+template <int WT, bool LO>
 __device__ __forceinline__ f32x4 hs_load(const Tl& T, int s, int t) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_LD));
+  return hs_load_p<WT, LO, TDQ_POL_LD>(T, s, t);
 }
 // the dK pass's read of h_{i-1} (the same lines are read again by the tanh-adjoint pass): cached
-template <int WT>
+template <int WT, bool LO>
 __device__ __forceinline__ f32x4 hs_load_c(const Tl& T, int s, int t) {
 #ifdef TDQ_NT_C_LOADS
-  return hs_load<WT>(T, s, t);
+  return hs_load<WT, LO>(T, s, t);
 #else
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_off(s, t, WT) * 4, 0));
+  return hs_load_p<WT, LO, 0>(T, s, t);
 #endif
 }
 // hi / lo A fragment of step `st` of a layer's weight image (lo 64 lanes = 1 KiB later)
@@ -410,7 +452,7 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       z[0] += biasP;
       tanh_jet_f<S, NSO>(sp, z, h);
 #pragma unroll
-      for (int s = 0; s < S; ++s) hs_store<WT>(Hl, s, t, h[s]);
+      for (int s = 0; s < S; ++s) hs_store<WT, LO>(Hl, s, t, h[s]);
       if (LAST) {
         out_dot<S>(h, Ko, t, g, vout);
       } else {
@@ -469,17 +511,17 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 
   // ---- layer 0 (input -> width) on VALU ---------------------------------------------------
   {
-    const Tl H0 = hs_region<WT>(Hs, 0, nwg, wg, S, w, l);
+    const Tl H0 = hs_region<WT, LO>(Hs, 0, nwg, wg, S, w, l);
     const bool save_all = !h0r || Lh == 1;  // else the backward rebuilds streams >= 1 (h0_stream)
     bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
       f32x4 h[S];
       h0_jet<WT, S, NSO>(sp, aux, d, x, t, g, h);
-      hs_store<WT>(H0, 0, t, h[0]);
+      hs_store<WT, LO>(H0, 0, t, h[0]);
       if (save_all) {
 #pragma unroll
-        for (int s = 1; s < S; ++s) hs_store<WT>(H0, s, t, h[s]);
+        for (int s = 1; s < S; ++s) hs_store<WT, LO>(H0, s, t, h[s]);
       }
       if (Lh == 1) {
         out_dot<S>(h, Ko, t, g, v);
@@ -504,14 +546,14 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // ---- hidden layers on bf16x3 MFMA --------------------------------------------------------
   for (int i = 1; i < Lh - 1; ++i) {
     fwd_hidden<WT, S, NSO, LO, false>(ah, al, tl_make(Wimg + (size_t)(i - 1) * NSTEP * 128, l),
-                                      aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT>(Hs, i, nwg, wg, S, w, l), stage,
+                                      aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT, LO>(Hs, i, nwg, wg, S, w, l), stage,
                                       Ko, v, sp, l, g);
     TDQ_TS(1 + i);
   }
   if (Lh >= 2) {
     const int i = Lh - 1;
     fwd_hidden<WT, S, NSO, LO, true>(ah, al, tl_make(Wimg + (size_t)(i - 1) * NSTEP * 128, l),
-                                     aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT>(Hs, i, nwg, wg, S, w, l), stage,
+                                     aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT, LO>(Hs, i, nwg, wg, S, w, l), stage,
                                      Ko, v, sp, l, g);
     TDQ_TS(1 + i);
   }
@@ -534,10 +576,10 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 // ------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------
-template <int S, int WT>
+template <int S, int WT, bool LO>
 __device__ __forceinline__ void h_tile(f32x4 (&h)[S], const Tl& Hl, int t) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) h[s] = hs_load<WT>(Hl, s, t);
+  for (int s = 0; s < S; ++s) h[s] = hs_load<WT, LO>(Hl, s, t);
 }
 
 // first-layer partials from zb_0 (fp32) of one feature tile: bias b0 and dK0[j][f] (one LDS slot
@@ -603,11 +645,11 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
   const bool rec = TO_FIRST && h0r;
   f32x4 hr[2][S];
   if (rec) {
-    hr[0][0] = hs_load<WT>(Hp, 0, 0);
-    if (WT > 1) hr[1][0] = hs_load<WT>(Hp, 0, 1);
+    hr[0][0] = hs_load<WT, LO>(Hp, 0, 0);
+    if (WT > 1) hr[1][0] = hs_load<WT, LO>(Hp, 0, 1);
   } else {
-    h_tile<S, WT>(hr[0], Hp, 0);
-    if (WT > 1) h_tile<S, WT>(hr[1], Hp, 1);
+    h_tile<S, WT, LO>(hr[0], Hp, 0);
+    if (WT > 1) h_tile<S, WT, LO>(hr[1], Hp, 1);
   }
   f32x4 accA[S], accB[S];
 #pragma unroll
@@ -633,13 +675,13 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
       f32x4 h[S], zb[S];
       if (rec) {
         h[0] = hr[t & 1][0];
-        if (t + 2 < WT) hr[t & 1][0] = hs_load<WT>(Hp, 0, t + 2);
+        if (t + 2 < WT) hr[t & 1][0] = hs_load<WT, LO>(Hp, 0, t + 2);
 #pragma unroll
         for (int s = 1; s < S; ++s) h[s] = h0_stream<WT, S, NSO>(sp, aux, h[0], t, g, s);
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) h[s] = hr[t & 1][s];
-        if (t + 2 < WT) h_tile<S, WT>(hr[t & 1], Hp, t + 2);
+        if (t + 2 < WT) h_tile<S, WT, LO>(hr[t & 1], Hp, t + 2);
       }
       tanh_jet_b<S, NSO>(sp, h, accP, zb);
       if (TO_FIRST)
@@ -652,7 +694,11 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
 }
 
 template <int WT, int S, int NSO, bool LO>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LO ? 1 : 2, LO ? 1 : 2)))
+#ifndef TDQ_BWD_BF16_WPE
+#define TDQ_BWD_BF16_WPE 2  // waves per SIMD of the bf16 backward (A/B: 1 = no spills, one workgroup per CU)
+#endif
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(LO ? 1 : TDQ_BWD_BF16_WPE, LO ? 1 : TDQ_BWD_BF16_WPE)))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
                    int Ptot, NetDims d, JetSpec sp, int rev, int h0r) {
@@ -724,7 +770,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   //      adjoint zb_{Lh-1} tile by tile (bias partials + B fragments, or first-layer partials)
   {
     const float* Ko = aux + aux_ko(d, W);
-    const Tl Hl = hs_region<WT>(Hs, Lh - 1, nwg, wg, S, w, l);
+    const Tl Hl = hs_region<WT, LO>(Hs, Lh - 1, nwg, wg, S, w, l);
     float* accBslot = Lh >= 2 ? accB + ((Lh - 1) & 1) * 4 * W : accB + 8 * W;
     float ub[S][TDQ_MAXO];
 #pragma unroll
@@ -734,14 +780,14 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     constexpr int DH = WT < 3 ? WT : 3;  // H tiles in flight
     f32x4 hr[DH][S];
 #pragma unroll
-    for (int k = 0; k < DH; ++k) h_tile<S, WT>(hr[k], Hl, k);
+    for (int k = 0; k < DH; ++k) h_tile<S, WT, LO>(hr[k], Hl, k);
     bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
       f32x4 h[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) h[s] = hr[t % DH][s];
-      if (t + DH < WT) h_tile<S, WT>(hr[t % DH], Hl, t + DH);
+      if (t + DH < WT) h_tile<S, WT, LO>(hr[t % DH], Hl, t + DH);
       // hb = Ko ub over the zero-padded 4 output columns: no branches
       f32x4 hbt[S];
 #pragma unroll
@@ -818,13 +864,13 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // ---- hidden layers i = Lh-1 .. 1: zh/zl hold zb_i --------------------------------------
   for (int i = Lh - 1; i >= 1; --i) {
     const int tsb = 2 + 8 * (Lh - 1 - i);
-    const Tl Hp = hs_region<WT>(Hs, i - 1, nwg, wg, S, w, l);
+    const Tl Hp = hs_region<WT, LO>(Hs, i - 1, nwg, wg, S, w, l);
     // layer 0 under h0r: hp keeps the value stream, stream s is rebuilt from it (h0_stream)
     const bool rec0 = h0r && i == 1;
     // h_{i-1} tiles of stream 0 for the dK images
     f32x4 hp[WT];
 #pragma unroll
-    for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT>(Hp, 0, t);
+    for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT, LO>(Hp, 0, t);
     TDQ_TS(tsb);
 
     // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index
@@ -861,7 +907,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       }
       if (s + 1 < S && !rec0) {  // next stream's h_{i-1} tiles fly while this stream's MFMAs run
 #pragma unroll
-        for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT>(Hp, s + 1, t);
+        for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT, LO>(Hp, s + 1, t);
       }
       __syncthreads();
       if (s == 0) TDQ_TS(tsb + 1);
