@@ -9,6 +9,12 @@ residual SA weights init U[0,1]; Keras Adam lr 0.005, beta1 0.99 on theta, gradi
 the SA weights.  One step = full-batch loss + gradients (HIP jet kernels) + DP all-reduce +
 fused Adam/SA update - the complete reference training step, nothing skipped.
 
+Precision (BASELINE.json names AC-SA "bf16"): the jet GEMMs take bf16 activations against split
+(hi + lo) bf16 weights with fp32 accumulation; tanh jets, loss, reductions and the optimizer are
+fp32.  Under the reference schedule (Adam 10k in this precision + L-BFGS 10k in bf16x3) the L2 on
+AC.mat matches all-bf16x3 training over three seeds (profiles/r2_v2_accuracy_mixed.jsonl).
+``--precision bf16x3`` measures the split-activation kernels.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--npts 50000] [--backend auto]
 
 Multi-GPU: launched by ``torch.distributed.run`` (one rank per GPU, RCCL); the timed region is
@@ -101,7 +107,7 @@ def main(argv=None):
     ap.add_argument("--npts", type=int, default=50000, help="collocation points per GPU")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--no-l2", action="store_true")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp32"],
+    ap.add_argument("--precision", default="bf16", choices=["bf16x3", "bf16", "fp32"],
                     help="GEMM precision of the HIP jet kernels (bf16x3 = split-bf16 MFMA, fp32 accumulate; "
                          "bf16 = bf16 activations x split-bf16 weights)")
     args = ap.parse_args(argv)
@@ -165,7 +171,8 @@ def main(argv=None):
                        "global_batch": n_glob, "seq_len": None, "parallelism": f"dp{world}",
                        "points_per_gpu": args.npts, "backend": backend,
                        "precision": PRECISION_NOTES[args.precision] if backend == "hip" else "fp32",
-                       "bc_points": "IC 512 (SA) + periodic 2x201 (u, u_x)"},
+                       "bc_points": "IC 512 (SA) + periodic 2x201 (u, u_x)",
+                       "accuracy_evidence": "profiles/r2_v2_accuracy_mixed.jsonl"},
             "loss_after": loss,
             "l2_rel_error_after_steps": l2,
             "total_adam_steps": int(model._state["epoch_host"]),

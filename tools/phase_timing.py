@@ -1,4 +1,4 @@
-"""Per-phase timing of the bf16x3 jet kernels (WT = 8 instantiations) from in-kernel s_memtime stamps.
+"""Per-phase timing of the split-bf16 (bf16x3 / bf16: --prec) jet kernels (WT = 8 instantiations) from in-kernel s_memtime stamps.
 
 Builds ``csrc/build_timing/libtdq_hip_timing.so`` with ``-DTDQ_PHASE_TIMING`` (separate from the
 production library), runs forward + backward of the Allen-Cahn plan on ``--npts`` points and prints,
@@ -39,6 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--npts", type=int, default=50000)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--prec", default="bf16x3", choices=["bf16x3", "bf16"])
     args = ap.parse_args()
     libpath = args.lib or build()
     from tensordiffeq_amd.ops import _lib
@@ -66,15 +67,16 @@ def main():
     dJ = torch.randn(S, N, 1, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     P = net.flat.detach()
+    lo = 1 if args.prec == "bf16x3" else 0
     for kind in ("fwd", "bwd"):
         for rep in range(3):
             ts.zero_()
             if kind == "fwd":
                 rc = lib.tdq_jet_fwd_bf3(X.data_ptr(), P.data_ptr(), J.data_ptr(), scr.data_ptr(), N, 2, 128, 1, 4, S,
-                                         spec_c, st)
+                                         spec_c, lo, st)
             else:
                 rc = lib.tdq_jet_bwd_bf3(X.data_ptr(), P.data_ptr(), dJ.data_ptr(), scr.data_ptr(), work.data_ptr(),
-                                         grad.data_ptr(), N, 2, 128, 1, 4, S, spec_c, st)
+                                         grad.data_ptr(), N, 2, 128, 1, 4, S, spec_c, lo, st)
             assert rc == 0, rc
             torch.cuda.synchronize()
         T = ts.view(nwg * 4, 64).cpu().numpy().astype(np.int64)
