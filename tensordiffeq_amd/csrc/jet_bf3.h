@@ -944,7 +944,10 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       // dK_i rows / columns this wave owns.  Unpadded width: one lane offset + uniform (r, c2, c)
       // offsets through a buffer resource (no per-store address VGPRs, no exec branches);
       // padded width: guarded stores.
-      const int in0 = 16 * dw_row(w, 0) + 4 * g, out0 = 16 * dw_col(w, 0) + p;
+      int in0 = 16 * dw_row(w, 0) + 4 * g, out0 = 16 * dw_col(w, 0) + p;
+      // opaque per iteration: otherwise LICM hoists the padded path's 64 guarded store addresses
+      // (and their exec masks) out of the layer loop, where they stay live and spill
+      asm volatile("" : "+v"(in0), "+v"(out0));
       float* gk = gs + off_layer(d, i);
       if (d.width == W) {
         const Tl G = tl_make(gk, 0);
