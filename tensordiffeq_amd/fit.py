@@ -20,6 +20,7 @@ import time
 
 import torch
 
+from .graphs import capture_graph
 from .optimizers import adam as adam_mod
 from .ops import fused
 
@@ -241,12 +242,12 @@ class AdamEngine:
         pool = torch.cuda.graph_pool_handle()
         if not split:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with capture_graph(g, pool=pool):
                 self.static_loss = self._eager_step()
             self.graph_a, self.graph_b = g, None
         else:
             ga = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga, pool=pool):
+            with capture_graph(ga, pool=pool):
                 loss, grads, terms = self._phase_a(for_step=True)
                 red_idx = self.red_idx
                 red = [grads[i] for i in red_idx]
@@ -256,7 +257,7 @@ class AdamEngine:
                 self._grads_static = grads
                 self._red_idx = red_idx
             gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=pool):
+            with capture_graph(gb, pool=pool):
                 red_out, scal = self._bucket.unpack(self._bucket_buf)
                 grads = list(self._grads_static)
                 for i, gg in zip(self._red_idx, red_out):
@@ -346,7 +347,7 @@ class LossGradEngine:
                 self._body()
             torch.cuda.current_stream(self.flat.device).wait_stream(stream)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with capture_graph(g):
                 self._static = self._body()
             self.graph = g
         if self.graph is not None:

@@ -24,6 +24,7 @@ import math
 
 import torch
 
+from ..graphs import capture_graph
 from ..ops import _lib
 
 # scalar-state layout (mirrors the LB_* enum of csrc/lbfgs.hip)
@@ -309,7 +310,7 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
     if opt.active():
         pool = torch.cuda.graph_pool_handle()
         ga = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(ga, pool=pool):
+        with capture_graph(ga, pool=pool):
             opt.axpy()
             fg_static = evaluate()
             if not split:
@@ -317,7 +318,7 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
         gb = None
         if split:
             gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=pool):
+            with capture_graph(gb, pool=pool):
                 opt.update(fg_static)
         launched = 1
         while opt.active() and launched <= 2 * max_iter + 8:  # the maxIter test always fires first
