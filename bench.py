@@ -9,9 +9,9 @@ residual SA weights init U[0,1]; Keras Adam lr 0.005, beta1 0.99 on theta, gradi
 the SA weights.  One step = full-batch loss + gradients (HIP jet kernels) + DP all-reduce +
 fused Adam/SA update - the complete reference training step, nothing skipped.
 
-Precision (BASELINE.json names AC-SA "bf16"): the jet GEMMs take bf16 activations against split
-(hi + lo) bf16 weights with fp32 accumulation; tanh jets, loss, reductions and the optimizer are
-fp32.  Under the reference schedule (Adam 10k in this precision + L-BFGS 10k in bf16x3) the L2 on
+Precision (BASELINE.json names AC-SA "bf16"): the jet GEMMs run bf16 x bf16 MFMAs with fp32
+accumulation (fp32 master weights rounded once per step); tanh jets, loss, reductions and the
+optimizer are fp32.  Under the reference schedule (Adam 10k in this precision + L-BFGS 10k in bf16x3) the L2 on
 AC.mat matches all-bf16x3 training over three seeds (profiles/r2_v2_accuracy_mixed.jsonl).
 ``--precision bf16x3`` measures the split-activation kernels.
 
@@ -40,8 +40,8 @@ sys.path.insert(0, HERE)
 METRIC = "collocation-pts/sec + L2 rel-error, Allen-Cahn SA-PINN @ 1/2/4/8 GPU"
 PRECISION_NOTES = {
     "bf16x3": "bf16x3: split-bf16 MFMA (hi*hi+hi*lo+lo*hi), fp32 accumulate, fp32 elementwise/loss/optimizer",
-    "bf16": "bf16: bf16 activations x split-bf16 weights (hi*hi+lo*hi), fp32 accumulate, "
-            "fp32 elementwise/loss/optimizer",
+    "bf16": "bf16: bf16 x bf16 MFMA (weights and activations rounded), fp32 accumulate, "
+            "fp32 master weights/elementwise/loss/optimizer",
     "fp32": "fp32 MFMA",
 }
 
@@ -109,7 +109,7 @@ def main(argv=None):
     ap.add_argument("--no-l2", action="store_true")
     ap.add_argument("--precision", default="bf16", choices=["bf16x3", "bf16", "fp32"],
                     help="GEMM precision of the HIP jet kernels (bf16x3 = split-bf16 MFMA, fp32 accumulate; "
-                         "bf16 = bf16 activations x split-bf16 weights)")
+                         "bf16 = bf16 x bf16 MFMA, fp32 accumulate)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

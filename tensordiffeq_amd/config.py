@@ -6,8 +6,8 @@ environment overrides so that a run can be re-tuned without code changes.
 field                  env var                     meaning
 =====================  ==========================  =========================================
 backend                TDQ_BACKEND                 auto | hip | jet | autograd
-precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 activations,
-                                                   split weights) | fp32 (fp32 MFMA)
+precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 MFMA operands,
+                                                   fp32 accumulate / jets / master weights) | fp32
 newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision)
 seed                   TDQ_SEED                    global seed applied at compile
 periodic_legacy        TDQ_PERIODIC_LEGACY         1: reference periodic-BC quirk (B12)

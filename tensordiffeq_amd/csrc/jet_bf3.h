@@ -79,14 +79,17 @@ __device__ __forceinline__ f32x4 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 b
   return mfma_bf(ah, bh, c);
 }
 
-// activation-operand products.  LO (precision "bf16x3"): activations split hi + lo like the weights,
-// 3 MFMAs per product.  !LO (precision "bf16"): activations rounded to bf16 once (8-bit mantissa),
-// weights still hi + lo: 2 MFMAs, half the activation fragments / staging / images, which is what
-// lets two workgroups share a CU.
+// weight x activation products.  LO (precision "bf16x3"): both operands split hi + lo, 3 MFMAs
+// per product.  !LO (precision "bf16"): weights and activations rounded to bf16 once, 1 MFMA: the
+// kernels then run a consistently bf16-rounded network (fp32 master weights, fp32 accumulation and
+// tanh jets), with half the activation fragments / staging / images - which is what lets two
+// workgroups share a CU.
 template <bool LO>
 __device__ __forceinline__ f32x4 mfma_w(bf16x8 ah, bf16x8 al, const bf16x8& bh, const bf16x8& bl, f32x4 c) {
-  c = mfma_bf(al, bh, c);
-  if constexpr (LO) c = mfma_bf(ah, bl, c);
+  if constexpr (LO) {
+    c = mfma_bf(al, bh, c);
+    c = mfma_bf(ah, bl, c);
+  }
   return mfma_bf(ah, bh, c);
 }
 // dK products: both operands are activations (saved h, adjoint zb)
@@ -338,10 +341,12 @@ __device__ __forceinline__ f32x4 hs_load_c(const Tl& T, int s, int t) {
   return hs_load_p<WT, LO, 0>(T, s, t);
 #endif
 }
-// hi / lo A fragment of step `st` of a layer's weight image (lo 64 lanes = 1 KiB later)
+// hi / lo A fragment of step `st` of a layer's weight image (lo 64 lanes = 1 KiB later; hi only
+// under !LO)
+template <bool LO>
 __device__ __forceinline__ void img_frag(const Tl& I, int st, bf16x8& hi, bf16x8& lo) {
   hi = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(I.r, I.v, st * 2048, 0));
-  lo = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(I.r, I.v, st * 2048 + 1024, 0));
+  if constexpr (LO) lo = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(I.r, I.v, st * 2048 + 1024, 0));
 }
 
 __device__ __forceinline__ void slab_store(float* p, float v) {
@@ -421,7 +426,7 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
   constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4, HL = LO ? 2 : 1;
   bf16x8 wh[D], wl[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) img_frag(Wi, k, wh[k], wl[k]);
+  for (int k = 0; k < D; ++k) img_frag<LO>(Wi, k, wh[k], wl[k]);
   f32x4 accA[S], accB[S], biasA = zero4(), biasB = zero4();
 #pragma unroll
   for (int s = 0; s < S; ++s) accA[s] = accB[s] = zero4();
@@ -439,7 +444,7 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       for (int kb = 0; kb < KB; ++kb) {
         const int st = o * KB + kb;
         const bf16x8 Ah = wh[st % D], Al = wl[st % D];
-        if (st + D < NSTEP) img_frag(Wi, st + D, wh[st % D], wl[st % D]);
+        if (st + D < NSTEP) img_frag<LO>(Wi, st + D, wh[st % D], wl[st % D]);
 #pragma unroll
         for (int s = 0; s < S; ++s) accC[s] = mfma_w<LO>(Ah, Al, ah[s][kb], al[s][kb], accC[s]);
       }
@@ -640,7 +645,7 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
   constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4;
   bf16x8 wh[D], wl[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) img_frag(Ki, k, wh[k], wl[k]);
+  for (int k = 0; k < D; ++k) img_frag<LO>(Ki, k, wh[k], wl[k]);
   // TO_FIRST && h0r: only layer 0's value stream is saved; the others are rebuilt (h0_stream)
   const bool rec = TO_FIRST && h0r;
   f32x4 hr[2][S];
@@ -665,7 +670,7 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
       for (int kb = 0; kb < KB; ++kb) {
         const int st = o * KB + kb;
         const bf16x8 Ah = wh[st % D], Al = wl[st % D];
-        if (st + D < NSTEP) img_frag(Ki, st + D, wh[st % D], wl[st % D]);
+        if (st + D < NSTEP) img_frag<LO>(Ki, st + D, wh[st % D], wl[st % D]);
 #pragma unroll
         for (int s = 0; s < S; ++s) accC[s] = mfma_w<LO>(Ah, Al, zh[s][kb], zl[s][kb], accC[s]);
       }
@@ -1056,7 +1061,7 @@ struct Bf3Args {
   NetDims d;
   JetSpec sp;
   hipStream_t st;
-  int lo;            // 1: bf16x3 (activations hi + lo), 0: bf16 activations
+  int lo;            // 1: bf16x3 (operands hi + lo), 0: bf16 (operands rounded to bf16)
 };
 
 template <int WT, int S, int NSO, bool LO>

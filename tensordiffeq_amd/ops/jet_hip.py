@@ -40,7 +40,7 @@ def _fns(lib, cfg):
 
 
 def _lo_args(cfg):
-    """Trailing kernel flag of the split-bf16 family: 1 = bf16x3, 0 = bf16 activations."""
+    """Trailing kernel flag of the split-bf16 family: 1 = bf16x3, 0 = bf16."""
     if cfg["precision"] == "bf16x3":
         return (1,)
     if cfg["precision"] == "bf16":

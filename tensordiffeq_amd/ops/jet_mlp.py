@@ -35,8 +35,8 @@ _precision = os.environ.get("TDQ_PRECISION", "bf16x3")
 
 def set_precision(p):
     """Default GEMM precision of the HIP jet kernels: ``"bf16x3"`` (split-bf16 MFMA, ~2^-16 relative
-    error per product, default), ``"bf16"`` (weights split hi + lo, activations rounded to bf16:
-    ~2^-9 relative error per activation, two MFMAs per product, two workgroups per CU) or
+    error per product, default), ``"bf16"`` (weights and activations rounded to bf16, one MFMA
+    per product, fp32 accumulation; two workgroups per CU) or
     ``"fp32"`` (exact-fp32 MFMA)."""
     global _precision
     if p not in PRECISIONS:
