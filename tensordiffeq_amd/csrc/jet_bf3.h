@@ -52,7 +52,7 @@ static __device__ unsigned long long* tdq_ts;  // per translation unit (no -fgpu
 #define TDQ_TS(k)                                                                                 \
   do {                                                                                            \
     if ((threadIdx.x & 63) == 0)                                                                  \
-      tdq_ts[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (k)] = __builtin_amdgcn_s_memtime(); \
+      tdq_ts[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define TDQ_TS(k) \
@@ -698,12 +698,19 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
   }
 }
 
-template <int WT, int S, int NSO, bool LO>
-#ifndef TDQ_BWD_BF16_WPE
-#define TDQ_BWD_BF16_WPE 2  // waves per SIMD of the bf16 backward (A/B: 1 = no spills, one workgroup per CU)
+// Waves per backward workgroup.  bf16 (!LO) at WT >= 4: 8 waves = 128 points, one workgroup per
+// CU (2 waves per SIMD, like two 4-wave workgroups): half the per-workgroup gradient slab rows
+// (written here, re-read by tdq_slab_reduce) and half the dK accumulators per wave (each wave owns
+// 8 of the 64 16x16 dK tiles instead of 16).  bf16x3 keeps 4 waves: its 32 KiB per-wave fragment
+// stage leaves no LDS for 8.  -DTDQ_BWD_WIDE=0 builds the 4-wave bf16 kernel (A/B).
+#ifndef TDQ_BWD_WIDE
+#define TDQ_BWD_WIDE 1
 #endif
-__global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(LO ? 1 : TDQ_BWD_BF16_WPE, LO ? 1 : TDQ_BWD_BF16_WPE)))
+__host__ __device__ constexpr int bwd_waves(int WT, bool lo) { return (TDQ_BWD_WIDE && !lo && WT >= 4) ? 8 : 4; }
+
+template <int WT, int S, int NSO, bool LO>
+__global__ void __launch_bounds__(64 * bwd_waves(WT, LO))
+__attribute__((amdgpu_waves_per_eu(LO ? 1 : 2, LO ? 1 : 2)))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
                    int Ptot, NetDims d, JetSpec sp, int rev, int h0r) {
@@ -723,42 +730,48 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #else
   constexpr int CHUNK_SWZ = 1;
 #endif
+  constexpr int NWV = bwd_waves(WT, LO), PTS = 16 * NWV;  // waves / points per workgroup
   constexpr int RS = 144;
-  constexpr int IMG = 64 * RS;
-  // dK tile ownership: the WT x WT output tiles split into 2 x 2 quadrants, wave w owns quadrant
-  // (w >> 1, w & 1): (WT/2)^2 tiles from WT/2 A and WT/2 B fragments per k-block (a 2 x 8 strip
-  // per wave would need 2 + 8 fragment loads for the same 16 tiles at WT = 8)
-  constexpr int NR = WT / 2;
+  constexpr int IMG = PTS * RS;
+  // dK tile ownership: the WT x WT output tiles split into (NWV/2) x 2 blocks, wave w owns block
+  // (w >> 1, w & 1): NR x NC tiles from NR A and NC B fragments per k-block (4 waves: quadrants;
+  // a 2 x 8 strip per wave would need 2 + 8 fragment loads for the same 16 tiles at WT = 8)
+  constexpr int NR = WT / (NWV / 2);
   constexpr int NC = WT / 2;
   // images: h hi, (h lo,) zb hi, (zb lo) - the lo images only under LO
   constexpr int HL = LO ? 2 : 1;
   constexpr int IH = 0, IHL = IMG, IZ = HL * IMG, IZL = 3 * IMG;
   constexpr int U1 = (2 * HL * IMG) / 2;      // images, in floats
-  constexpr int U2 = 2 * S * WT * 256 * HL;   // per-wave zb fragment stage (bf16 hi(/lo))
+  constexpr int U2 = NWV * S * WT * HL * 128;  // per-wave zb fragment stages (bf16 hi(/lo))
   constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
-  static_assert(4 * W * TDQ_MAXO + 4 * TDQ_MAXO + 4 * TDQ_MAXD * W <= U, "partials must fit the union");
+  static_assert(NWV * (W * TDQ_MAXO + TDQ_MAXO + TDQ_MAXD * W) <= U, "partials must fit the union");
   __bf16* img = reinterpret_cast<__bf16*>(lds);
-  float* accB = lds + U;                      // [3: layer parity 0/1, layer 0][4][W]
+  float* accB = lds + U;                      // [3: layer parity 0/1, layer 0][NWV][W]
   // output- and first-layer partials alias the image / stage union: they live while neither does
   // (Ko is reduced right after the output phase, K0 after the last image read)
-  float* accKo = lds;                         // [4][W * TDQ_MAXO]
-  float* accBo = accKo + 4 * W * TDQ_MAXO;    // [4][TDQ_MAXO]
-  float* accK0 = accBo + 4 * TDQ_MAXO;        // [4][TDQ_MAXD * W]
+  float* accKo = lds;                         // [NWV][W * TDQ_MAXO]
+  float* accBo = accKo + NWV * W * TDQ_MAXO;  // [NWV][TDQ_MAXO]
+  float* accK0 = accBo + NWV * TDQ_MAXO;      // [NWV][TDQ_MAXD * W]
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // rev: tiles in reverse dispatch order - the forward wrote the highest tiles last, so theirs are
   // the saved activations still resident in the 256 MiB Infinity Cache when the backward starts
   const int nwg = gridDim.x, wg = rev ? nwg - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  const int n = wg * 64 + w * 16 + p;
+  const int n = wg * PTS + w * 16 + p;
+  // saved activations are laid out by the forward's 64-point workgroups: this wave's region is
+  // forward workgroup wg_f, wave w_f (clamped: the padding half of a last 128-point workgroup
+  // reads a real region - finite values, multiplied by zero adjoints)
+  const int nwg_f = (N + 63) / 64;
+  const int wg_f = min(wg * (NWV / 4) + (w >> 2), nwg_f - 1), w_f = w & 3;
   const bool valid = n < N;
   const int nc = valid ? n : N - 1;
   const float vmask = valid ? 1.f : 0.f;  // zero adjoints for padding points: zb = 0 downstream
   const int Lh = d.n_hidden;
   float* gs = slab + (size_t)wg * Ptot;
   bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * HL * 64 * 2);
-  auto dw_row = [](int wv, int r) { return (WT / 2) * (wv >> 1) + r; };
-  auto dw_col = [](int wv, int c) { return (WT / 2) * (wv & 1) + c; };
+  auto dw_row = [](int wv, int r) { return NR * (wv >> 1) + r; };
+  auto dw_col = [](int wv, int c) { return NC * (wv & 1) + c; };
   // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
   const int tr_row = 8 * g + ((l & 15) >> 2), tr_col = 4 * (l & 3);
   const int swz = (g & 1) << 6;  // bit 3 of every row this lane's transposed reads touch
@@ -775,8 +788,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   //      adjoint zb_{Lh-1} tile by tile (bias partials + B fragments, or first-layer partials)
   {
     const float* Ko = aux + aux_ko(d, W);
-    const Tl Hl = hs_region<WT, LO>(Hs, Lh - 1, nwg, wg, S, w, l);
-    float* accBslot = Lh >= 2 ? accB + ((Lh - 1) & 1) * 4 * W : accB + 8 * W;
+    const Tl Hl = hs_region<WT, LO>(Hs, Lh - 1, nwg_f, wg_f, S, w_f, l);
+    float* accBslot = Lh >= 2 ? accB + ((Lh - 1) & 1) * NWV * W : accB + 2 * NWV * W;
     float ub[S][TDQ_MAXO];
 #pragma unroll
     for (int q = 0; q < TDQ_MAXO; ++q)
@@ -858,18 +871,24 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     for (int e = l; e < d.width * d.d_out; e += 64) {
       const int f = e / d.d_out, q = e - f * d.d_out;
       const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
-      gs[ko + e] = ((accKo[k] + accKo[st + k]) + accKo[2 * st + k]) + accKo[3 * st + k];
+      float a = accKo[k];
+#pragma unroll
+      for (int v = 1; v < NWV; ++v) a += accKo[v * st + k];
+      gs[ko + e] = a;
     }
-    if (l < d.d_out)
-      gs[ko + d.width * d.d_out + l] =
-          ((accBo[l] + accBo[TDQ_MAXO + l]) + accBo[2 * TDQ_MAXO + l]) + accBo[3 * TDQ_MAXO + l];
+    if (l < d.d_out) {
+      float a = accBo[l];
+#pragma unroll
+      for (int v = 1; v < NWV; ++v) a += accBo[v * TDQ_MAXO + l];
+      gs[ko + d.width * d.d_out + l] = a;
+    }
   }
   TDQ_TS(1);
 
   // ---- hidden layers i = Lh-1 .. 1: zh/zl hold zb_i --------------------------------------
   for (int i = Lh - 1; i >= 1; --i) {
     const int tsb = 2 + 8 * (Lh - 1 - i);
-    const Tl Hp = hs_region<WT, LO>(Hs, i - 1, nwg, wg, S, w, l);
+    const Tl Hp = hs_region<WT, LO>(Hs, i - 1, nwg_f, wg_f, S, w_f, l);
     // layer 0 under h0r: hp keeps the value stream, stream s is rebuilt from it (h0_stream)
     const bool rec0 = h0r && i == 1;
     // h_{i-1} tiles of stream 0 for the dK images
@@ -888,10 +907,14 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     for (int s = 0; s < S; ++s) {
       __syncthreads();  // previous readers of the region (zb stage / last stream's images) done
       if (s == 0 && w == 0) {  // bias of layer i: partials of all waves landed before this barrier
-        const float* accBi = accB + (i & 1) * 4 * W;
+        const float* accBi = accB + (i & 1) * NWV * W;
         const int bo = off_layer(d, i) + d.width * d.width;
-        for (int f = l; f < d.width; f += 64)
-          gs[bo + f] = ((accBi[f] + accBi[W + f]) + accBi[2 * W + f]) + accBi[3 * W + f];
+        for (int f = l; f < d.width; f += 64) {
+          float a = accBi[f];
+#pragma unroll
+          for (int v = 1; v < NWV; ++v) a += accBi[v * W + f];
+          gs[bo + f] = a;
+        }
       }
       {
         const int row = 16 * w + p;
@@ -924,7 +947,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       const int ca1 = tr_row * RS + ((16 * dw_col(w, 0) + tr_col1) ^ swz);
       const int ca2 = (tr_row + 4) * RS + ((16 * dw_col(w, 0) + tr_col2) ^ swz);
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {  // 64 points = 2 k-blocks of 32
+      for (int kb = 0; kb < PTS / 32; ++kb) {  // k-blocks of 32 points
         bf16x8 Ah[NR], Al[NR];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -985,7 +1008,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     // (d) hb_{i-1} = K_i zb_i, fused with the adjoint of tanh layer i-1
     const Tl Ki = tl_make(Kimg + (size_t)(i - 1) * (WT * KB) * 128, l);
     if (i >= 2) {
-      bwd_hidden_d<WT, S, NSO, LO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * 4 * W, accK0, xrow, sp, d, aux,
+      bwd_hidden_d<WT, S, NSO, LO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * NWV * W, accK0, xrow, sp, d, aux,
                                       h0r != 0, w, l, p, g);
 #pragma unroll
       for (int s = 0; s < S; ++s)
@@ -995,7 +1018,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
           if constexpr (LO) zl[s][kb] = *reinterpret_cast<const bf16x8*>(&stage[(((s * KB + kb) * HL + 1) * 64 + l) * 2]);
         }
     } else {
-      bwd_hidden_d<WT, S, NSO, LO, true>(zh, zl, Ki, Hp, stage, accB + 8 * W, accK0, xrow, sp, d, aux, h0r != 0, w, l,
+      bwd_hidden_d<WT, S, NSO, LO, true>(zh, zl, Ki, Hp, stage, accB + 2 * NWV * W, accK0, xrow, sp, d, aux, h0r != 0, w, l,
                                      p, g);
     }
     TDQ_TS(tsb + 4);
@@ -1004,15 +1027,22 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // ---- first-layer / output-layer slabs (partials of all waves are in LDS) ----------------
   __syncthreads();
   if (w == 0) {
-    const float* accB0 = accB + 8 * W;
+    const float* accB0 = accB + 2 * NWV * W;
     const int bo = d.d_in * d.width;
-    for (int f = l; f < d.width; f += 64)
-      gs[bo + f] = ((accB0[f] + accB0[W + f]) + accB0[2 * W + f]) + accB0[3 * W + f];
+    for (int f = l; f < d.width; f += 64) {
+      float a = accB0[f];
+#pragma unroll
+      for (int v = 1; v < NWV; ++v) a += accB0[v * W + f];
+      gs[bo + f] = a;
+    }
   } else if (w == 1) {
     for (int e = l; e < d.d_in * d.width; e += 64) {
       const int j = e / d.width, f = e - j * d.width;
       const int k = j * W + f;
-      gs[e] = ((accK0[k] + accK0[TDQ_MAXD * W + k]) + accK0[2 * TDQ_MAXD * W + k]) + accK0[3 * TDQ_MAXD * W + k];
+      float a = accK0[k];
+#pragma unroll
+      for (int v = 1; v < NWV; ++v) a += accK0[v * TDQ_MAXD * W + k];
+      gs[e] = a;
     }
   }
   TDQ_TS(63);
@@ -1043,10 +1073,10 @@ inline int h0_recompute() {
 }
 
 inline size_t bwd_bf3_lds(int WT, int S, bool lo) {
-  const int W = 16 * WT, hl = lo ? 2 : 1;
-  const size_t u1 = (size_t)(2 * hl * 64 * 144) / 2, u2 = (size_t)2 * S * WT * 256 * hl;
+  const int W = 16 * WT, hl = lo ? 2 : 1, nwv = bwd_waves(WT, lo);
+  const size_t u1 = (size_t)(2 * hl * 16 * nwv * 144) / 2, u2 = (size_t)nwv * S * WT * hl * 128;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
-  return (u + 12 * W) * sizeof(float);
+  return (u + 3 * nwv * W) * sizeof(float);
 }
 
 struct Bf3Args {
@@ -1087,7 +1117,8 @@ int launch_fwd_bf3(const Bf3Args& a) {
 
 template <int WT, int S, int NSO, bool LO>
 int launch_bwd_bf3_lo(const Bf3Args& a) {
-  const int nwg = (a.N + 63) / 64;
+  constexpr int NWV = bwd_waves(WT, LO);
+  const int nwg = (a.N + 16 * NWV - 1) / (16 * NWV);
   const size_t lds = bwd_bf3_lds(WT, S, LO);
   static bool attr = false;
   if (!attr) {
@@ -1095,7 +1126,7 @@ int launch_bwd_bf3_lo(const Bf3Args& a) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.dJ,
+  hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(64 * NWV), lds, a.st, a.X, a.aux, a.img, a.dJ,
                      a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute());
   TDQ_CHECK_LAUNCH();
   return 0;

@@ -152,9 +152,10 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int nwg = (N + 63) / 64;
+  const int nwg = (N + 63) / 64;                               // forward (saved-activation) geometry
+  const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
-  const int chunks = slab_chunks(nwg);
+  const int chunks = slab_chunks(nwg_b);
   float* slab = work;
   // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
   const float* img = Hs + (int64_t)n_hidden * nwg * S * 4 * WT * 256 + img_floats(WT, n_hidden);
@@ -165,7 +166,7 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
             slab_stride(Ptot), d, sp, st, lo};
   int rc = dispatch(false, WT, S, nso, a);
   if (rc) return rc;
-  return tdq_slab_reduce(work, grad, nwg, Ptot, chunks, stream);
+  return tdq_slab_reduce(work, grad, nwg_b, Ptot, chunks, stream);
 }
 
 }  // extern "C"

@@ -7,6 +7,7 @@ cd $R
 O=gpurun_out/${TDQ_RUN:-r2ab2}
 mkdir -p $O
 VB=$R/tensordiffeq_amd/csrc/build_${VARIANT:?}/libtdq_hip.so
+[ -n "$PREC_ERR" ] && { timeout -k 10 300 python -u tools/precision_errors.py > $O/prec_err.txt 2>&1 || { tail -20 $O/prec_err.txt; exit 1; }; grep "bf16 " $O/prec_err.txt; }
 timeout -k 10 600 python -u -m pytest tests/test_hip_kernels.py -x -q --timeout 120 --timeout-method thread > $O/pytest_k.log 2>&1 || { tail -30 $O/pytest_k.log; exit 1; }
 tail -1 $O/pytest_k.log
 for p in ${PRECS:-bf16 bf16x3}; do
