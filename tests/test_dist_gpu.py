@@ -26,18 +26,18 @@ def _free_port():
     return port
 
 
-def _build(dist, world=1):
+def _build(dist, world=1, precision=None):
     import bench
-    return bench.build_problem(N_F // world, world, "hip", torch.device("cuda", 0), dist)
+    return bench.build_problem(N_F // world, world, "hip", torch.device("cuda", 0), dist, precision)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, precision):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from tensordiffeq_amd.parallel import dist as pdist
     pdist.reset_context()
     ctx = pdist.init_distributed(backend="gloo", device="cuda:0")
-    m = _build(True, world)
+    m = _build(True, world, precision)
     assert m.active_backend == "hip"
     eng = m._get_engine(None, 10)
     loss, grads, terms = eng._phase_a()
@@ -55,8 +55,9 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(600)
-def test_dp_two_ranks_on_gpu_match_single_process():
-    ref = _build(False)
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
+def test_dp_two_ranks_on_gpu_match_single_process(precision):
+    ref = _build(False, 1, precision)
     eng = ref._get_engine(None, 10)
     loss, grads, terms = eng._phase_a()
     loss = float(loss)   # persistent device buffer: read before fit() overwrites it
@@ -69,7 +70,7 @@ def test_dp_two_ranks_on_gpu_match_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, precision)) for r in range(2)]
     for p in procs:
         p.start()
     res = q.get(timeout=500)
