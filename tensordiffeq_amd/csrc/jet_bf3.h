@@ -279,17 +279,31 @@ __device__ __forceinline__ Tl tl_make(const void* uniform_base, int lane) {
 #endif
 // Precision "bf16" (!LO) saves the derivative streams (s >= 1) as bf16: the next layer's GEMM already
 // consumed them rounded to bf16, so the dK images are unchanged, and the tanh-jet adjoint sees the
-// same 2^-9 relative rounding the forward applied; the value stream stays fp32 (s1 = 1 - h^2 near
-// saturation needs it).  Per wave and layer: [t] fp32 value tiles, then [s-1][t] bf16 tiles with an
-// 8-byte lane stride.  -DTDQ_BF16_HS_FP32 keeps every stream fp32 (A/B).
+// same 2^-9 relative rounding the forward applied.  The value stream h in (-1, 1) is saved as fp16
+// (absolute error <= 2^-12, vs bf16's 2^-9 relative: s1 = 1 - h^2 near saturation needs the
+// mantissa).  Every tile is 8 bytes per lane: per wave and layer [s][t] tiles of 64 x 8 B.
+// -DTDQ_BF16_HS_FP32 keeps every stream fp32, -DTDQ_HS_VALUE_FP32 only the value stream (A/B;
+// the value tiles then take 16 B per lane).
 #ifdef TDQ_BF16_HS_FP32
 #define TDQ_HS_HALF(LO) false
 #else
 #define TDQ_HS_HALF(LO) (!(LO))
 #endif
+#ifdef TDQ_HS_VALUE_FP32
+#define TDQ_HS_V16 0
+#else
+#define TDQ_HS_V16 1
+#endif
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 template <int WT, bool LO>
 __host__ __device__ constexpr int hs_wave_floats(int S) {
-  return TDQ_HS_HALF(LO) ? WT * (256 + (S - 1) * 128) : S * WT * 256;
+  return TDQ_HS_HALF(LO) ? WT * ((TDQ_HS_V16 ? 128 : 256) + (S - 1) * 128) : S * WT * 256;
+}
+// byte offset of tile (s, t) inside a wave's half-precision region (lane stride 8 B, or 16 B for
+// an fp32 value stream)
+template <int WT>
+__device__ __forceinline__ int hs_half_off(int s, int t) {
+  return TDQ_HS_V16 ? (s * WT + t) * 512 : (s == 0 ? t * 1024 : WT * 1024 + ((s - 1) * WT + t) * 512);
 }
 // wave w's region of saved layer `layer` (uniform base; the lane offset lives in Tl::v)
 template <int WT, bool LO>
@@ -303,13 +317,14 @@ typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
 template <int WT, bool LO>
 __device__ __forceinline__ void hs_store(const Tl& T, int s, int t, const f32x4& v) {
   if constexpr (TDQ_HS_HALF(LO)) {
-    if (s > 0) {
-      const bf16x4 b = __builtin_convertvector(v, bf16x4);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, b), T.r, T.v >> 1,
-                                            (WT * 256 + ((s - 1) * WT + t) * 128) * 4, TDQ_POL_ST);
+    if (s == 0 && !TDQ_HS_V16) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_half_off<WT>(0, t),
+                                             TDQ_POL_ST);
       return;
     }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, t * 256 * 4, TDQ_POL_ST);
+    const u32x2v u = s == 0 ? __builtin_bit_cast(u32x2v, __builtin_convertvector(v, f16x4))
+                            : __builtin_bit_cast(u32x2v, __builtin_convertvector(v, bf16x4));
+    __builtin_amdgcn_raw_buffer_store_b64(u, T.r, T.v >> 1, hs_half_off<WT>(s, t), TDQ_POL_ST);
   } else {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_ST);
   }
@@ -317,13 +332,13 @@ __device__ __forceinline__ void hs_store(const Tl& T, int s, int t, const f32x4&
 template <int WT, bool LO, int POL>
 __device__ __forceinline__ f32x4 hs_load_p(const Tl& T, int s, int t) {
   if constexpr (TDQ_HS_HALF(LO)) {
-    if (s > 0) {
-      const u32x2v u = __builtin_amdgcn_raw_buffer_load_b64(T.r, T.v >> 1, (WT * 256 + ((s - 1) * WT + t) * 128) * 4, POL);
-      // bf16 -> fp32: the bf16 bits are the high half of the fp32 word
-      return f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
-                   __uint_as_float(u[1] & 0xffff0000u)};
-    }
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, t * 256 * 4, POL));
+    if (s == 0 && !TDQ_HS_V16)
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_half_off<WT>(0, t), POL));
+    const u32x2v u = __builtin_amdgcn_raw_buffer_load_b64(T.r, T.v >> 1, hs_half_off<WT>(s, t), POL);
+    if (s == 0) return __builtin_convertvector(__builtin_bit_cast(f16x4, u), f32x4);
+    // bf16 -> fp32: the bf16 bits are the high half of the fp32 word
+    return f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+                 __uint_as_float(u[1] & 0xffff0000u)};
   } else {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(T.r, T.v, hs_off(s, t, WT) * 4, POL));
   }
