@@ -756,7 +756,12 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // images: h hi, (h lo,) zb hi, (zb lo) - the lo images only under LO
   constexpr int HL = LO ? 2 : 1;
   constexpr int IH = 0, IHL = IMG, IZ = HL * IMG, IZL = 3 * IMG;
-  constexpr int U1 = (2 * HL * IMG) / 2;      // images, in floats
+  // bf16 (!LO): two image buffers, stream s writes buffer s & 1, so one barrier per stream
+  // separates "images of s written" from "MFMAs of s - 1 done" (bf16x3: one buffer, two barriers;
+  // its LDS holds no second set)
+  constexpr bool DBUF = !LO;
+  constexpr int IBUF = 2 * HL * IMG;          // one buffer's images, in bf16
+  constexpr int U1 = (DBUF ? 2 : 1) * IBUF / 2;  // images, in floats
   constexpr int U2 = NWV * S * WT * HL * 128;  // per-wave zb fragment stages (bf16 hi(/lo))
   constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
   static_assert(NWV * (W * TDQ_MAXO + TDQ_MAXO + TDQ_MAXD * W) <= U, "partials must fit the union");
@@ -920,7 +925,11 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       for (int c = 0; c < NC; ++c) dw[r][c] = zero4();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      __syncthreads();  // previous readers of the region (zb stage / last stream's images) done
+      // previous users of the region done: the zb stage (s = 0) / the last stream's images (one
+      // buffer only; with two, the barrier after this stream's image writes already orders them
+      // after the MFMAs of s - 1, the last readers of the buffer written here)
+      if (s == 0 || !DBUF) __syncthreads();
+      __bf16* const im = img + (DBUF ? (s & 1) * IBUF : 0);
       if (s == 0 && w == 0) {  // bias of layer i: partials of all waves landed before this barrier
         const float* accBi = accB + (i & 1) * NWV * W;
         const int bo = off_layer(d, i) + d.width * d.width;
@@ -940,11 +949,11 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
           bf16x4 hi, lo;
           split_or_round<LO>(rec0 ? h0_stream<WT, S, NSO>(sp, aux, hp[t], t, g, s) : hp[t], hi, lo);
           const int off = row * RS + ((16 * t + 4 * wch) ^ rsw);
-          *reinterpret_cast<bf16x4*>(img + IH + off) = hi;
-          *reinterpret_cast<bf16x4*>(img + IZ + off) = half8(zh[s][t >> 1], t & 1);
+          *reinterpret_cast<bf16x4*>(im + IH + off) = hi;
+          *reinterpret_cast<bf16x4*>(im + IZ + off) = half8(zh[s][t >> 1], t & 1);
           if constexpr (LO) {
-            *reinterpret_cast<bf16x4*>(img + IHL + off) = lo;
-            *reinterpret_cast<bf16x4*>(img + IZL + off) = half8(zl[s][t >> 1], t & 1);
+            *reinterpret_cast<bf16x4*>(im + IHL + off) = lo;
+            *reinterpret_cast<bf16x4*>(im + IZL + off) = half8(zl[s][t >> 1], t & 1);
           }
         }
       }
@@ -968,16 +977,16 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
         for (int r = 0; r < NR; ++r) {
           const int off = ra1 + 32 * kb * RS + 16 * r;
           const int of2 = ra2 + 32 * kb * RS + 16 * r;
-          Ah[r] = cat8(tr_read(img + IH + off), tr_read(img + IH + of2));
-          if constexpr (LO) Al[r] = cat8(tr_read(img + IHL + off), tr_read(img + IHL + of2));
+          Ah[r] = cat8(tr_read(im + IH + off), tr_read(im + IH + of2));
+          if constexpr (LO) Al[r] = cat8(tr_read(im + IHL + off), tr_read(im + IHL + of2));
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           const int off = ca1 + 32 * kb * RS + 16 * c;
           const int of2 = ca2 + 32 * kb * RS + 16 * c;
-          const bf16x8 Bh = cat8(tr_read(img + IZ + off), tr_read(img + IZ + of2));
+          const bf16x8 Bh = cat8(tr_read(im + IZ + off), tr_read(im + IZ + of2));
           bf16x8 Bl;
-          if constexpr (LO) Bl = cat8(tr_read(img + IZL + off), tr_read(img + IZL + of2));
+          if constexpr (LO) Bl = cat8(tr_read(im + IZL + off), tr_read(im + IZL + of2));
 #pragma unroll
           for (int r = 0; r < NR; ++r) dw[r][c] = mfma_aa<LO>(Ah[r], Al[r], Bh, Bl, dw[r][c]);
         }
@@ -1089,7 +1098,7 @@ inline int h0_recompute() {
 
 inline size_t bwd_bf3_lds(int WT, int S, bool lo) {
   const int W = 16 * WT, hl = lo ? 2 : 1, nwv = bwd_waves(WT, lo);
-  const size_t u1 = (size_t)(2 * hl * 16 * nwv * 144) / 2, u2 = (size_t)nwv * S * WT * hl * 128;
+  const size_t u1 = (size_t)(lo ? 1 : 2) * (2 * hl * 16 * nwv * 144) / 2, u2 = (size_t)nwv * S * WT * hl * 128;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
   return (u + 3 * nwv * W) * sizeof(float);
 }
