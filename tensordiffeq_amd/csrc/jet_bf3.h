@@ -279,20 +279,21 @@ __device__ __forceinline__ Tl tl_make(const void* uniform_base, int lane) {
 #endif
 // Precision "bf16" (!LO) saves the derivative streams (s >= 1) as bf16: the next layer's GEMM already
 // consumed them rounded to bf16, so the dK images are unchanged, and the tanh-jet adjoint sees the
-// same 2^-9 relative rounding the forward applied.  The value stream h in (-1, 1) is saved as fp16
-// (absolute error <= 2^-12, vs bf16's 2^-9 relative: s1 = 1 - h^2 near saturation needs the
-// mantissa).  Every tile is 8 bytes per lane: per wave and layer [s][t] tiles of 64 x 8 B.
-// -DTDQ_BF16_HS_FP32 keeps every stream fp32, -DTDQ_HS_VALUE_FP32 only the value stream (A/B;
-// the value tiles then take 16 B per lane).
+// same 2^-9 relative rounding the forward applied.  The value stream h stays fp32: s1 = 1 - h^2
+// of a saturated unit loses every digit to a 16-bit h (fp16 ulp at |h| ~ 1 is 2^-11).  Storing it
+// as fp16 (-DTDQ_HS_VALUE_FP16: every tile 8 B per lane) was 2.5 % faster per step, but the AC-SA
+// reference schedule (Adam bf16 + L-BFGS bf16x3) ended at L2 4.3/2.8/4.9/3.7/3.6e-2 over seeds
+// 0-4 against 3.3/2.6/3.4/4.8/2.9e-2 with the fp32 value stream (profiles/r2_v7_accuracy_seeds.txt).
+// -DTDQ_BF16_HS_FP32 keeps every stream fp32 (A/B).
 #ifdef TDQ_BF16_HS_FP32
 #define TDQ_HS_HALF(LO) false
 #else
 #define TDQ_HS_HALF(LO) (!(LO))
 #endif
-#ifdef TDQ_HS_VALUE_FP32
-#define TDQ_HS_V16 0
-#else
+#ifdef TDQ_HS_VALUE_FP16
 #define TDQ_HS_V16 1
+#else
+#define TDQ_HS_V16 0
 #endif
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 template <int WT, bool LO>
