@@ -1,6 +1,20 @@
 // Host ABI + weight-image packing for the split-bf16 (bf16x3) jet kernels (kernels: jet_bf3.h,
-// instantiations: jet_bf3_w{2,4,8}.hip).
+// instantiations: jet_bf3_w{2,4,8}.hip), and the fused step tail of a captured Adam step.
+//
+// Step tail (tdq_step_tail_bf3): the single-GPU Adam step used to end in seven small launches
+// (weight-image pack, loss reduction, two slab-reduction passes, bookkeeping, Adam) of ~4.7 us
+// each on MI355X, mostly launch/drain floor.  Two launches now do that work:
+//   tail_reduce1: slab pass 1 (columns x chunks) + ONE extra workgroup that reduces the loss
+//                 partials (per-term losses, scalar-lambda gradients) and runs the scalar
+//                 bookkeeping (history row, best loss + "improved" flag, step counters, epoch) -
+//                 nothing else in that launch reads those scalars, so no grid sync is needed;
+//   tail_adam:    slab pass 2 fused element-wise into the Adam update of theta (the reduced
+//                 gradient is also written out), the Adam ascent of the SA weights, the best-
+//                 weights snapshot, and the next step's weight images: every updated weight is
+//                 scattered straight into its forward / backward A-image (bf16 hi + lo) or aux
+//                 slot, so the next forward runs without a pack launch.
 #include "jet_bf3.h"
+#include "optim_common.h"
 
 // A-operand images: img[layer-1][o][kb][hl][lane] = 8 bf16 (hl 0 = hi, 1 = lo)
 //   element j of lane (p, g): row 16o + p, k = 8g + j -> feature 32kb + (j<4 ? 4g+j : 16+4g+j-4)
@@ -69,6 +83,168 @@ __global__ void __launch_bounds__(256) pack_all_kernel(const float* __restrict__
   }
 }
 
+// ---- fused step tail ------------------------------------------------------------------------
+struct TailBook {
+  const float* lpart;  // loss-kernel block partials [n_lblocks][n_terms + n_scal]
+  int n_lblocks, n_terms, n_scal;
+  float* losses;
+  float* total;
+  float* dscal;
+  float* hist;
+  int64_t hist_rows;
+  int64_t* epoch;
+  float* best_loss;
+  int64_t* best_epoch;
+  int* improved;
+  Counters cnt;
+};
+
+__global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restrict__ slab, float* __restrict__ part,
+                                                           int nwg, int Pst, int chunks, int nqb, TailBook tb) {
+  if ((int)blockIdx.x < nqb) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (4 * q < Pst) slab_reduce1_body(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+    return;
+  }
+  if (blockIdx.y != 0) return;
+  // loss partials -> per-term losses / scalar gradients (the loss_reduce_kernel order), then the
+  // bookkeeping on the summed terms
+  __shared__ float sh[256];
+  const int ns = tb.n_terms + tb.n_scal;
+  for (int slot = 0; slot < ns; ++slot) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < tb.n_lblocks; b += 256) s += tb.lpart[(size_t)b * ns + slot];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+      if ((int)threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (slot < tb.n_terms) tb.losses[slot] = sh[0];
+      else tb.dscal[slot - tb.n_terms] = sh[0];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    step_book_body(tb.total, tb.losses, tb.n_terms, 1, tb.hist, tb.hist_rows, tb.epoch, tb.best_loss, tb.best_epoch,
+                   tb.improved, tb.cnt);
+}
+
+struct TailImg {
+  __bf16* fimg;  // forward A image (nullptr: no image update)
+  __bf16* bimg;  // backward A image
+  float* aux;
+  NetDims d;
+  int WT;
+};
+
+// element (row, kf) of hidden layer `layer`'s A image -> bf16 hi / lo (inverse of pack_frag)
+__device__ __forceinline__ void img_put(__bf16* __restrict__ img, int layer, int row, int kf, int WT, __bf16 hi,
+                                        __bf16 lo) {
+  const int KB = WT / 2;
+  const int o = row >> 4, p = row & 15, kb = kf >> 5, rr = kf & 31;
+  const int g = (rr & 15) >> 2, j = (rr & 3) + (rr >= 16 ? 4 : 0);
+  const int lane = p + 16 * g;
+  const size_t frag = ((size_t)(layer - 1) * WT + o) * KB + kb;
+  img[((frag * 2) * 64 + lane) * 8 + j] = hi;
+  img[((frag * 2 + 1) * 64 + lane) * 8 + j] = lo;
+}
+
+// flat (Keras-order) parameter e with new value v -> its slot in the images (inverse of pack_all)
+__device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti) {
+  const NetDims& d = ti.d;
+  const int W = 16 * ti.WT, w = d.width;
+  const int n0 = d.d_in * w;
+  if (e < n0) {
+    const int j = e / w;
+    ti.aux[j * W + (e - j * w)] = v;
+    return;
+  }
+  if (e < n0 + w) {
+    ti.aux[aux_b0(d, W) + (e - n0)] = v;
+    return;
+  }
+  const int r = e - (n0 + w), L = w * w + w;
+  if (r < (d.n_hidden - 1) * L) {
+    const int i = r / L + 1, q = r - (i - 1) * L;
+    if (q < w * w) {
+      const int in = q / w, out = q - in * w;
+      const __bf16 hi = (__bf16)v, lo = (__bf16)(v - (float)hi);
+      img_put(ti.fimg, i, out, in, ti.WT, hi, lo);  // forward: A[row = out][k = in]
+      img_put(ti.bimg, i, in, out, ti.WT, hi, lo);  // backward: A[row = in][k = out]
+    } else {
+      ti.aux[aux_bh(d, W) + (i - 1) * W + (q - w * w)] = v;
+    }
+    return;
+  }
+  const int r2 = r - (d.n_hidden - 1) * L;
+  if (r2 < w * d.d_out) {
+    const int f = r2 / d.d_out;
+    ti.aux[aux_ko(d, W) + f * 4 + (r2 - f * d.d_out)] = v;
+  } else {
+    ti.aux[aux_bo(d, W) + (r2 - w * d.d_out)] = v;
+  }
+}
+
+// Adam over every group; group 0 = theta, whose gradient is the second slab pass of its float4
+// column (slot == column), written to args.grp[0].g as well
+__global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const float* __restrict__ part, int Pst,
+                                                        int chunks, const int* __restrict__ improved,
+                                                        float* __restrict__ snap, TailImg ti) {
+  const bool do_snap = snap != nullptr && *improved != 0;
+  const int64_t total = args.start[args.ngroups];
+  for (int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x; slot < total; slot += (int64_t)gridDim.x * 256) {
+    const int gi = adam_group_of(args, slot);
+    const AdamGroup gr = args.grp[gi];
+    const int64_t e0 = (slot - args.start[gi]) * 4;
+    const float sg = gr.sign, b1 = gr.b1, b2 = gr.b2, eps = gr.eps;
+    const float lr_t = adam_lr_t(gr);
+    const bool th = gi == 0;
+    float* gout = const_cast<float*>(gr.g);
+    f32x4 g = zero4();
+    if (th) g = slab_reduce2_sum(part, Pst, chunks, (int)slot);
+    const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
+    if (aligned && e0 + 4 <= gr.n) {
+      f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
+      if (do_snap && th) *reinterpret_cast<f32x4*>(snap + e0) = p;
+      if (th) *reinterpret_cast<f32x4*>(gout + e0) = g;
+      else g = *reinterpret_cast<const f32x4*>(gr.g + e0);
+      f32x4 m = *reinterpret_cast<const f32x4*>(gr.m + e0);
+      f32x4 v = *reinterpret_cast<const f32x4*>(gr.v + e0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float pc = p[c], mc = m[c], vc = v[c];
+        adam_elem(pc, sg * g[c], mc, vc, b1, b2, eps, lr_t);
+        p[c] = pc; m[c] = mc; v[c] = vc;
+      }
+      *reinterpret_cast<f32x4*>(gr.p + e0) = p;
+      *reinterpret_cast<f32x4*>(gr.m + e0) = m;
+      *reinterpret_cast<f32x4*>(gr.v + e0) = v;
+      if (th && ti.fimg != nullptr) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) scatter_param(p[c], (int)(e0 + c), ti);
+      }
+    } else {
+      for (int c = 0; c < 4; ++c) {
+        const int64_t e = e0 + c;
+        if (e < gr.n) {
+          if (do_snap && th) snap[e] = gr.p[e];
+          float gc;
+          if (th) {
+            gc = g[c];
+            gout[e] = gc;
+          } else {
+            gc = gr.g[e];
+          }
+          adam_elem(gr.p[e], sg * gc, gr.m[e], gr.v[e], b1, b2, eps, lr_t);
+          if (th && ti.fimg != nullptr) scatter_param(gr.p[e], (int)e, ti);
+        }
+      }
+    }
+  }
+}
+
 namespace {
 
 int64_t img_floats(int WT, int n_hidden) {  // hi/lo A images, in floats
@@ -121,9 +297,20 @@ int64_t tdq_jet_bf3_slab_floats(int N, int d_in, int width, int d_out, int n_hid
   return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
 
-// lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16)
-int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
-                    int d_out, int n_hidden, int S, const int* spec, int lo, void* stream) {
+// image pointers inside the forward's scratch (right after the saved post-activations Hs)
+static inline void scratch_images(float* scratch, int N, int n_hidden, int S, int WT, float** img, float** bimg,
+                                  float** aux) {
+  const int64_t nwg = (N + 63) / 64;
+  *img = scratch + (int64_t)n_hidden * nwg * S * 4 * WT * 256;
+  *bimg = *img + img_floats(WT, n_hidden);
+  *aux = *bimg + img_floats(WT, n_hidden);
+}
+
+// lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16).
+// pack = 0: the weight images in scratch are already current (written by the previous step's
+// tail_adam), so the forward skips its pack launch.
+int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
+                       int d_out, int n_hidden, int S, const int* spec, int lo, int pack, void* stream) {
   if (N <= 0) return 0;
   const int WT = width_tiles(width);
   JetSpec sp;
@@ -131,20 +318,38 @@ int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, in
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int64_t nwg = (N + 63) / 64;
   float* Hs = scratch;
-  float* img = scratch + (int64_t)n_hidden * nwg * S * 4 * WT * 256;
-  float* bimg = img + img_floats(WT, n_hidden);
-  float* aux = bimg + img_floats(WT, n_hidden);
-  int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
-  if (rc) return rc;
+  float *img, *bimg, *aux;
+  scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+  if (pack) {
+    int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
+    if (rc) return rc;
+  }
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo};
   return dispatch(true, WT, S, nso, a);
 }
 
-int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
-                    int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo,
-                    void* stream) {
+int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
+                    int d_out, int n_hidden, int S, const int* spec, int lo, void* stream) {
+  return tdq_jet_fwd_bf3_ex(X, P, J, scratch, N, d_in, width, d_out, n_hidden, S, spec, lo, 1, stream);
+}
+
+// the weight images of a forward scratch, packed from P (one launch)
+int tdq_jet_bf3_pack(const float* P, float* scratch, int N, int d_in, int width, int d_out, int n_hidden, int S,
+                     void* stream) {
+  const int WT = width_tiles(width);
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  NetDims d{d_in, width, d_out, n_hidden};
+  float *img, *bimg, *aux;
+  scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+  return launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT,
+                     reinterpret_cast<hipStream_t>(stream));
+}
+
+// reduce = 0: only the backward kernel (gradient slabs in work); tdq_step_tail_bf3 reduces them
+int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
+                       int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo, int reduce,
+                       void* stream) {
   if (N <= 0) return 0;
   const int WT = width_tiles(width);
   JetSpec sp;
@@ -152,21 +357,87 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int nwg = (N + 63) / 64;                               // forward (saved-activation) geometry
   const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
   const int chunks = slab_chunks(nwg_b);
   float* slab = work;
   // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
-  const float* img = Hs + (int64_t)n_hidden * nwg * S * 4 * WT * 256 + img_floats(WT, n_hidden);
-  const float* aux = img + img_floats(WT, n_hidden);
+  float *img, *bimg, *aux;
+  scratch_images(const_cast<float*>(Hs), N, n_hidden, S, WT, &img, &bimg, &aux);
   (void)P;
+  (void)img;
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
-  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), dJ, nullptr, const_cast<float*>(Hs), slab, N,
+  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), slab, N,
             slab_stride(Ptot), d, sp, st, lo};
   int rc = dispatch(false, WT, S, nso, a);
-  if (rc) return rc;
+  if (rc || !reduce) return rc;
   return tdq_slab_reduce(work, grad, nwg_b, Ptot, chunks, stream);
+}
+
+int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
+                    int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo,
+                    void* stream) {
+  return tdq_jet_bwd_bf3_ex(X, P, dJ, Hs, work, grad, N, d_in, width, d_out, n_hidden, S, spec, lo, 1, stream);
+}
+
+// The end of a single-process Adam step in two launches (see the file comment).  work: the
+// backward's gradient slabs (tdq_jet_bwd_bf3_ex with reduce = 0); grad: receives the reduced theta
+// gradient; scratch: the forward's scratch whose images are rewritten for the next step (nullptr:
+// leave them).  groups[0] must be theta (n == parameter count); its g pointer is replaced by grad.
+int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in, int width, int d_out, int n_hidden,
+                      int S, int lo, const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses,
+                      float* total, float* dscal, float* hist, int64_t hist_rows, int64_t* epoch, float* best_loss,
+                      int64_t* best_epoch, int* improved, double* const* counters, int ncnt, const void* groups,
+                      int ngroups, float* snap, void* stream) {
+  const int WT = width_tiles(width);
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || ncnt < 0 || ncnt > TDQ_MAX_COUNTERS || n_lblocks < 0 ||
+      n_terms < 0 || n_scal < 0)
+    return (int)hipErrorInvalidValue;
+  AdamArgs args;
+  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups)) return (int)hipErrorInvalidValue;
+  const int Ptot = param_count(d_in, width, d_out, n_hidden);
+  if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
+  args.grp[0].g = grad;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;
+  const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
+  float* part = work + (size_t)nwg_b * Pst;
+  TailBook tb;
+  tb.lpart = lpart;
+  tb.n_lblocks = n_lblocks;
+  tb.n_terms = n_terms;
+  tb.n_scal = n_scal;
+  tb.losses = losses;
+  tb.total = total;
+  tb.dscal = dscal;
+  tb.hist = hist;
+  tb.hist_rows = hist_rows;
+  tb.epoch = epoch;
+  tb.best_loss = best_loss;
+  tb.best_epoch = best_epoch;
+  tb.improved = improved;
+  tb.cnt.n = ncnt;
+  for (int i = 0; i < TDQ_MAX_COUNTERS; ++i) tb.cnt.c[i] = i < ncnt ? counters[i] : nullptr;
+  const int nqb = (Pst / 4 + 255) / 256;
+  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
+                     nqb, tb);
+  TDQ_CHECK_LAUNCH();
+  TailImg ti{nullptr, nullptr, nullptr, NetDims{d_in, width, d_out, n_hidden}, WT};
+  if (scratch != nullptr) {
+    float *img, *bimg, *aux;
+    scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+    ti.fimg = reinterpret_cast<__bf16*>(img);
+    ti.bimg = reinterpret_cast<__bf16*>(bimg);
+    ti.aux = aux;
+  }
+  const int64_t tot = args.start[ngroups];
+  int64_t blocks = (tot + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(tail_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, args, part, Pst, chunks, improved,
+                     snap, ti);
+  TDQ_CHECK_LAUNCH();
+  return 0;
 }
 
 }  // extern "C"

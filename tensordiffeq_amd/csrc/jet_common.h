@@ -87,5 +87,37 @@ static inline int slab_stride(int P) { return (P + 3) & ~3; }
 // workgroup-chunk count of the first reduction pass
 static inline int slab_chunks(int nwg) { return nwg < 16 ? nwg : 16; }
 
+// first reduction pass, float4 column q of chunk c: part[c][q] = sum of slab rows of the chunk
+__device__ __forceinline__ void slab_reduce1_body(const float* __restrict__ slab, float* __restrict__ part, int nwg,
+                                                  int Pst, int chunks, int q, int c) {
+  const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab) + q;
+  const size_t row = (size_t)(Pst >> 2);
+  f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();
+  int wgi = lo;
+  for (; wgi + 3 < hi; wgi += 4) {
+    a0 += s4[(size_t)wgi * row];
+    a1 += s4[(size_t)(wgi + 1) * row];
+    a2 += s4[(size_t)(wgi + 2) * row];
+    a3 += s4[(size_t)(wgi + 3) * row];
+  }
+  for (; wgi < hi; ++wgi) a0 += s4[(size_t)wgi * row];
+  reinterpret_cast<f32x4*>(part)[(size_t)c * row + q] = (a0 + a1) + (a2 + a3);
+}
+
+// second pass: the gradient of float4 column q (fixed summation order: deterministic)
+__device__ __forceinline__ f32x4 slab_reduce2_sum(const float* __restrict__ part, int Pst, int chunks, int q) {
+  const f32x4* p4 = reinterpret_cast<const f32x4*>(part) + q;
+  const size_t row = (size_t)(Pst >> 2);
+  f32x4 a0 = zero4(), a1 = zero4();
+  int c = 0;
+  for (; c + 1 < chunks; c += 2) {
+    a0 += p4[(size_t)c * row];
+    a1 += p4[(size_t)(c + 1) * row];
+  }
+  if (c < chunks) a0 += p4[(size_t)c * row];
+  return a0 + a1;
+}
+
 // slabs [nwg][slab_stride(P)] at work, partials [chunks][slab_stride(P)] right after -> grad[P]
 extern "C" int tdq_slab_reduce(float* work, float* grad, int nwg, int P, int chunks, void* stream);

@@ -598,37 +598,15 @@ jet_bwd_kernel(const float* __restrict__ X, const float* __restrict__ P, const f
 __global__ void __launch_bounds__(256) slab_reduce1(const float* __restrict__ slab, float* __restrict__ part,
                                                     int nwg, int Pst, int chunks) {
   const int q = blockIdx.x * 256 + threadIdx.x;  // float4 column
-  const int c = blockIdx.y;
   if (4 * q >= Pst) return;
-  const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
-  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab) + q;
-  const size_t row = (size_t)(Pst >> 2);
-  f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();
-  int wgi = lo;
-  for (; wgi + 3 < hi; wgi += 4) {
-    a0 += s4[(size_t)wgi * row];
-    a1 += s4[(size_t)(wgi + 1) * row];
-    a2 += s4[(size_t)(wgi + 2) * row];
-    a3 += s4[(size_t)(wgi + 3) * row];
-  }
-  for (; wgi < hi; ++wgi) a0 += s4[(size_t)wgi * row];
-  reinterpret_cast<f32x4*>(part)[(size_t)c * row + q] = (a0 + a1) + (a2 + a3);
+  slab_reduce1_body(slab, part, nwg, Pst, chunks, q, blockIdx.y);
 }
 
 __global__ void __launch_bounds__(256) slab_reduce2(const float* __restrict__ part, float* __restrict__ grad, int P,
                                                     int Pst, int chunks) {
   const int q = blockIdx.x * 256 + threadIdx.x;
   if (4 * q >= P) return;
-  const f32x4* p4 = reinterpret_cast<const f32x4*>(part) + q;
-  const size_t row = (size_t)(Pst >> 2);
-  f32x4 a0 = zero4(), a1 = zero4();
-  int c = 0;
-  for (; c + 1 < chunks; c += 2) {
-    a0 += p4[(size_t)c * row];
-    a1 += p4[(size_t)(c + 1) * row];
-  }
-  if (c < chunks) a0 += p4[(size_t)c * row];
-  const f32x4 a = a0 + a1;
+  const f32x4 a = slab_reduce2_sum(part, Pst, chunks, q);
 #pragma unroll
   for (int e = 0; e < 4; ++e)
     if (4 * q + e < P) grad[4 * q + e] = a[e];

@@ -14,36 +14,7 @@
 //   every Adam step counter += 1, epoch += 1.  The Adam kernel then snapshots theta into the
 //   best-weights buffer (before its update) when the flag is set, so best tracking costs no
 //   extra launch.
-#include "common.h"
-
-#define TDQ_MAX_GROUPS 16
-
-// one tensor of the update with its optimizer's hyper-parameters and device step counter, so the
-// network (descent) and self-adaptive-weight (ascent) optimizers share one launch
-struct AdamGroup {
-  float* p;
-  const float* g;
-  float* m;
-  float* v;
-  int64_t n;
-  float sign;
-  float lr, b1, b2, eps;
-  float pad;
-  const double* t;
-};
-
-struct AdamArgs {
-  AdamGroup grp[TDQ_MAX_GROUPS];
-  int64_t start[TDQ_MAX_GROUPS + 1];  // prefix sums of float4 "slots" per group
-  int ngroups;
-};
-
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2,
-                                          float eps, float lr_t) {
-  m = fmaf(1.f - b1, g, b1 * m);
-  v = fmaf(1.f - b2, g * g, b2 * v);
-  p = p - lr_t * m / (sqrtf(v) + eps);
-}
+#include "optim_common.h"
 
 __global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const int* __restrict__ improved,
                                                           float* __restrict__ snap) {
@@ -51,15 +22,11 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamArgs args, const in
   const int64_t total = args.start[args.ngroups];
   for (int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x; slot < total;
        slot += (int64_t)gridDim.x * 256) {
-    int gi = 0;
-#pragma unroll
-    for (int q = 1; q < TDQ_MAX_GROUPS; ++q)
-      if (q < args.ngroups && slot >= args.start[q]) gi = q;
+    const int gi = adam_group_of(args, slot);
     const AdamGroup gr = args.grp[gi];
     const int64_t e0 = (slot - args.start[gi]) * 4;
     const float sg = gr.sign, b1 = gr.b1, b2 = gr.b2, eps = gr.eps;
-    const double t = *gr.t;  // bias-corrected step size from the group's device step counter
-    const float lr_t = (float)((double)gr.lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
+    const float lr_t = adam_lr_t(gr);
     const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
     if (aligned && e0 + 4 <= gr.n) {
       f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
@@ -107,41 +74,16 @@ __global__ void best_scalar_kernel(const float* __restrict__ loss, float* __rest
   }
 }
 
-#define TDQ_MAX_COUNTERS 8
-struct Counters {
-  double* c[TDQ_MAX_COUNTERS];
-  int n;
-};
-
 __global__ void step_book_kernel(float* __restrict__ loss, const float* __restrict__ terms, int n_terms, int sum_terms,
                                  float* __restrict__ hist, int64_t hist_rows, int64_t* __restrict__ epoch,
                                  float* __restrict__ best_loss, int64_t* __restrict__ best_epoch,
                                  int* __restrict__ improved, Counters cnt) {
-  float lv = *loss;
-  if (sum_terms) {  // fused loss: total = sum of the (all-reduced) terms, in term order
-    lv = 0.f;
-    for (int t = 0; t < n_terms; ++t) lv += terms[t];
-    *loss = lv;
-  }
-  const int64_t ep = *epoch;
-  if (ep >= 0 && ep < hist_rows) {
-    float* row = hist + ep * (1 + n_terms);
-    row[0] = lv;
-    for (int t = 0; t < n_terms; ++t) row[1 + t] = terms[t];
-  }
-  const int imp = lv < *best_loss;  // NaN never improves
-  if (imp) {
-    *best_loss = lv;
-    *best_epoch = ep;
-  }
-  *improved = imp;
-  for (int i = 0; i < cnt.n; ++i) *cnt.c[i] += 1.0;
-  *epoch = ep + 1;
+  step_book_body(loss, terms, n_terms, sum_terms, hist, hist_rows, epoch, best_loss, best_epoch, improved, cnt);
 }
 
 extern "C" {
 
-int tdq_abi_version() { return 9; }
+int tdq_abi_version() { return 10; }
 
 int tdq_step_book(float* loss, const float* terms, int n_terms, int sum_terms, float* hist, int64_t hist_rows,
                   int64_t* epoch, float* best_loss, int64_t* best_epoch, int* improved, double* const* counters,
@@ -159,20 +101,8 @@ int tdq_step_book(float* loss, const float* terms, int n_terms, int sum_terms, f
 // groups carry their own lr / b1 / b2 / eps / step-counter pointer.  improved / snap: optional
 // (nullptr) best-weights snapshot of group 0 before its update
 int tdq_adam_multi(const void* groups, int ngroups, const int* improved, float* snap, void* stream) {
-  if (ngroups <= 0 || ngroups > TDQ_MAX_GROUPS) return (int)hipErrorInvalidValue;
   AdamArgs args;
-  const AdamGroup* src = reinterpret_cast<const AdamGroup*>(groups);
-  args.ngroups = ngroups;
-  args.start[0] = 0;
-  for (int i = 0; i < TDQ_MAX_GROUPS; ++i) {
-    if (i < ngroups) {
-      args.grp[i] = src[i];
-      args.start[i + 1] = args.start[i] + (src[i].n + 3) / 4;
-    } else {
-      args.grp[i] = AdamGroup{nullptr, nullptr, nullptr, nullptr, 0, 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, nullptr};
-      if (i + 1 <= TDQ_MAX_GROUPS) args.start[i + 1] = args.start[i];
-    }
-  }
+  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups)) return (int)hipErrorInvalidValue;
   const int64_t total = args.start[ngroups];
   if (total == 0) return 0;
   int64_t blocks = (total + 255) / 256;

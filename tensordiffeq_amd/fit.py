@@ -99,6 +99,7 @@ class AdamEngine:
     def _bind_opts(self):
         """(Re)read optimizer objects - users may replace e.g. ``model.tf_optimizer``."""
         self.opts = [g.get_opt() for g in self.groups]
+        self._tail_ok = None
         self.counters = [o.step_counter(self.device) for o in self.opts]
         self.moments = [[o.state_for(t) for t in g.tensors] for o, g in zip(self.opts, self.groups)]
 
@@ -134,16 +135,8 @@ class AdamEngine:
                            else ("zero", 0))
         return src
 
-    def _phase_a_fused(self, fop, for_step=False):
-        # (Running the loss reduction + bookkeeping on a side stream beside the jet backward was
-        # measured slower on MI355X: 0.505 vs 0.494 ms per AC-SA step on one box - the backward
-        # holds every SIMD's registers, so the side kernels only delay its workgroups.)
-        from .ops import jet_hip
-        prog = self.program
-        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
-        # inside an optimizer step the bookkeeping kernel (fused.step_book) sums the terms
-        total, losses, dJ, dlam, dscal = fop(J, with_total=not for_step)
-        gflat = jet_hip.backward_raw(saved, dJ)
+    def _fused_grads(self, fop, gflat, dlam, dscal):
+        """Per-wrt-tensor gradients from the fused-loss outputs and the flat theta gradient."""
         if getattr(self, "_fsrc", None) is None:
             self._fsrc = self._fused_map(fop)
         grads = []
@@ -162,6 +155,19 @@ class AdamEngine:
                 grads.append(dscal[k].view_as(w))
             else:
                 grads.append(torch.zeros_like(w))
+        return grads
+
+    def _phase_a_fused(self, fop, for_step=False):
+        # (Running the loss reduction + bookkeeping on a side stream beside the jet backward was
+        # measured slower on MI355X: 0.505 vs 0.494 ms per AC-SA step on one box - the backward
+        # holds every SIMD's registers, so the side kernels only delay its workgroups.)
+        from .ops import jet_hip
+        prog = self.program
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+        # inside an optimizer step the bookkeeping kernel (fused.step_book) sums the terms
+        total, losses, dJ, dlam, dscal = fop(J, with_total=not for_step)
+        gflat = jet_hip.backward_raw(saved, dJ)
+        grads = self._fused_grads(fop, gflat, dlam, dscal)
         return total, grads, losses   # losses: contiguous per-term vector
 
     def _phase_a(self, for_step=False):
@@ -204,13 +210,9 @@ class AdamEngine:
         fused.step_book(loss, tv.reshape(-1).float().contiguous(), st, self.counters,
                         sum_terms=getattr(self, "_sum_terms", False))
 
-    def _phase_b(self, loss, grads, terms):
-        """Bookkeeping (``fused.step_book``: history row, best tracking, step counters, epoch),
-        then ONE Adam launch for every group (each with its optimizer's counter and
-        hyper-parameters), which also snapshots the best weights (before the update) when the
-        step improved the loss."""
-        st = self.state
-        self._book(loss, terms)
+    def _opt_groups(self, grads):
+        """``fused.adam_multi_opts`` rows: each group with its optimizer's counter and
+        hyper-parameters."""
         off = 0
         opt_groups = []
         for grp, opt, t, mom in zip(self.groups, self.opts, self.counters, self.moments):
@@ -218,12 +220,71 @@ class AdamEngine:
             items = [(p, g, m, v, grp.sign) for p, g, (m, v) in zip(grp.tensors, grads[off:off + n], mom)]
             opt_groups.append((items, t, opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon))
             off += n
+        return opt_groups
+
+    def _phase_b(self, loss, grads, terms):
+        """Bookkeeping (``fused.step_book``: history row, best tracking, step counters, epoch),
+        then ONE Adam launch for every group (each with its optimizer's counter and
+        hyper-parameters), which also snapshots the best weights (before the update) when the
+        step improved the loss."""
+        st = self.state
+        self._book(loss, terms)
+        opt_groups = self._opt_groups(grads)
         # theta descent + SA-weight ascent in one launch; it also snapshots the best weights
         snap = (st["best_flat"], st["improved"]) if self.groups[0].tensors[0] is self.flat else None
         fused.adam_multi_opts(opt_groups, snapshot=snap)
         return loss
 
+    # ------------------------------------------------------------ fused step tail ------
+    def _tail_eligible(self):
+        """Single-process step on the split-bf16 jet kernels with the fused loss: the end of the
+        step runs as two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``)."""
+        if getattr(self, "_tail_ok", None) is not None:
+            return self._tail_ok
+        ok = False
+        fop = getattr(self.program, "fused_op", None)
+        if (os.environ.get("TDQ_FUSED_TAIL", "1") != "0" and fop is not None and not self.dist.is_distributed
+                and self.device.type == "cuda" and self.groups[0].tensors[0] is self.flat):
+            from .ops import _lib, jet_hip
+            from .ops.jet_mlp import hip_config
+            prog = self.program
+            try:
+                ok = jet_hip.is_split_bf16(hip_config(prog.net, prog.plan, prog.precision)) and _lib.available()
+            except (ValueError, AttributeError):
+                ok = False
+            if ok:
+                probe = [(w, w, m, v, 1.0) for w, (m, v) in zip(self.wrt, (mv for ms in self.moments for mv in ms))]
+                ok = fused.group_array([(probe, self.counters[0], 0.0, 0.0, 0.0, 0.0)]) is not None
+        self._tail_ok = ok
+        return ok
+
+    def _tail_step(self, in_graph):
+        """One Adam step ending in the fused tail.  ``in_graph``: the step is being captured, so
+        the forward reuses the weight images that the previous replay's tail wrote (the engine
+        re-packs them once before the first replay of every :meth:`run`)."""
+        from .ops import jet_hip
+        prog = self.program
+        fop = prog.fused_op
+        st = self.state
+        if "improved" not in st:
+            st["improved"] = torch.zeros((), dtype=torch.int32, device=self.device)
+        if st["best_flat"].numel() != self.flat.numel():
+            raise ValueError(f"best-weights snapshot has {st['best_flat'].numel()} elements, parameters "
+                             f"{self.flat.numel()}")
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                       pack=not in_graph)
+        fop(J, with_total=False, reduce=False)
+        grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
+        grads = self._fused_grads(fop, grad, fop.dlam, fop.dscal)
+        arr, n = fused.group_array(self._opt_groups(grads))
+        jet_hip.step_tail(saved, work, grad, fop, st, self.counters, arr, n, st["best_flat"],
+                          write_images=in_graph)
+        self._tail_saved = saved
+        return fop.total
+
     def _eager_step(self):
+        if self._tail_eligible():
+            return self._tail_step(in_graph=False)
         loss, grads, terms = self._phase_a(for_step=True)
         loss, grads, terms = self._reduce(loss, grads, terms)
         return self._phase_b(loss, grads, terms)
@@ -240,11 +301,15 @@ class AdamEngine:
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
         pool = torch.cuda.graph_pool_handle()
+        self._graph_saved = None
         if not split:
+            tail = self._tail_eligible()
             g = torch.cuda.CUDAGraph()
             with capture_graph(g, pool=pool):
-                self.static_loss = self._eager_step()
+                self.static_loss = self._tail_step(in_graph=True) if tail else self._eager_step()
             self.graph_a, self.graph_b = g, None
+            if tail:
+                self._graph_saved = self._tail_saved
         else:
             ga = torch.cuda.CUDAGraph()
             with capture_graph(ga, pool=pool):
@@ -294,6 +359,12 @@ class AdamEngine:
             done = 1
             if progress is not None and n_steps == 1:
                 progress(1, float(loss))
+        if use_graph and self.graph_a is not None and getattr(self, "_graph_saved", None) is not None \
+                and done < n_steps:
+            # the captured step's forward reads weight images written by the previous replay's
+            # tail: bring them up to date with the parameters as they are now
+            from .ops import jet_hip
+            jet_hip.pack_images(self._graph_saved)
         while done < n_steps:
             loss = self._replay() if (use_graph and self.graph_a is not None) else self._eager_step()
             done += 1

@@ -34,6 +34,30 @@ def _native(t):
     return t.is_cuda and _lib.available()
 
 
+def _group_array(flat):
+    arr = (_Group * len(flat))()
+    for i, (p, g, m, v, sign, t, lr, b1, b2, eps) in enumerate(flat):
+        arr[i] = _Group(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                        float(sign), float(lr), float(b1), float(b2), float(eps), 0.0, t.data_ptr())
+    return arr
+
+
+def flatten_opt_groups(opt_groups):
+    """``[(groups, t, lr, b1, b2, eps), ...]`` -> one row per tensor."""
+    return [(p, g, m, v, sign, t, lr, b1, b2, eps)
+            for groups, t, lr, b1, b2, eps in opt_groups for (p, g, m, v, sign) in groups]
+
+
+def group_array(opt_groups):
+    """ctypes ``AdamGroup`` array (csrc/optim_common.h) for ONE launch, or ``None`` when the
+    tensors do not fit it (more than 16, or not contiguous float32)."""
+    flat = flatten_opt_groups(opt_groups)
+    if not flat or len(flat) > _MAX_GROUPS or not all(
+            x.dtype == torch.float32 and x.is_contiguous() for gr in flat for x in gr[:4]):
+        return None
+    return _group_array(flat), len(flat)
+
+
 def adam_multi(groups, t, lr, b1, b2, eps, snapshot=None):
     """groups: list of (param, grad, m, v, sign) sharing one optimizer.  ``t``: float64 device step
     counter (already +1).  ``snapshot=(best, improved)``: copy group 0's parameters into ``best``
@@ -45,8 +69,7 @@ def adam_multi_opts(opt_groups, snapshot=None):
     """One launch for several optimizers: ``opt_groups`` = list of ``(groups, t, lr, b1, b2, eps)``
     (e.g. Adam descent on theta and Adam ascent on the SA weights, each with its own step
     counter and hyper-parameters).  ``snapshot`` applies to the first tensor of the first group."""
-    flat = [(p, g, m, v, sign, t, lr, b1, b2, eps)
-            for groups, t, lr, b1, b2, eps in opt_groups for (p, g, m, v, sign) in groups]
+    flat = flatten_opt_groups(opt_groups)
     if not flat:
         return
     if snapshot is not None and snapshot[0].numel() != flat[0][0].numel():
@@ -60,11 +83,7 @@ def adam_multi_opts(opt_groups, snapshot=None):
         for lo in range(0, len(flat), _MAX_GROUPS):
             chunk = flat[lo:lo + _MAX_GROUPS]
             snap = snapshot if lo == 0 else None
-            arr = (_Group * len(chunk))()
-            for i, (p, g, m, v, sign, t, lr, b1, b2, eps) in enumerate(chunk):
-                arr[i] = _Group(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
-                                float(sign), float(lr), float(b1), float(b2), float(eps), 0.0,
-                                t.data_ptr())
+            arr = _group_array(chunk)
             rc = lib.tdq_adam_multi(ctypes.cast(arr, ctypes.c_void_p), len(chunk),
                                     _lib.ptr(snap[1]) if snap else None, _lib.ptr(snap[0]) if snap else None,
                                     _lib.stream_ptr(flat[0][0].device))

@@ -48,11 +48,13 @@ def _lo_args(cfg):
     return ()
 
 
-def forward_raw(X, P, net, plan, precision=None):
+def forward_raw(X, P, net, plan, precision=None, pack=True):
     """Autograd-free forward: returns ``(J, saved)`` where ``saved`` feeds :func:`backward_raw`.
 
     ``precision``: ``"bf16x3"`` / ``"bf16"`` (csrc/jet_bf3.hip, saves post-activations) or ``"fp32"``
-    (csrc/jet_mlp.hip, saves pre-activations); the saved buffer only fits its own backward."""
+    (csrc/jet_mlp.hip, saves pre-activations); the saved buffer only fits its own backward.
+    ``pack=False`` (split-bf16 only): the weight images inside the scratch are already current
+    (a captured Adam step whose fused tail rewrote them, see :func:`step_tail`)."""
     lib = _lib.load()
     cfg = hip_config(net, plan, precision)
     fwd, _, scratch_floats, _ = _fns(lib, cfg)
@@ -66,14 +68,21 @@ def forward_raw(X, P, net, plan, precision=None):
     if nscr < 0:
         raise ValueError(f"jet kernels cannot serve {cfg}")
     scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
-    rc = fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
-                         cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
+    if not pack and cfg["precision"] in ("bf16x3", "bf16"):
+        rc = lib.tdq_jet_fwd_bf3_ex(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
+                                    cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), 0,
+                                    _lib.stream_ptr(X.device))
+    else:
+        rc = fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
+                 cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
     _lib.check(rc, f"tdq_jet_fwd[{cfg['precision']}]")
     return J, (X, P, scratch, cfg, spec, S)
 
 
-def backward_raw(saved, dJ):
-    """Flat parameter gradient for the adjoint ``dJ`` of the jet."""
+def backward_raw(saved, dJ, reduce=True):
+    """Flat parameter gradient for the adjoint ``dJ`` of the jet.  ``reduce=False`` (split-bf16
+    only): launch only the backward kernel and return ``(grad, work)`` - the per-workgroup
+    gradient slabs in ``work`` are reduced into ``grad`` later by :func:`step_tail`."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     _, bwd, _, slab_floats = _fns(lib, cfg)
@@ -83,11 +92,54 @@ def backward_raw(saved, dJ):
     work = torch.empty(max(int(nwork), 1), dtype=torch.float32, device=X.device)
     grad = torch.empty_like(P)
     spec_c = (ctypes.c_int * len(spec))(*spec)
+    if not reduce:
+        if not is_split_bf16(cfg):
+            raise ValueError("backward_raw(reduce=False) needs a split-bf16 precision")
+        rc = lib.tdq_jet_bwd_bf3_ex(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
+                                    _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"],
+                                    S, spec_c, *_lo_args(cfg), 0, _lib.stream_ptr(X.device))
+        _lib.check(rc, f"tdq_jet_bwd_bf3_ex[{cfg['precision']}]")
+        return grad, work
     rc = bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
                          _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S,
                          spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
     _lib.check(rc, f"tdq_jet_bwd[{cfg['precision']}]")
     return grad
+
+
+def is_split_bf16(cfg):
+    return cfg["precision"] in ("bf16x3", "bf16")
+
+
+def pack_images(saved):
+    """Re-pack the weight images of a forward scratch from the current parameters (one launch)."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    rc = lib.tdq_jet_bf3_pack(_lib.ptr(P), _lib.ptr(scratch), X.shape[0], cfg["d_in"], cfg["width"],
+                              cfg["d_out"], cfg["n_hidden"], S, _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_jet_bf3_pack")
+
+
+def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, snapshot, write_images=True):
+    """End of a single-process Adam step in two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``):
+    slab reduction + loss reduction + bookkeeping, then the reduced gradient fused into Adam
+    (theta, SA weights), the best-weights snapshot and - ``write_images`` - the next step's
+    weight images.  ``book``: the engine's device state dict; ``group_array``: ctypes array of
+    ``fused._Group`` with theta first."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    hist = book["hist"]
+    carr = (ctypes.c_void_p * max(1, len(counters)))(*[c.data_ptr() for c in counters])
+    rc = lib.tdq_step_tail_bf3(
+        _lib.ptr(work), _lib.ptr(grad), _lib.ptr(scratch) if write_images else None,
+        X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S, *_lo_args(cfg),
+        _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms, fop.n_scal,
+        _lib.ptr(fop.losses), _lib.ptr(fop.total), _lib.ptr(fop.dscal),
+        _lib.ptr(hist), int(hist.shape[0]), _lib.ptr(book["epoch"]), _lib.ptr(book["best_loss"]),
+        _lib.ptr(book["best_epoch"]), _lib.ptr(book["improved"]), ctypes.cast(carr, ctypes.c_void_p), len(counters),
+        ctypes.cast(group_array, ctypes.c_void_p), n_groups,
+        _lib.ptr(snapshot) if snapshot is not None else None, _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_step_tail_bf3")
 
 
 class JetMLPFunction(torch.autograd.Function):

@@ -328,3 +328,64 @@ def test_step_book_and_adam_snapshot_match_torch():
     for x, y in zip(a[3], b[3]):
         assert torch.allclose(x.cpu(), y, rtol=1e-5, atol=1e-6)
     assert torch.allclose(a[2].cpu(), b[2], rtol=1e-5, atol=1e-6)
+
+
+def _ac_sa_model(prec, n_f=3000):
+    import math
+    import numpy as np
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.boundaries import DomainND, IC, periodicBC
+    tdq.set_seed(0)
+    D = DomainND(["x", "t"], time_var="t")
+    D.add("x", [-1.0, 1.0], 512)
+    D.add("t", [0.0, 1.0], 201)
+    D.generate_collocation_points(n_f)
+
+    def deriv_model(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        return u, tdq.grad(u, x)
+
+    def f_model(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        u_xx = tdq.grad(tdq.grad(u, x), x)
+        return tdq.grad(u, t) - 0.0001 * u_xx + 5.0 * u ** 3 - 5.0 * u
+
+    m = tdq.CollocationSolverND(verbose=False)
+    g = torch.Generator().manual_seed(1)
+    m.compile([2, 128, 128, 128, 128, 1], f_model, D,
+              [IC(D, [lambda x: x ** 2 * np.cos(math.pi * x)], var=[["x"]]), periodicBC(D, ["x"], [deriv_model])],
+              Adaptive_type="self-adaptive", dict_adaptive={"residual": [True], "BCs": [True, False]},
+              init_weights={"residual": [torch.rand(n_f, 1, generator=g)],
+                            "BCs": [100 * torch.rand(512, 1, generator=g), None]},
+              backend="hip", device="cuda", precision=prec)
+    return m
+
+
+@pytest.mark.parametrize("prec", ["bf16", "bf16x3"])
+def test_fused_step_tail_matches_unfused(prec, monkeypatch):
+    """The two-launch step tail (slab + loss reduction + bookkeeping, then reduction fused into
+    Adam with the weight images rewritten in place) reproduces the seven-launch step bit for bit:
+    parameters, SA weights, loss history, best loss / epoch / weights - across two fit() calls
+    with the parameters changed in between (the images are re-packed before the first replay)."""
+    def run(fused_tail):
+        monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
+        m = _ac_sa_model(prec)
+        m.fit(tf_iter=25)
+        with torch.no_grad():
+            m.u_model.flat.mul_(0.97)
+        m.fit(tf_iter=15)
+        return m
+
+    a = run(True)
+    b = run(False)
+    assert torch.equal(a.u_model.flat, b.u_model.flat)
+    for x, y in zip(a.lambdas, b.lambdas):
+        assert torch.equal(x, y)
+    la = [r["Total Loss"] for r in a.losses]
+    lb = [r["Total Loss"] for r in b.losses]
+    assert la == lb and len(la) == 40
+    assert a.min_loss["adam"] == b.min_loss["adam"] and a.best_epoch["adam"] == b.best_epoch["adam"]
+    X = torch.rand(300, 2, generator=torch.Generator().manual_seed(3)).numpy()
+    u1, _ = a.predict(X, best_model=True)
+    u2, _ = b.predict(X, best_model=True)
+    assert (u1 == u2).all()
