@@ -126,9 +126,19 @@ __global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restri
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0 && tb.hist != nullptr)  // DP: the bookkeeping waits for the all-reduce
     step_book_body(tb.total, tb.losses, tb.n_terms, 1, tb.hist, tb.hist_rows, tb.epoch, tb.best_loss, tb.best_epoch,
                    tb.improved, tb.cnt);
+}
+
+__global__ void __launch_bounds__(256) slab_reduce2_bf3(const float* __restrict__ part, float* __restrict__ grad, int P,
+                                                        int Pst, int chunks) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (4 * q >= P) return;
+  const f32x4 a = slab_reduce2_sum(part, Pst, chunks, q);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (4 * q + e < P) grad[4 * q + e] = a[e];
 }
 
 struct TailImg {
@@ -187,6 +197,49 @@ __device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti)
   }
 }
 
+#ifndef TDQ_TAIL_ELEM
+#define TDQ_TAIL_ELEM 1
+#endif
+
+#if TDQ_TAIL_ELEM
+// Adam over every group, one ELEMENT per thread (args.start in elements); group 0 = theta, whose
+// gradient is the second slab pass of its column (the f32x4 pass's summation order, so the
+// result is bit-identical), written to args.grp[0].g as well
+__global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const float* __restrict__ part, int Pst,
+                                                        int chunks, const int* __restrict__ improved,
+                                                        float* __restrict__ snap, TailImg ti) {
+  const bool do_snap = snap != nullptr && *improved != 0;
+  const int64_t total = args.start[args.ngroups];
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int gi = adam_group_of(args, idx);
+    const AdamGroup gr = args.grp[gi];
+    const int64_t e = idx - args.start[gi];
+    const bool th = gi == 0;
+    float g;
+    if (th && part != nullptr) {
+      float a0 = 0.f, a1 = 0.f;
+      int c = 0;
+      for (; c + 1 < chunks; c += 2) {
+        a0 += part[(size_t)c * Pst + e];
+        a1 += part[(size_t)(c + 1) * Pst + e];
+      }
+      if (c < chunks) a0 += part[(size_t)c * Pst + e];
+      g = a0 + a1;
+      const_cast<float*>(gr.g)[e] = g;
+    } else {
+      g = gr.g[e];
+    }
+    float p = gr.p[e], m = gr.m[e], v = gr.v[e];
+    if (do_snap && th) snap[e] = p;
+    adam_elem(p, gr.sign * g, m, v, gr.b1, gr.b2, gr.eps, adam_lr_t(gr));
+    gr.p[e] = p;
+    gr.m[e] = m;
+    gr.v[e] = v;
+    if (th && ti.fimg != nullptr) scatter_param(p, (int)e, ti);
+  }
+}
+#else
+// (TDQ_TAIL_ELEM=0: float4 slots per thread, measured ~2 us slower per step: profiles/r2_v10_ab_tail_elem.jsonl)
 // Adam over every group; group 0 = theta, whose gradient is the second slab pass of its float4
 // column (slot == column), written to args.grp[0].g as well
 __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const float* __restrict__ part, int Pst,
@@ -202,13 +255,14 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
     const float lr_t = adam_lr_t(gr);
     const bool th = gi == 0;
     float* gout = const_cast<float*>(gr.g);
+    const bool red = th && part != nullptr;  // theta gradient from the slab partials (else: gr.g)
     f32x4 g = zero4();
-    if (th) g = slab_reduce2_sum(part, Pst, chunks, (int)slot);
+    if (red) g = slab_reduce2_sum(part, Pst, chunks, (int)slot);
     const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
     if (aligned && e0 + 4 <= gr.n) {
       f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
       if (do_snap && th) *reinterpret_cast<f32x4*>(snap + e0) = p;
-      if (th) *reinterpret_cast<f32x4*>(gout + e0) = g;
+      if (red) *reinterpret_cast<f32x4*>(gout + e0) = g;
       else g = *reinterpret_cast<const f32x4*>(gr.g + e0);
       f32x4 m = *reinterpret_cast<const f32x4*>(gr.m + e0);
       f32x4 v = *reinterpret_cast<const f32x4*>(gr.v + e0);
@@ -231,7 +285,7 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
         if (e < gr.n) {
           if (do_snap && th) snap[e] = gr.p[e];
           float gc;
-          if (th) {
+          if (red) {
             gc = g[c];
             gout[e] = gc;
           } else {
@@ -244,6 +298,7 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
     }
   }
 }
+#endif
 
 namespace {
 
@@ -394,7 +449,8 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
       n_terms < 0 || n_scal < 0)
     return (int)hipErrorInvalidValue;
   AdamArgs args;
-  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups)) return (int)hipErrorInvalidValue;
+  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, TDQ_TAIL_ELEM != 0))
+    return (int)hipErrorInvalidValue;
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
   args.grp[0].g = grad;
@@ -436,6 +492,63 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(tail_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, args, part, Pst, chunks, improved,
                      snap, ti);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// Data-parallel step, first half (before the all-reduce): slab pass 1 + the loss reduction in one
+// launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad.
+int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int d_out, int n_hidden, int lo,
+                      const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
+                      void* stream) {
+  const int WT = width_tiles(width);
+  if (WT < 2 || n_lblocks < 0 || n_terms < 0 || n_scal < 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int Ptot = param_count(d_in, width, d_out, n_hidden);
+  const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;
+  const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
+  float* part = work + (size_t)nwg_b * Pst;
+  TailBook tb{};
+  tb.lpart = lpart;
+  tb.n_lblocks = n_lblocks;
+  tb.n_terms = n_terms;
+  tb.n_scal = n_scal;
+  tb.losses = losses;
+  tb.dscal = dscal;
+  const int nqb = (Pst / 4 + 255) / 256;
+  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
+                     nqb, tb);
+  TDQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nqb), dim3(256), 0, st, part, grad, Ptot, Pst, chunks);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// Data-parallel step, second half (after the all-reduce and tdq_step_book): Adam over every group
+// with theta's gradient read from groups[0].g (the all-reduced bucket), the best-weights snapshot
+// and the next step's weight images written into the forward scratch.
+int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, int width, int d_out, int n_hidden, int S,
+                      const void* groups, int ngroups, const int* improved, float* snap, void* stream) {
+  const int WT = width_tiles(width);
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  AdamArgs args;
+  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, TDQ_TAIL_ELEM != 0))
+    return (int)hipErrorInvalidValue;
+  if (args.grp[0].n != param_count(d_in, width, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  TailImg ti{nullptr, nullptr, nullptr, NetDims{d_in, width, d_out, n_hidden}, WT};
+  if (scratch != nullptr) {
+    float *img, *bimg, *aux;
+    scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+    ti.fimg = reinterpret_cast<__bf16*>(img);
+    ti.bimg = reinterpret_cast<__bf16*>(bimg);
+    ti.aux = aux;
+  }
+  const int64_t tot = args.start[ngroups];
+  int64_t blocks = (tot + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(tail_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     args, nullptr, 0, 0, improved, snap, ti);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

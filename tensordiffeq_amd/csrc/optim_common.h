@@ -54,15 +54,16 @@ __device__ __forceinline__ int adam_group_of(const AdamArgs& args, int64_t slot)
   return gi;
 }
 
-// host: fill the argument block (prefix sums of float4 slots); false on a bad group count
-static inline bool adam_args_fill(AdamArgs& args, const AdamGroup* src, int ngroups) {
+// host: fill the argument block (prefix sums of float4 slots, or of elements with per_elem);
+// false on a bad group count
+static inline bool adam_args_fill(AdamArgs& args, const AdamGroup* src, int ngroups, bool per_elem = false) {
   if (ngroups <= 0 || ngroups > TDQ_MAX_GROUPS) return false;
   args.ngroups = ngroups;
   args.start[0] = 0;
   for (int i = 0; i < TDQ_MAX_GROUPS; ++i) {
     if (i < ngroups) {
       args.grp[i] = src[i];
-      args.start[i + 1] = args.start[i] + (src[i].n + 3) / 4;
+      args.start[i + 1] = args.start[i] + (per_elem ? src[i].n : (src[i].n + 3) / 4);
     } else {
       args.grp[i] = AdamGroup{nullptr, nullptr, nullptr, nullptr, 0, 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, nullptr};
       args.start[i + 1] = args.start[i];

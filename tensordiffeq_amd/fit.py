@@ -237,13 +237,14 @@ class AdamEngine:
 
     # ------------------------------------------------------------ fused step tail ------
     def _tail_eligible(self):
-        """Single-process step on the split-bf16 jet kernels with the fused loss: the end of the
-        step runs as two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``)."""
+        """Step on the split-bf16 jet kernels with the fused loss: single-process, the end of the
+        step runs as two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``); under DP the captured
+        halves use ``tdq_dp_tail_a_bf3`` / ``tdq_dp_tail_b_bf3`` around the all-reduce."""
         if getattr(self, "_tail_ok", None) is not None:
             return self._tail_ok
         ok = False
         fop = getattr(self.program, "fused_op", None)
-        if (os.environ.get("TDQ_FUSED_TAIL", "1") != "0" and fop is not None and not self.dist.is_distributed
+        if (os.environ.get("TDQ_FUSED_TAIL", "1") != "0" and fop is not None
                 and self.device.type == "cuda" and self.groups[0].tensors[0] is self.flat):
             from .ops import _lib, jet_hip
             from .ops.jet_mlp import hip_config
@@ -282,8 +283,33 @@ class AdamEngine:
         self._tail_saved = saved
         return fop.total
 
+    def _dp_tail_phase_a(self):
+        """DP graph half before the all-reduce (fused-tail kernels; see :meth:`_tail_eligible`)."""
+        from .ops import jet_hip
+        prog = self.program
+        fop = prog.fused_op
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision, pack=False)
+        fop(J, with_total=False, reduce=False)
+        grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
+        jet_hip.dp_tail_a(saved, work, grad, fop)
+        self._sum_terms = True
+        self._tail_saved = saved
+        return fop.total, self._fused_grads(fop, grad, fop.dlam, fop.dscal), fop.losses
+
+    def _dp_tail_phase_b(self, loss, grads, terms):
+        """DP graph half after the all-reduce: bookkeeping, then Adam + snapshot + weight images."""
+        from .ops import jet_hip
+        st = self.state
+        self._book(loss, terms)
+        if st["best_flat"].numel() != self.flat.numel():
+            raise ValueError(f"best-weights snapshot has {st['best_flat'].numel()} elements, parameters "
+                             f"{self.flat.numel()}")
+        arr, n = fused.group_array(self._opt_groups(grads))
+        jet_hip.dp_tail_b(self._tail_saved, arr, n, st["improved"], st["best_flat"])
+        return loss
+
     def _eager_step(self):
-        if self._tail_eligible():
+        if not self.dist.is_distributed and self._tail_eligible():
             return self._tail_step(in_graph=False)
         loss, grads, terms = self._phase_a(for_step=True)
         loss, grads, terms = self._reduce(loss, grads, terms)
@@ -311,9 +337,10 @@ class AdamEngine:
             if tail:
                 self._graph_saved = self._tail_saved
         else:
+            tail = self._tail_eligible()
             ga = torch.cuda.CUDAGraph()
             with capture_graph(ga, pool=pool):
-                loss, grads, terms = self._phase_a(for_step=True)
+                loss, grads, terms = self._dp_tail_phase_a() if tail else self._phase_a(for_step=True)
                 red_idx = self.red_idx
                 red = [grads[i] for i in red_idx]
                 terms = _term_list(terms)
@@ -327,8 +354,10 @@ class AdamEngine:
                 grads = list(self._grads_static)
                 for i, gg in zip(self._red_idx, red_out):
                     grads[i] = gg.view_as(grads[i])
-                self.static_loss = self._phase_b(scal[0], grads, scal[1:])
+                self.static_loss = (self._dp_tail_phase_b if tail else self._phase_b)(scal[0], grads, scal[1:])
             self.graph_a, self.graph_b = ga, gb
+            if tail:
+                self._graph_saved = self._tail_saved
         return warm
 
     def _replay(self):

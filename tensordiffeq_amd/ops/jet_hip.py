@@ -157,3 +157,26 @@ class JetMLPFunction(torch.autograd.Function):
         if dJ is None:
             dJ = torch.zeros((S, X.shape[0], cfg["d_out"]), device=X.device)
         return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None
+
+
+def dp_tail_a(saved, work, grad, fop):
+    """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
+    slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``)."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
+                               cfg["n_hidden"], *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
+                               fop.n_scal, _lib.ptr(fop.losses), _lib.ptr(fop.dscal), _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_dp_tail_a_bf3")
+
+
+def dp_tail_b(saved, group_array, n_groups, improved, snapshot):
+    """Data-parallel step after the all-reduce and the bookkeeping: Adam over every group (theta's
+    gradient = the all-reduced bucket slice in ``group_array[0].g``), best-weights snapshot and the
+    next step's weight images (``tdq_dp_tail_b_bf3``)."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    rc = lib.tdq_dp_tail_b_bf3(_lib.ptr(scratch), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
+                               cfg["n_hidden"], S, ctypes.cast(group_array, ctypes.c_void_p), n_groups,
+                               _lib.ptr(improved), _lib.ptr(snapshot), _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_dp_tail_b_bf3")
