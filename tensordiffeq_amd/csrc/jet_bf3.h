@@ -373,6 +373,20 @@ __device__ __forceinline__ void slab_store(float* p, float v) {
 #endif
 }
 
+// Precision "bf16" (!LO) writes its per-workgroup gradient slabs as bf16 (RNE): half the slab
+// bytes written by the backward and re-read by the reduction.  Each entry is a 128-point partial
+// sum; the reduction adds the rows in fp32, so the rounding adds ~2^-9 relative error per partial,
+// below the bf16 GEMM operands' own (kernel gradient error vs fp64: profiles/r2_v12_*).
+// -DTDQ_SLAB_BF16=0 keeps fp32 slabs (A/B); bf16x3 always uses fp32.
+#ifndef TDQ_SLAB_BF16
+#define TDQ_SLAB_BF16 1
+#endif
+__host__ __device__ constexpr bool slab_half(bool lo) { return TDQ_SLAB_BF16 && !lo; }
+template <bool H> struct SlabType { using T = float; };
+template <> struct SlabType<true> { using T = __bf16; };
+__device__ __forceinline__ void slab_put(float* p, float v) { slab_store(p, v); }
+__device__ __forceinline__ void slab_put(__bf16* p, float v) { *p = (__bf16)v; }
+
 // layer 0 (input -> width, VALU; derivative streams are rows of K0): the post-activation streams of
 // feature tile t (forward).
 template <int WT, int S, int NSO>
@@ -789,7 +803,9 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const int nc = valid ? n : N - 1;
   const float vmask = valid ? 1.f : 0.f;  // zero adjoints for padding points: zb = 0 downstream
   const int Lh = d.n_hidden;
-  float* gs = slab + (size_t)wg * Ptot;
+  constexpr bool SH = slab_half(LO);
+  using ST = typename SlabType<SH>::T;
+  ST* gs = reinterpret_cast<ST*>(slab) + (size_t)wg * Ptot;
   bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * HL * 64 * 2);
   auto dw_row = [](int wv, int r) { return NR * (wv >> 1) + r; };
   auto dw_col = [](int wv, int c) { return NC * (wv & 1) + c; };
@@ -895,13 +911,13 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       float a = accKo[k];
 #pragma unroll
       for (int v = 1; v < NWV; ++v) a += accKo[v * st + k];
-      gs[ko + e] = a;
+      slab_put(gs + ko + e, a);
     }
     if (l < d.d_out) {
       float a = accBo[l];
 #pragma unroll
       for (int v = 1; v < NWV; ++v) a += accBo[v * TDQ_MAXO + l];
-      gs[ko + d.width * d.d_out + l] = a;
+      slab_put(gs + ko + d.width * d.d_out + l, a);
     }
   }
   TDQ_TS(1);
@@ -938,7 +954,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
           float a = accBi[f];
 #pragma unroll
           for (int v = 1; v < NWV; ++v) a += accBi[v * W + f];
-          gs[bo + f] = a;
+          slab_put(gs + bo + f, a);
         }
       }
       {
@@ -1001,10 +1017,11 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       // opaque per iteration: otherwise LICM hoists the padded path's 64 guarded store addresses
       // (and their exec masks) out of the layer loop, where they stay live and spill
       asm volatile("" : "+v"(in0), "+v"(out0));
-      float* gk = gs + off_layer(d, i);
+      ST* gk = gs + off_layer(d, i);
       if (d.width == W) {
         const Tl G = tl_make(gk, 0);
-        const int voff = (in0 * W + out0) * 4;
+        constexpr int EB = (int)sizeof(ST);  // slab entry bytes
+        const int voff = (in0 * W + out0) * EB;
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -1012,7 +1029,11 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const float v = dw[r][c2][c];
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), G.r, voff, ((16 * r + c) * W + 16 * c2) * 4, 0);
+              if constexpr (SH)
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)v), G.r, voff,
+                                                      ((16 * r + c) * W + 16 * c2) * EB, 0);
+              else
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), G.r, voff, ((16 * r + c) * W + 16 * c2) * 4, 0);
             }
       } else {
 #pragma unroll
@@ -1022,7 +1043,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const int in = in0 + 16 * r + c, out = out0 + 16 * c2;
-              if (in < d.width && out < d.width) slab_store(gk + in * d.width + out, dw[r][c2][c]);
+              if (in < d.width && out < d.width) slab_put(gk + in * d.width + out, dw[r][c2][c]);
             }
       }
     }
@@ -1058,7 +1079,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       float a = accB0[f];
 #pragma unroll
       for (int v = 1; v < NWV; ++v) a += accB0[v * W + f];
-      gs[bo + f] = a;
+      slab_put(gs + bo + f, a);
     }
   } else if (w == 1) {
     for (int e = l; e < d.d_in * d.width; e += 64) {
@@ -1067,7 +1088,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       float a = accK0[k];
 #pragma unroll
       for (int v = 1; v < NWV; ++v) a += accK0[v * TDQ_MAXD * W + k];
-      gs[e] = a;
+      slab_put(gs + e, a);
     }
   }
   TDQ_TS(63);

@@ -100,10 +100,13 @@ struct TailBook {
 };
 
 __global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restrict__ slab, float* __restrict__ part,
-                                                           int nwg, int Pst, int chunks, int nqb, TailBook tb) {
+                                                           int nwg, int Pst, int chunks, int nqb, int half, TailBook tb) {
   if ((int)blockIdx.x < nqb) {
     const int q = blockIdx.x * 256 + threadIdx.x;
-    if (4 * q < Pst) slab_reduce1_body(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+    if (4 * q < Pst) {
+      if (half) slab_reduce1_body<true>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+      else slab_reduce1_body<false>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+    }
     return;
   }
   if (blockIdx.y != 0) return;
@@ -426,7 +429,7 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
             slab_stride(Ptot), d, sp, st, lo};
   int rc = dispatch(false, WT, S, nso, a);
   if (rc || !reduce) return rc;
-  return tdq_slab_reduce(work, grad, nwg_b, Ptot, chunks, stream);
+  return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, chunks, (int)slab_half(lo != 0), stream);
 }
 
 int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
@@ -476,7 +479,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   for (int i = 0; i < TDQ_MAX_COUNTERS; ++i) tb.cnt.c[i] = i < ncnt ? counters[i] : nullptr;
   const int nqb = (Pst / 4 + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
-                     nqb, tb);
+                     nqb, (int)slab_half(lo != 0), tb);
   TDQ_CHECK_LAUNCH();
   TailImg ti{nullptr, nullptr, nullptr, NetDims{d_in, width, d_out, n_hidden}, WT};
   if (scratch != nullptr) {
@@ -517,7 +520,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int 
   tb.dscal = dscal;
   const int nqb = (Pst / 4 + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
-                     nqb, tb);
+                     nqb, (int)slab_half(lo != 0), tb);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nqb), dim3(256), 0, st, part, grad, Ptot, Pst, chunks);
   TDQ_CHECK_LAUNCH();

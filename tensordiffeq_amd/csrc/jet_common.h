@@ -87,21 +87,34 @@ static inline int slab_stride(int P) { return (P + 3) & ~3; }
 // workgroup-chunk count of the first reduction pass
 static inline int slab_chunks(int nwg) { return nwg < 16 ? nwg : 16; }
 
+// four consecutive slab entries (float4 column q of row `row`) as fp32; H: the slab holds bf16
+template <bool H>
+__device__ __forceinline__ f32x4 slab_ld4(const void* __restrict__ slab, size_t row, int Pst, int q) {
+  if constexpr (H) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(slab) + row * Pst + 4 * q);
+    return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                 __uint_as_float(u.y & 0xffff0000u)};
+  } else {
+    return reinterpret_cast<const f32x4*>(slab)[row * (size_t)(Pst >> 2) + q];
+  }
+}
+
 // first reduction pass, float4 column q of chunk c: part[c][q] = sum of slab rows of the chunk
-__device__ __forceinline__ void slab_reduce1_body(const float* __restrict__ slab, float* __restrict__ part, int nwg,
+// (fp32 partials; H: bf16 slab rows)
+template <bool H = false>
+__device__ __forceinline__ void slab_reduce1_body(const void* __restrict__ slab, float* __restrict__ part, int nwg,
                                                   int Pst, int chunks, int q, int c) {
   const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
-  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab) + q;
   const size_t row = (size_t)(Pst >> 2);
   f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();
   int wgi = lo;
   for (; wgi + 3 < hi; wgi += 4) {
-    a0 += s4[(size_t)wgi * row];
-    a1 += s4[(size_t)(wgi + 1) * row];
-    a2 += s4[(size_t)(wgi + 2) * row];
-    a3 += s4[(size_t)(wgi + 3) * row];
+    a0 += slab_ld4<H>(slab, wgi, Pst, q);
+    a1 += slab_ld4<H>(slab, wgi + 1, Pst, q);
+    a2 += slab_ld4<H>(slab, wgi + 2, Pst, q);
+    a3 += slab_ld4<H>(slab, wgi + 3, Pst, q);
   }
-  for (; wgi < hi; ++wgi) a0 += s4[(size_t)wgi * row];
+  for (; wgi < hi; ++wgi) a0 += slab_ld4<H>(slab, wgi, Pst, q);
   reinterpret_cast<f32x4*>(part)[(size_t)c * row + q] = (a0 + a1) + (a2 + a3);
 }
 
@@ -121,3 +134,5 @@ __device__ __forceinline__ f32x4 slab_reduce2_sum(const float* __restrict__ part
 
 // slabs [nwg][slab_stride(P)] at work, partials [chunks][slab_stride(P)] right after -> grad[P]
 extern "C" int tdq_slab_reduce(float* work, float* grad, int nwg, int P, int chunks, void* stream);
+// the same for bf16 slab rows when half != 0 (partials stay fp32, right after nwg fp32-sized rows)
+extern "C" int tdq_slab_reduce_h(float* work, float* grad, int nwg, int P, int chunks, int half, void* stream);

@@ -595,11 +595,12 @@ jet_bwd_kernel(const float* __restrict__ X, const float* __restrict__ P, const f
 
 // deterministic slab reduction (fixed summation order): pass 1 sums chunks of workgroups, one
 // float4 column per thread with four independent 16-byte loads in flight; pass 2 sums the chunks
+template <bool H>
 __global__ void __launch_bounds__(256) slab_reduce1(const float* __restrict__ slab, float* __restrict__ part,
                                                     int nwg, int Pst, int chunks) {
   const int q = blockIdx.x * 256 + threadIdx.x;  // float4 column
   if (4 * q >= Pst) return;
-  slab_reduce1_body(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+  slab_reduce1_body<H>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
 }
 
 __global__ void __launch_bounds__(256) slab_reduce2(const float* __restrict__ part, float* __restrict__ grad, int P,
@@ -770,13 +771,20 @@ int tdq_jet_bwd(const float* X, const float* P, const float* dJ, const float* Zs
 }
 
 int tdq_slab_reduce(float* work, float* grad, int nwg, int P, int chunks, void* stream) {
+  return tdq_slab_reduce_h(work, grad, nwg, P, chunks, 0, stream);
+}
+
+int tdq_slab_reduce_h(float* work, float* grad, int nwg, int P, int chunks, int half, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Pst = slab_stride(P);
   const int nq = Pst / 4;
   float* slab = work;
   float* part = work + (size_t)nwg * Pst;
   dim3 g1((nq + 255) / 256, chunks);
-  hipLaunchKernelGGL(slab_reduce1, g1, dim3(256), 0, st, slab, part, nwg, Pst, chunks);
+  if (half)
+    hipLaunchKernelGGL(slab_reduce1<true>, g1, dim3(256), 0, st, slab, part, nwg, Pst, chunks);
+  else
+    hipLaunchKernelGGL(slab_reduce1<false>, g1, dim3(256), 0, st, slab, part, nwg, Pst, chunks);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(slab_reduce2, dim3((nq + 255) / 256), dim3(256), 0, st, part, grad, P, Pst, chunks);
   TDQ_CHECK_LAUNCH();
