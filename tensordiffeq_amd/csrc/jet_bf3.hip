@@ -129,6 +129,11 @@ __global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restri
     }
     __syncthreads();
   }
+  if (threadIdx.x == 0 && tb.hist == nullptr && tb.total != nullptr) {  // loss + gradient only (L-BFGS)
+    float s = 0.f;
+    for (int t = 0; t < tb.n_terms; ++t) s += tb.losses[t];
+    *tb.total = s;
+  }
   if (threadIdx.x == 0 && tb.hist != nullptr)  // DP: the bookkeeping waits for the all-reduce
     step_book_body(tb.total, tb.losses, tb.n_terms, 1, tb.hist, tb.hist_rows, tb.epoch, tb.best_loss, tb.best_epoch,
                    tb.improved, tb.cnt);
@@ -500,10 +505,11 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
 }
 
 // Data-parallel step, first half (before the all-reduce): slab pass 1 + the loss reduction in one
-// launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad.
+// launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad.  total
+// (optional): also the summed loss - the L-BFGS objective writes [grad | loss] in place this way.
 int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int d_out, int n_hidden, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
-                      void* stream) {
+                      float* total, void* stream) {
   const int WT = width_tiles(width);
   if (WT < 2 || n_lblocks < 0 || n_terms < 0 || n_scal < 0) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -518,6 +524,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int 
   tb.n_scal = n_scal;
   tb.losses = losses;
   tb.dscal = dscal;
+  tb.total = total;
   const int nqb = (Pst / 4 + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
                      nqb, (int)slab_half(lo != 0), tb);

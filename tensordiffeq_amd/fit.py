@@ -415,12 +415,36 @@ class LossGradEngine:
         self.graph = None
         self.n_evals = 0
 
+    def _fused_tail(self):
+        """Split-bf16 kernels with the fused loss on a GPU: ``[grad | loss]`` is written in place
+        by the fused tail (slab pass 1 + loss reduction + total in one launch, slab pass 2 into the
+        buffer) instead of loss-reduce / total / slab / concatenate launches."""
+        ok = getattr(self, "_tail", None)
+        if ok is None:
+            ok = False
+            if os.environ.get("TDQ_FUSED_TAIL", "1") != "0" and self.flat.is_cuda:
+                from .ops import _lib, jet_hip
+                from .ops.jet_mlp import hip_config
+                prog = self.program
+                try:
+                    ok = jet_hip.is_split_bf16(hip_config(prog.net, prog.plan, prog.precision)) and _lib.available()
+                except (ValueError, AttributeError):
+                    ok = False
+            self._tail = ok
+        return ok
+
     def _body(self):
         fop = getattr(self.program, "fused_op", None)
         if fop is not None:
             from .ops import jet_hip
             prog = self.program
             J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+            if self._fused_tail():
+                fop(J, with_total=False, reduce=False)
+                fg = torch.empty(self.flat.numel() + 1, dtype=torch.float32, device=self.flat.device)
+                grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=fg[:-1])
+                jet_hip.dp_tail_a(saved, work, grad, fop, total=fg[-1:])
+                return fg
             total, _, dJ, _, _ = fop(J)
             g = jet_hip.backward_raw(saved, dJ)
             return torch.cat([g.reshape(-1), total.reshape(1)])

@@ -79,7 +79,7 @@ def forward_raw(X, P, net, plan, precision=None, pack=True):
     return J, (X, P, scratch, cfg, spec, S)
 
 
-def backward_raw(saved, dJ, reduce=True):
+def backward_raw(saved, dJ, reduce=True, grad=None):
     """Flat parameter gradient for the adjoint ``dJ`` of the jet.  ``reduce=False`` (split-bf16
     only): launch only the backward kernel and return ``(grad, work)`` - the per-workgroup
     gradient slabs in ``work`` are reduced into ``grad`` later by :func:`step_tail`."""
@@ -90,7 +90,8 @@ def backward_raw(saved, dJ, reduce=True):
     dJ = dJ.contiguous()
     nwork = slab_floats(N)
     work = torch.empty(max(int(nwork), 1), dtype=torch.float32, device=X.device)
-    grad = torch.empty_like(P)
+    if grad is None:
+        grad = torch.empty_like(P)
     spec_c = (ctypes.c_int * len(spec))(*spec)
     if not reduce:
         if not is_split_bf16(cfg):
@@ -159,14 +160,16 @@ class JetMLPFunction(torch.autograd.Function):
         return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None
 
 
-def dp_tail_a(saved, work, grad, fop):
+def dp_tail_a(saved, work, grad, fop, total=None):
     """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
-    slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``)."""
+    slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``).  ``total`` (a 1-element
+    view): also write the summed loss there."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
                                cfg["n_hidden"], *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
-                               fop.n_scal, _lib.ptr(fop.losses), _lib.ptr(fop.dscal), _lib.stream_ptr(X.device))
+                               fop.n_scal, _lib.ptr(fop.losses), _lib.ptr(fop.dscal), _lib.ptr(total),
+                               _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")
 
 

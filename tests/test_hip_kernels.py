@@ -389,3 +389,24 @@ def test_fused_step_tail_matches_unfused(prec, monkeypatch):
     u1, _ = a.predict(X, best_model=True)
     u2, _ = b.predict(X, best_model=True)
     assert (u1 == u2).all()
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+def test_fused_lbfgs_objective_matches_unfused(prec, monkeypatch):
+    """The L-BFGS objective writing ``[grad | loss]`` in place through the fused tail gives the same
+    device L-BFGS trajectory, bit for bit, as the loss-reduce / total / slab / concatenate path."""
+    def run(fused_tail):
+        monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
+        m = _ac_sa_model(prec)
+        m.fit(tf_iter=5, newton_iter=30)
+        return m
+
+    a = run(True)
+    b = run(False)
+    assert torch.equal(a.u_model.flat, b.u_model.flat)
+    assert a.min_loss["l-bfgs"] == b.min_loss["l-bfgs"] and np_isfinite(a.min_loss["l-bfgs"])
+
+
+def np_isfinite(v):
+    import math
+    return math.isfinite(float(v))
