@@ -79,8 +79,11 @@ def gradients(ys, xs):
 
 
 def _autograd(y, x):
-    g = torch.autograd.grad(y, x, grad_outputs=torch.ones_like(y), create_graph=True,
-                            allow_unused=True)[0]
+    # d(sum y)/dx == the VJP with ones (each point's outputs depend on its own coordinates only).
+    # A scalar output also keeps torch.autograd.grad off its grad_outputs check, whose first call
+    # imports torch.fx.experimental.symbolic_shapes (sympy): ~0.8 s of every program build on the
+    # GPU box (tools/prof_program.py).
+    g = torch.autograd.grad(y.sum(), x, create_graph=True, allow_unused=True)[0]
     if g is None:
         g = torch.zeros_like(x)
     return g
