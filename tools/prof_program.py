@@ -1,3 +1,5 @@
+"""cProfile of CollocationSolverND.program() (trace + plan + fused-loss build) for the AC-SA example
+(run from the repo root on the GPU box): python tools/prof_program.py"""
 import cProfile, pstats, os, sys, io, importlib.util
 sys.path.insert(0, "examples"); sys.path.insert(0, ".")
 spec = importlib.util.spec_from_file_location("ac_sa", "examples/AC-SA.py")
