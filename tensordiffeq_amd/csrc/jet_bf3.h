@@ -176,9 +176,61 @@ __device__ __forceinline__ T sel_first(const T (&v)[S], int idx, const float (&s
   }
 }
 
+// Packed-fp32 (v_pk_mul / v_pk_fma / v_pk_add_f32) variant of the forward tanh jet: the two
+// halves of each f32x4 accumulator tile are already even-aligned register pairs, so the jet
+// arithmetic runs on pairs (exp / rcp / compares stay per element).  -DTDQ_PK_TANH=0: scalar.
+#ifndef TDQ_PK_TANH
+#define TDQ_PK_TANH 1
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void tanh_s1_x2(f32x2 z, f32x2& h, f32x2& s1) {
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  const f32x2 a = az * -2.8853900817779268f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  const f32x2 ep = e + 1.f;
+  const f32x2 r = {__builtin_amdgcn_rcpf(ep.x), __builtin_amdgcn_rcpf(ep.y)};
+  const f32x2 z2 = az * az;
+  const f32x2 poly = az * (z2 * (z2 * (z2 * -0.053968254f + 0.13333334f) + -0.33333334f) + 1.f);
+  const f32x2 big = (1.f - e) * r;
+  const f32x2 t = {az.x < 0.125f ? poly.x : big.x, az.y < 0.125f ? poly.y : big.y};
+  h = f32x2{__builtin_copysignf(t.x, z.x), __builtin_copysignf(t.y, z.y)};
+  s1 = (e * 4.f) * (r * r);
+}
+
 // forward tanh jet of one feature tile: z -> h
 template <int S, int NSO>
 __device__ __forceinline__ void tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
+#if TDQ_PK_TANH
+  constexpr int S1p = S - 1 - NSO, SOp = 1 + S1p;
+  f32x4 zap[S], zbp[S];
+#pragma unroll
+  for (int s = SOp; s < S; ++s) {
+    zap[s] = sel_first<S, S1p>(z, sp.ia[s], sp.selA[s]);
+    zbp[s] = sel_first<S, S1p>(z, sp.ib[s], sp.selB[s]);
+  }
+#pragma unroll
+  for (int cp = 0; cp < 2; ++cp) {
+    f32x2 hv, s1;
+    tanh_s1_x2(f32x2{z[0][2 * cp], z[0][2 * cp + 1]}, hv, s1);
+    const f32x2 s2 = (hv * -2.f) * s1;
+    h[0][2 * cp] = hv.x;
+    h[0][2 * cp + 1] = hv.y;
+#pragma unroll
+    for (int s = 1; s < SOp; ++s) {
+      const f32x2 r = s1 * f32x2{z[s][2 * cp], z[s][2 * cp + 1]};
+      h[s][2 * cp] = r.x;
+      h[s][2 * cp + 1] = r.y;
+    }
+#pragma unroll
+    for (int s = SOp; s < S; ++s) {
+      const f32x2 r = (s2 * f32x2{zap[s][2 * cp], zap[s][2 * cp + 1]}) * f32x2{zbp[s][2 * cp], zbp[s][2 * cp + 1]} +
+                      s1 * f32x2{z[s][2 * cp], z[s][2 * cp + 1]};
+      h[s][2 * cp] = r.x;
+      h[s][2 * cp + 1] = r.y;
+    }
+  }
+  return;
+#endif
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
   f32x4 za[S], zb[S];
 #pragma unroll
@@ -204,6 +256,50 @@ template <int S, int NSO>
 __device__ __forceinline__ void tanh_jet_b(const JetSpec& sp, const f32x4 (&h)[S], const f32x4 (&hb)[S],
                                            f32x4 (&zb)[S]) {
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+#if TDQ_PK_TANH
+#pragma unroll
+  for (int cp = 0; cp < 2; ++cp) {
+    f32x2 hc[S], hbc[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      hc[s] = f32x2{h[s][2 * cp], h[s][2 * cp + 1]};
+      hbc[s] = f32x2{hb[s][2 * cp], hb[s][2 * cp + 1]};
+    }
+    const f32x2 hv = hc[0];
+    const f32x2 s1 = 1.f - hv * hv;
+    const f32x2 m2h = hv * -2.f;
+    f32x2 zbv[S];
+    f32x2 sb1 = {0.f, 0.f}, sb2 = {0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < S; ++s) zbv[s] = s1 * hbc[s];
+#pragma unroll
+    for (int s = 1; s < S; ++s) sb1 = hc[s] * hbc[s] + sb1;
+#pragma unroll
+    for (int s = SO; s < S; ++s) {
+      const f32x2 ha = sel_first<S, S1>(hc, sp.ia[s], sp.selA[s]), hq = sel_first<S, S1>(hc, sp.ib[s], sp.selB[s]);
+      const f32x2 hbs = hbc[s];
+      sb2 = (ha * hq) * hbs + sb2;
+      const f32x2 ga = (m2h * hq) * hbs, gb = (m2h * ha) * hbs;
+      if constexpr (S1 <= 2) {
+#pragma unroll
+        for (int q = 1; q < SO; ++q) {
+          if (sp.ia[s] == q) zbv[q] += ga;
+          if (sp.ib[s] == q) zbv[q] += gb;
+        }
+      } else {
+#pragma unroll
+        for (int q = 1; q < SO; ++q) zbv[q] = sp.selA[s][q] * ga + (sp.selB[s][q] * gb + zbv[q]);
+      }
+    }
+    zbv[0] = m2h * sb1 + (sb2 * -2.f + zbv[0]);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      zb[s][2 * cp] = zbv[s].x;
+      zb[s][2 * cp + 1] = zbv[s].y;
+    }
+  }
+  return;
+#endif
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     float hc[S];
