@@ -280,16 +280,10 @@ __device__ __forceinline__ void tanh_jet_b(const JetSpec& sp, const f32x4 (&h)[S
       const f32x2 hbs = hbc[s];
       sb2 = (ha * hq) * hbs + sb2;
       const f32x2 ga = (m2h * hq) * hbs, gb = (m2h * ha) * hbs;
-      if constexpr (S1 <= 2) {
+      // one-hot FMAs (uniform 0 / 1 weights): two packed FMAs per first-order stream, where the
+      // compiler if-converts the equivalent uniform branches into adds + per-element selects
 #pragma unroll
-        for (int q = 1; q < SO; ++q) {
-          if (sp.ia[s] == q) zbv[q] += ga;
-          if (sp.ib[s] == q) zbv[q] += gb;
-        }
-      } else {
-#pragma unroll
-        for (int q = 1; q < SO; ++q) zbv[q] = sp.selA[s][q] * ga + (sp.selB[s][q] * gb + zbv[q]);
-      }
+      for (int q = 1; q < SO; ++q) zbv[q] = sp.selA[s][q] * ga + (sp.selB[s][q] * gb + zbv[q]);
     }
     zbv[0] = m2h * sb1 + (sb2 * -2.f + zbv[0]);
 #pragma unroll
