@@ -277,8 +277,11 @@ class AdamEngine:
         fop(J, with_total=False, reduce=False)
         grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
         grads = self._fused_grads(fop, grad, fop.dlam, fop.dscal)
-        arr, n = fused.group_array(self._opt_groups(grads))
-        jet_hip.step_tail(saved, work, grad, fop, st, self.counters, arr, n, st["best_flat"],
+        packed = fused.group_array(self._opt_groups(grads))
+        if packed is None:  # gradient tensors the single launch cannot take: reduce, then Adam
+            raise RuntimeError("fused step tail: parameter groups do not fit one launch "
+                               "(set TDQ_FUSED_TAIL=0)")
+        jet_hip.step_tail(saved, work, grad, fop, st, self.counters, packed[0], packed[1], st["best_flat"],
                           write_images=in_graph)
         self._tail_saved = saved
         return fop.total
@@ -304,8 +307,11 @@ class AdamEngine:
         if st["best_flat"].numel() != self.flat.numel():
             raise ValueError(f"best-weights snapshot has {st['best_flat'].numel()} elements, parameters "
                              f"{self.flat.numel()}")
-        arr, n = fused.group_array(self._opt_groups(grads))
-        jet_hip.dp_tail_b(self._tail_saved, arr, n, st["improved"], st["best_flat"])
+        packed = fused.group_array(self._opt_groups(grads))
+        if packed is None:
+            raise RuntimeError("fused step tail: parameter groups do not fit one launch "
+                               "(set TDQ_FUSED_TAIL=0)")
+        jet_hip.dp_tail_b(self._tail_saved, packed[0], packed[1], st["improved"], st["best_flat"])
         return loss
 
     def _eager_step(self):
