@@ -128,3 +128,35 @@ def test_graph_lbfgs_quadratic():
         return 0.5 * x @ A @ x, A @ x
     x, n = graph_lbfgs(f, torch.ones(10, dtype=torch.float64), 50)
     assert x.abs().max() < 1e-6
+
+
+def test_group_array_layout_and_limits():
+    """The ctypes AdamGroup block used by the single-launch Adam / fused step tail: one row per
+    tensor (theta first), refusing what one launch cannot take (non-contiguous, > 16 tensors)."""
+    import torch
+    from tensordiffeq_amd.ops import fused
+    t = torch.zeros((), dtype=torch.float64)
+    p, g, m, v = (torch.zeros(10) for _ in range(4))
+    lam = [torch.zeros(5) for _ in range(4)]
+    groups = [([(p, g, m, v, 1.0)], t, 0.005, 0.99, 0.999, 1e-7),
+              ([(x, x, x, x, -1.0) for x in lam], t, 0.01, 0.9, 0.999, 1e-7)]
+    arr, n = fused.group_array(groups)
+    assert n == 5 and arr[0].n == 10 and arr[0].sign == 1.0 and arr[1].sign == -1.0
+    assert arr[0].p == p.data_ptr() and abs(arr[1].lr - 0.01) < 1e-9
+    big = [([(p, g, m, v, 1.0)] * 17, t, 0.005, 0.99, 0.999, 1e-7)]
+    assert fused.group_array(big) is None
+    nc = torch.zeros(10, 2)[:, 0]
+    assert fused.group_array([([(nc, nc, nc, nc, 1.0)], t, 0.005, 0.99, 0.999, 1e-7)]) is None
+
+
+def test_fused_tail_off_on_cpu():
+    """The fused step tail is a GPU path: a CPU engine keeps the reference-order Adam step."""
+    import tensordiffeq_amd as tdq
+    from tests.test_solver import burgers
+    D, bcs, f_model = burgers(n_f=200)
+    m = tdq.CollocationSolverND(verbose=False)
+    m.compile([2, 16, 16, 1], f_model, D, bcs)
+    eng = m._get_engine(None, 5)
+    assert eng._tail_eligible() is False
+    m.fit(tf_iter=3)
+    assert len(m.losses) == 3
