@@ -84,8 +84,11 @@ static inline int spec_nso(int S, const int* spec) {
 // row is 16-byte aligned for the float4 reduction
 static inline int slab_stride(int P) { return (P + 3) & ~3; }
 
-// workgroup-chunk count of the first reduction pass
-static inline int slab_chunks(int nwg) { return nwg < 16 ? nwg : 16; }
+// workgroup-chunk count of the first reduction pass (-DTDQ_SLAB_CHUNKS for A/B runs)
+#ifndef TDQ_SLAB_CHUNKS
+#define TDQ_SLAB_CHUNKS 16
+#endif
+static inline int slab_chunks(int nwg) { return nwg < TDQ_SLAB_CHUNKS ? nwg : TDQ_SLAB_CHUNKS; }
 
 // four consecutive slab entries (float4 column q of row `row`) as fp32; H: the slab holds bf16
 template <bool H>
