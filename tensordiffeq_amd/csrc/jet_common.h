@@ -86,7 +86,7 @@ static inline int slab_stride(int P) { return (P + 3) & ~3; }
 
 // workgroup-chunk count of the first reduction pass (-DTDQ_SLAB_CHUNKS for A/B runs)
 #ifndef TDQ_SLAB_CHUNKS
-#define TDQ_SLAB_CHUNKS 16
+#define TDQ_SLAB_CHUNKS 8
 #endif
 static inline int slab_chunks(int nwg) { return nwg < TDQ_SLAB_CHUNKS ? nwg : TDQ_SLAB_CHUNKS; }
 
