@@ -172,7 +172,7 @@ def main(argv=None):
                        "points_per_gpu": args.npts, "backend": backend,
                        "precision": PRECISION_NOTES[args.precision] if backend == "hip" else "fp32",
                        "bc_points": "IC 512 (SA) + periodic 2x201 (u, u_x)",
-                       "accuracy_evidence": "profiles/r2_v2_accuracy_mixed.jsonl"},
+                       "accuracy_evidence": "profiles/r2_v26_accuracy_final.jsonl"},
             "loss_after": loss,
             "l2_rel_error_after_steps": l2,
             "total_adam_steps": int(model._state["epoch_host"]),
