@@ -68,7 +68,9 @@ def main(argv=None):
     res = report("AC-SA", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"]),
                            "min_loss_adam": float(model.min_loss["adam"]),
                            "min_loss_lbfgs": float(model.min_loss["l-bfgs"]),
-                           "adam_s": t1 - t0, "lbfgs_s": t2 - t1, "backend": model.active_backend}, args.quiet)
+                           "adam_s": t1 - t0, "lbfgs_s": t2 - t1, "backend": model.active_backend,
+                           "lbfgs_n_iter": model.fit_info.get("lbfgs", {}).get("n_iter"),
+                           "lbfgs_reason": model.fit_info.get("lbfgs", {}).get("reason")}, args.quiet)
     if args.plot:
         tdq.plotting.plot_solution_domain1D(model, [x, t], ub=np.array([1.0, 1.0]), lb=np.array([-1.0, 0.0]),
                                             Exact_u=U)

@@ -28,6 +28,8 @@ def parser(desc, iters=10000, newton=0, n_f=None):
     ap.add_argument("--backend", default="auto", help="auto | hip | jet | autograd")
     ap.add_argument("--precision", default=None, help="bf16x3 | bf16 | fp32 (HIP jet GEMMs)")
     ap.add_argument("--newton-precision", default=None, help="jet precision of the L-BFGS phase (default: --precision)")
+    ap.add_argument("--lbfgs-stop", default=None, choices=["fixed", "legacy"],
+                    help="L-BFGS function-change test: |f - f_old| < tolX (fixed) or the reference's |f| < tolX")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--plot", action="store_true", help="draw the reference-style figures")
     ap.add_argument("--quiet", action="store_true")
@@ -38,6 +40,8 @@ def solver_kw(args):
     kw = {"backend": args.backend, "device": args.device, "precision": args.precision}
     if getattr(args, "newton_precision", None):
         kw["newton_precision"] = args.newton_precision
+    if getattr(args, "lbfgs_stop", None):
+        kw["lbfgs_stop"] = args.lbfgs_stop
     return kw
 
 

@@ -18,6 +18,12 @@ fused_loss             TDQ_FUSED_LOSS=0 disables   single-kernel loss program
 allow_torch_fallback   TDQ_ALLOW_TORCH_FALLBACK    1: let GPU runs fall back to torch ops
 lbfgs                  TDQ_LBFGS                   auto (device on GPU, host on CPU) | device
                                                    (GPU-resident kernels, graph-replayed) | host
+lbfgs_stop             TDQ_LBFGS_STOP              fixed (|f - f_old| < tolX) | legacy (the reference's
+                                                   effective |f| < tolX, optimizers.py:273)
+force_dp               TDQ_FORCE_DP=1              DP machinery (process group, bucket all-reduce)
+                                                   even at world 1 (parallel/dist.py)
+dp_graph               TDQ_DP_GRAPH=0 disables     RCCL all-reduce captured inside the step graph
+nan_check              TDQ_NAN_CHECK=0 disables    device loss-history NaN/Inf scan (fit.py)
 (profiling)            TDQ_PROFILE                 directory: every fit() runs under torch.profiler
                                                    -> trace.json + kernels.txt (profiling.py)
 =====================  ==========================  =========================================
@@ -48,6 +54,7 @@ class SolverConfig:
     fused_loss: bool = True
     allow_torch_fallback: bool = False
     lbfgs: str = "auto"
+    lbfgs_stop: str = "fixed"
 
     @classmethod
     def from_env(cls, **overrides):
@@ -65,6 +72,7 @@ class SolverConfig:
             "fused_loss": _env_bool("TDQ_FUSED_LOSS", True),
             "allow_torch_fallback": _env_bool("TDQ_ALLOW_TORCH_FALLBACK", False),
             "lbfgs": e.get("TDQ_LBFGS", cls.lbfgs),
+            "lbfgs_stop": e.get("TDQ_LBFGS_STOP", cls.lbfgs_stop),
         }
         vals.update({k: v for k, v in overrides.items() if v is not None})
         cfg = cls(**vals)
@@ -82,6 +90,8 @@ class SolverConfig:
             raise ValueError("log_every must be >= 1")
         if self.lbfgs not in ("auto", "device", "host"):
             raise ValueError(f"lbfgs {self.lbfgs!r}")
+        if self.lbfgs_stop not in ("fixed", "legacy"):
+            raise ValueError(f"lbfgs_stop {self.lbfgs_stop!r}")
 
     def apply_process_env(self):
         """Push the process-wide switches that the kernels / engines read."""

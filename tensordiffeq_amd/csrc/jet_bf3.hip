@@ -511,7 +511,9 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int 
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
                       float* total, void* stream) {
   const int WT = width_tiles(width);
-  if (WT < 2 || n_lblocks < 0 || n_terms < 0 || n_scal < 0) return (int)hipErrorInvalidValue;
+  // the S-independent part of the geometry check of the sibling entry points (one stream)
+  if (!bf3_ok(WT, 1, d_in, d_out, n_hidden) || N < 1 || n_lblocks < 0 || n_terms < 0 || n_scal < 0)
+    return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
   const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;

@@ -65,6 +65,8 @@ struct LbCfg {
   double lr;        // fixed step (0.8)
   double tol_fun;
   double tol_x;
+  int legacy_stop;  // 1: the reference's effective function-change test |f| < tolX (tf.abs(f, f_old),
+                    //    optimizers.py:273 - the second argument is the op name); 0: |f - f_old| < tolX
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -204,7 +206,8 @@ __global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restric
         if (n_iter >= c.max_iter || fe >= c.max_eval) {
           done = 1;
           reason = LB_R_MAXITER;
-        } else if (sc[4] <= c.tol_fun || st[LB_DT1] <= c.tol_x || fabs(f - st[LB_FOLD]) < c.tol_x) {
+        } else if (sc[4] <= c.tol_fun || st[LB_DT1] <= c.tol_x ||
+                   (c.legacy_stop ? fabs(f) : fabs(f - st[LB_FOLD])) < c.tol_x) {
           done = 1;
           reason = LB_R_TOL;
         }
@@ -412,9 +415,9 @@ int tdq_lbfgs_nst() { return LB_NST; }
 int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
                      double* st, double* SY, double* YY, double* coef, double* part, double* part2, float* fhist,
                      int p, int m, int max_iter, int nchunks, int nblk, int fhist_len, double max_eval, double lr,
-                     double tol_fun, double tol_x, void* stream) {
+                     double tol_fun, double tol_x, int legacy_stop, void* stream) {
   if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
-  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x};
+  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t lds = ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m + 4 * 64) * sizeof(double);
   static bool attr = false;

@@ -252,12 +252,8 @@ __global__ void loss_total_kernel(const float* __restrict__ losses, int n_terms,
   *total = s;
 }
 
-extern "C" {
-
-// code: int4 per instruction; outs / groups / ptrs: device buffers of LFOut / LFGroup / LFPtrs
-// partials -> per-term losses and scalar gradients (+ the total when with_total); a separate entry
-// so a captured step can run it on a side stream, beside the jet backward
-int tdq_loss_reduce(const float* partials, int n_blocks, int n_terms, int n_scal, float* losses, float* total,
+// partials -> per-term losses and scalar gradients (+ the total when with_total)
+static int loss_reduce(const float* partials, int n_blocks, int n_terms, int n_scal, float* losses, float* total,
                     float* dscal, int with_total, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int ns = n_terms + n_scal;
@@ -273,7 +269,11 @@ int tdq_loss_reduce(const float* partials, int n_blocks, int n_terms, int n_scal
   return 0;
 }
 
-// do_reduce = 0: only the loss kernel (dJ, dlam, block partials); tdq_loss_reduce finishes
+extern "C" {
+
+// code: int4 per instruction; outs / groups / ptrs: device buffers of LFOut / LFGroup / LFPtrs
+// do_reduce = 0: only the loss kernel (dJ, dlam, block partials); the fused step tail
+// (tdq_step_tail_bf3 / tdq_dp_tail_a_bf3) reduces the partials itself
 int tdq_loss_fused(const int* code, const float* consts, const void* outs, const void* groups,
                    const void* ptrs, int n_groups, int n_terms, int n_scal, int S, int d_in, int N,
                    const float* J, const float* X, float* dJ, float* partials, int n_blocks, int max_regs,
@@ -296,7 +296,7 @@ int tdq_loss_fused(const int* code, const float* consts, const void* outs, const
                      dJ, partials);
   TDQ_CHECK_LAUNCH();
   if (!do_reduce) return 0;
-  return tdq_loss_reduce(partials, n_blocks, meta.n_terms, meta.n_scal, losses, total, dscal, with_total, stream);
+  return loss_reduce(partials, n_blocks, meta.n_terms, meta.n_scal, losses, total, dscal, with_total, stream);
 }
 
 int tdq_loss_meta_sizes(int* out) {

@@ -344,27 +344,44 @@ class AdamEngine:
                 self._graph_saved = self._tail_saved
         else:
             tail = self._tail_eligible()
-            ga = torch.cuda.CUDAGraph()
-            with capture_graph(ga, pool=pool):
-                loss, grads, terms = self._dp_tail_phase_a() if tail else self._phase_a(for_step=True)
-                red_idx = self.red_idx
-                red = [grads[i] for i in red_idx]
-                terms = _term_list(terms)
-                self._bucket = _Bucket(red, 1 + len(terms))
-                self._bucket_buf = self._bucket.pack(red, [loss] + terms)
-                self._grads_static = grads
-                self._red_idx = red_idx
-            gb = torch.cuda.CUDAGraph()
-            with capture_graph(gb, pool=pool):
-                red_out, scal = self._bucket.unpack(self._bucket_buf)
-                grads = list(self._grads_static)
-                for i, gg in zip(self._red_idx, red_out):
-                    grads[i] = gg.view_as(grads[i])
-                self.static_loss = (self._dp_tail_phase_b if tail else self._phase_b)(scal[0], grads, scal[1:])
-            self.graph_a, self.graph_b = ga, gb
+            if self.dist.graph_collectives:
+                # RCCL: the bucket all-reduce is captured in the step graph - one replay per step
+                g = torch.cuda.CUDAGraph()
+                with capture_graph(g, pool=pool):
+                    self._dp_half_a(tail)
+                    self.dist.all_reduce_(self._bucket_buf)
+                    self._dp_half_b(tail)
+                self.graph_a, self.graph_b = g, None
+            else:
+                ga = torch.cuda.CUDAGraph()
+                with capture_graph(ga, pool=pool):
+                    self._dp_half_a(tail)
+                gb = torch.cuda.CUDAGraph()
+                with capture_graph(gb, pool=pool):
+                    self._dp_half_b(tail)
+                self.graph_a, self.graph_b = ga, gb
             if tail:
                 self._graph_saved = self._tail_saved
         return warm
+
+    def _dp_half_a(self, tail):
+        """DP step up to the collective: loss + gradients, packed into the static bucket."""
+        loss, grads, terms = self._dp_tail_phase_a() if tail else self._phase_a(for_step=True)
+        red_idx = self.red_idx
+        red = [grads[i] for i in red_idx]
+        terms = _term_list(terms)
+        self._bucket = _Bucket(red, 1 + len(terms))
+        self._bucket_buf = self._bucket.pack(red, [loss] + terms)
+        self._grads_static = grads
+        self._red_idx = red_idx
+
+    def _dp_half_b(self, tail):
+        """DP step after the collective: unpack the bucket, bookkeeping, optimizer update."""
+        red_out, scal = self._bucket.unpack(self._bucket_buf)
+        grads = list(self._grads_static)
+        for i, gg in zip(self._red_idx, red_out):
+            grads[i] = gg.view_as(grads[i])
+        self.static_loss = (self._dp_tail_phase_b if tail else self._phase_b)(scal[0], grads, scal[1:])
 
     def _replay(self):
         self.graph_a.replay()
@@ -400,13 +417,36 @@ class AdamEngine:
             # tail: bring them up to date with the parameters as they are now
             from .ops import jet_hip
             jet_hip.pack_images(self._graph_saved)
+        checked = int(st["epoch_host"]) - done
         while done < n_steps:
             loss = self._replay() if (use_graph and self.graph_a is not None) else self._eager_step()
             done += 1
             st["epoch_host"] += 1
             if progress is not None and (done % log_every == 0 or done == n_steps):
+                checked = self._check_finite(checked)
                 progress(done, float(loss))
+        self._check_finite(checked)
         return loss
+
+    def _check_finite(self, lo):
+        """Failure detection: the loss-history rows ``[lo, epoch)`` written on the
+        device by the captured steps are scanned with one reduction and one read-back, at the
+        progress cadence and at the end of every :meth:`run` - never inside the step.  A NaN / Inf
+        total loss raises ``FloatingPointError`` naming the first bad epoch (the best-weights
+        snapshot, taken before each update, still holds the last finite model).  ``TDQ_NAN_CHECK=0``
+        disables the check.  Returns the new low-water mark."""
+        st = self.state
+        hi = int(st["epoch_host"])
+        if hi <= lo or os.environ.get("TDQ_NAN_CHECK", "1") == "0":
+            return hi
+        col = st["hist"][lo:hi, 0]
+        bad = ~torch.isfinite(col)
+        if bool(bad.any()):
+            first = lo + int(torch.nonzero(bad)[0, 0])
+            raise FloatingPointError(f"Adam: loss became {float(st['hist'][first, 0])} at epoch {first} "
+                                     f"(best finite loss {float(st['best_loss']):.6g} at epoch "
+                                     f"{int(st['best_epoch'])}; predict(best_model=True) uses it)")
+        return hi
 
 
 class LossGradEngine:
@@ -470,6 +510,7 @@ class LossGradEngine:
         with torch.no_grad():
             self.flat.copy_(x)
         use_graph = _use_graphs(self.flat.device)
+        in_graph = self.dist.graph_collectives   # the all-reduce is captured with the evaluation
         if use_graph and self.graph is None and self.n_evals >= 1:
             stream = torch.cuda.Stream(device=self.flat.device)
             stream.wait_stream(torch.cuda.current_stream(self.flat.device))
@@ -479,14 +520,18 @@ class LossGradEngine:
             g = torch.cuda.CUDAGraph()
             with capture_graph(g):
                 self._static = self._body()
+                if in_graph:
+                    self.dist.all_reduce_(self._static)
             self.graph = g
         if self.graph is not None:
             self.graph.replay()
             buf = self._static.clone()
+            reduced = in_graph
         else:
             buf = self._body()
+            reduced = False
         self.n_evals += 1
-        if self.dist.is_distributed:
+        if self.dist.is_distributed and not reduced:
             self.dist.all_reduce_(buf)
         return buf[-1], buf[:-1]
 
@@ -510,10 +555,12 @@ class Timer:
         return False
 
 
-def nan_guard(loss):
+def nan_guard(loss, where="loss"):
+    """Host-side check of one scalar (the L-BFGS wrappers; the Adam engine scans its device
+    history instead, :meth:`AdamEngine._check_finite`)."""
     v = float(loss)
     if math.isnan(v) or math.isinf(v):
-        raise FloatingPointError(f"loss became {v}")
+        raise FloatingPointError(f"{where} became {v}")
     return v
 
 

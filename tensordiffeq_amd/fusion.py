@@ -168,6 +168,8 @@ class Sym:
         syms = [a for a in args if isinstance(a, Sym)]
         if name in ("cat", "stack", "hstack", "concat"):
             return _CatMarker()
+        if name in ("ones_like",):  # the unit cotangent of torch.autograd.grad(u, x, ones_like(u))
+            return _OnesMarker()
         if not syms:
             raise TraceError(f"unsupported torch function {name}")
         s = syms[0]
@@ -198,6 +200,11 @@ class Sym:
 
 class _CatMarker:
     """Result of ``torch.cat([x, t], 1)`` inside a traced callable (only fed to u_model)."""
+
+
+class _OnesMarker:
+    """Result of ``torch.ones_like(u)`` inside a traced callable (only fed to
+    ``torch.autograd.grad`` as the cotangent, see :func:`autodiff._routed_autograd_grad`)."""
 
 
 class _TraceCtx(autodiff._Ctx):

@@ -46,6 +46,13 @@ class MetricsLogger:
         self._t, self._last = now, epoch
         return rec
 
+    def log_event(self, event, **fields):
+        """One non-periodic record (e.g. why L-BFGS stopped)."""
+        rec = {"event": event, "rank": self.rank, "world": self.world, "time": time.time()}
+        rec.update(fields)
+        self._f.write(json.dumps(rec) + "\n")
+        return rec
+
     def close(self):
         if self._f:
             self._f.close()

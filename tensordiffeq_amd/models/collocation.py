@@ -15,6 +15,7 @@ reports the true global loss (B4); repeated ``fit`` calls resume (B6); L-BFGS ru
 from __future__ import annotations
 
 import math
+import time
 
 import numpy as np
 import torch
@@ -76,6 +77,7 @@ class CollocationSolverND:
         self._state = None
         self._programs = {}
         self._best_flat = {}
+        self.fit_info = {}    # last fit(): per-phase steps / wall time, L-BFGS stop reason
         self.log_every = 100
         self.metrics = None   # MetricsLogger (compile(metrics_path=...) or TDQ_METRICS)
 
@@ -83,11 +85,11 @@ class CollocationSolverND:
     def compile(self, layer_sizes, f_model, domain, bcs, Adaptive_type=0, dict_adaptive=None,
                 init_weights=None, g=None, dist=False, backend="auto", device=None,
                 periodic_legacy=False, seed=None, network=None, precision=None, metrics_path=None,
-                log_every=None, newton_precision=None):
+                log_every=None, newton_precision=None, lbfgs_stop=None):
         from ..config import SolverConfig
         self.config = SolverConfig.from_env(backend=None if backend == "auto" else backend, precision=precision,
                                             seed=seed, metrics_path=metrics_path, log_every=log_every,
-                                            newton_precision=newton_precision)
+                                            newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
         backend = self.config.backend
         precision = self.config.precision
         # jet-GEMM precision of the L-BFGS phase (None: same as the Adam phase).  L-BFGS's
@@ -172,7 +174,7 @@ class CollocationSolverND:
                                     dtype=torch.float32).to(self.device)
                 if ctx.is_distributed:
                     ctx.broadcast_(t)
-                sharded = key == "residual" and t.numel() == self.N_f and ctx.world > 1
+                sharded = key == "residual" and t.numel() == self.N_f and ctx.is_distributed
                 if sharded:
                     t = t.reshape(-1, 1)[self._lo:self._hi]
                 t = t.reshape(-1, 1).contiguous() if t.numel() > 1 else t.reshape(()).contiguous()
@@ -339,7 +341,7 @@ class CollocationSolverND:
 
     def _lam_replicated(self):
         ctx = self.dist_ctx
-        return [not (k == "residual" and ctx.world > 1 and l.numel() > 1)
+        return [not (k == "residual" and ctx.is_distributed and l.numel() > 1)
                 for l, k in zip(self.lambdas, self._lam_kind)]
 
     # ================================================================== loss API =========
@@ -423,6 +425,7 @@ class CollocationSolverND:
                         self._log_metrics("adam", loss)
                 bar.refresh()
 
+            t_adam = time.perf_counter()
             if batches == [None]:
                 eng = self._get_engine(None, tf_iter)
                 eng.run(tf_iter, progress=progress, log_every=self.log_every)
@@ -435,7 +438,8 @@ class CollocationSolverND:
                         progress(ep + 1, float(loss))
             bar.close()
             st = self._state
-            self.min_loss["adam"] = float(st["best_loss"])
+            self.min_loss["adam"] = float(st["best_loss"])   # (device sync: the phase is done)
+            self.fit_info["adam"] = {"steps": int(tf_iter), "wall_s": time.perf_counter() - t_adam}
             self.best_epoch["adam"] = int(st["best_epoch"])
             self._best_flat["adam"] = st["best_flat"].clone()
             self.best_model["adam"] = _FlatModel(self.u_model, self._best_flat["adam"])
@@ -461,7 +465,20 @@ class CollocationSolverND:
         return impl == "device"
 
     def _fit_lbfgs(self, newton_iter, newton_eager):
+        t0 = time.perf_counter()
+        info = self._fit_lbfgs_body(newton_iter, newton_eager)
+        info["wall_s"] = time.perf_counter() - t0
+        info["max_iter"] = int(newton_iter)
+        self.fit_info["lbfgs"] = info
+        if self.metrics is not None:
+            self.metrics.log_event("lbfgs_stop", **info)
+        if self.verbose and self.dist_ctx.rank == 0:
+            print(f"L-BFGS stopped after {info['n_iter']} iterations: {info['reason']}")
+
+    def _fit_lbfgs_body(self, newton_iter, newton_eager):
+        """Run L-BFGS; returns ``{"impl", "n_iter", "func_evals", "reason", "stop"}``."""
         ctx = self.dist_ctx
+        stop = getattr(getattr(self, "config", None), "lbfgs_stop", "fixed")
         if self.verbose and ctx.rank == 0:
             print("Starting L-BFGS training")
         eng = self._get_lbfgs_engine()
@@ -491,20 +508,28 @@ class CollocationSolverND:
 
             opt = lbfgs_device.minimize(eng.evaluate_fg, flat.data, newton_iter, lr=0.8,
                                         all_reduce=ctx.all_reduce_ if ctx.is_distributed else None,
+                                        capture_all_reduce=ctx.graph_collectives,
                                         use_graph=_use_graphs(self.device),
-                                        poll_every=max(1, min(int(self.log_every), 64)), on_poll=on_poll)
+                                        poll_every=max(1, min(int(self.log_every), 64)), on_poll=on_poll,
+                                        stop=stop)
             with torch.no_grad():
                 flat.copy_(opt.best_x)
             self.min_loss["l-bfgs"] = opt.min_loss
             self.best_epoch["l-bfgs"] = opt.best_epoch
             self.lbfgs_state = opt
+            info = {"impl": "device", "n_iter": opt.n_iter, "func_evals": opt.func_eval, "reason": opt.reason}
         elif newton_eager:
-            x, _, _, best_w, min_loss, best_epoch = eager_lbfgs(
-                eng, flat.detach().clone(), maxIter=newton_iter, learningRate=0.8, on_eval=on_eval)
+            from ..optimizers.lbfgs import Struct
+            state = Struct()
+            x, _, fe, best_w, min_loss, best_epoch = eager_lbfgs(
+                eng, flat.detach().clone(), state=state, maxIter=newton_iter, learningRate=0.8, on_eval=on_eval,
+                stop=stop)
             with torch.no_grad():
                 flat.copy_(best_w)
             self.min_loss["l-bfgs"] = float(min_loss)
             self.best_epoch["l-bfgs"] = int(best_epoch)
+            info = {"impl": "host", "n_iter": int(getattr(state, "nIter", 0)), "func_evals": int(fe),
+                    "reason": getattr(state, "reason", "?")}
         else:
             x, _ = graph_lbfgs(eng, flat.detach().clone(), newton_iter, on_eval=on_eval)
             with torch.no_grad():
@@ -512,9 +537,13 @@ class CollocationSolverND:
             f, _ = eng(flat.detach().clone())
             self.min_loss["l-bfgs"] = float(f)
             self.best_epoch["l-bfgs"] = newton_iter
+            info = {"impl": "strong-wolfe", "n_iter": int(newton_iter), "func_evals": int(eng.n_evals),
+                    "reason": "maxIter"}
         bar.close()
         self._best_flat["l-bfgs"] = flat.detach().clone()
         self.best_model["l-bfgs"] = _FlatModel(self.u_model, self._best_flat["l-bfgs"])
+        info["stop"] = stop
+        return info
 
     def _select_overall(self, start_epoch, tf_iter):
         if self.min_loss["adam"] <= self.min_loss["l-bfgs"]:

@@ -138,7 +138,7 @@ class DiscoveryModel:
     def _get_engine(self, n_hint):
         prog = self.program()
         if self._engine is None:
-            rep = not (self.dist_ctx.world > 1)
+            rep = not self.dist_ctx.is_distributed
             groups = [ParamGroup([self.u_model.flat], lambda: self.tf_optimizer, 1.0),
                       ParamGroup(self._lambdas(), lambda: self.tf_optimizer_weights, -1.0, [rep]),
                       ParamGroup(self.vars, lambda: self.tf_optimizer_vars, 1.0)]

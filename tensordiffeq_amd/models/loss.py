@@ -133,18 +133,26 @@ class LossProgram:
         if not isinstance(self.net, TanhMLP):
             jetable = False
             reasons.append("u_model is not a TanhMLP")
+        recorded = []
         for fn, si, extra in self.callables:
             if not jetable:
                 break
             X = self.segments[si].X
             probe = X[: min(8, X.shape[0])].detach().double() if X.shape[0] else X.double()
             net64 = _Float64View(self.net)
-            req, ok, why, _ = autodiff.record_callable(fn, net64, probe, extra_args=extra)
+            req, ok, why, _, outs = autodiff.record_callable(fn, net64, probe, extra_args=extra,
+                                                              return_outputs=True)
             requests |= req
             seg_req.setdefault(si, set()).update(req)
+            recorded.append((fn, extra, probe, outs))
             if not ok:
                 jetable = False
                 reasons.extend(why)
+        if jetable and recorded:
+            ok, why = self._validate_jet(recorded, requests)
+            if not ok:
+                jetable = False
+                reasons.append(why)
         backend = self.requested_backend
         for s in self.segments:
             s.part = 0
@@ -186,6 +194,43 @@ class LossProgram:
                     raise RuntimeError("HIP jet backend unavailable: " + why)
         self.backend = backend
         self.reasons = reasons
+
+    def _validate_jet(self, recorded, requests):
+        """Re-run every recorded callable in a :class:`~tensordiffeq_amd.autodiff.JetContext` on
+        its float64 probe points, served by the torch jet engine with the union plan, and compare
+        with the autograd values of the recording pass.  Any exception or mismatch means the jet
+        path would not compute what the user wrote (e.g. a derivative taken through a name the
+        recorder cannot see), so the program falls back to the autograd backend."""
+        from ..jet import jet_forward
+        if not requests and not any(outs for *_, outs in recorded):
+            return True, ""
+        plan = JetPlan(requests, self.d_in)
+        w64 = [(k.detach().double(), b.detach().double()) for k, b in self.net.weights()]
+        for fn, extra, probe, ref in recorded:
+            if ref is None or probe.shape[0] == 0:
+                continue
+            try:
+                with torch.no_grad():
+                    J = jet_forward(probe, w64, plan)
+                    cols = [probe[:, j:j + 1] for j in range(self.d_in)]
+                    ctx = autodiff.JetContext(cols, jet_dict(J, plan))
+                    with autodiff.use(ctx):
+                        out = fn(ctx.proxy(), *extra, *cols)
+                outs = list(out) if isinstance(out, (tuple, list)) else [out]
+                if len(outs) != len(ref):
+                    return False, f"jet validation: {getattr(fn, '__name__', fn)} returned {len(outs)} outputs, " \
+                                  f"autograd {len(ref)}"
+                for a, b in zip(outs, ref):
+                    a = torch.as_tensor(a, dtype=torch.float64).reshape(-1)
+                    b = torch.as_tensor(b, dtype=torch.float64).reshape(-1)
+                    if a.numel() != b.numel() and a.numel() != 1 and b.numel() != 1:
+                        return False, f"jet validation: output shape mismatch in {getattr(fn, '__name__', fn)}"
+                    if not torch.allclose(a, b, rtol=1e-6, atol=1e-8 * (1.0 + float(b.abs().max()))):
+                        return False, f"jet validation: {getattr(fn, '__name__', fn)} differs from autograd " \
+                                      f"(max |diff| {float((a - b).abs().max()):.3e})"
+            except Exception as e:  # noqa: BLE001 - any failure means "not servable from a jet"
+                return False, f"jet validation: {getattr(fn, '__name__', fn)} raised {type(e).__name__}: {e}"
+        return True, ""
 
     def _split_by_order(self, seg_req):
         """Partition segments by the order their callables need: (lo requests, hi requests, hi

@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lock = threading.Lock()
 _lib = None
@@ -54,10 +54,9 @@ def _declare(lib):
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
         "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, I, I, P]),
-        "tdq_loss_reduce": (I, [P, I, I, I, P, P, P, I, P]),
         "tdq_loss_meta_sizes": (I, [P]),
         "tdq_lbfgs_nst": (I, []),
-        "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [P]),
+        "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
     }
     for name, (res, args) in sig.items():
@@ -84,12 +83,36 @@ def load(required=None):
             _declare(lib)
             ver = lib.tdq_abi_version()
             if ver != ABI_VERSION:
-                raise NativeUnavailable(f"libtdq_hip.so ABI {ver} != expected {ABI_VERSION}; rebuild")
+                _err = f"libtdq_hip.so ABI {ver} != expected {ABI_VERSION}; rebuild"
+                raise NativeUnavailable(_err)
+            built, want = library_hash(lib), expected_hash()
+            if want is not None and built != want and os.environ.get("TDQ_SKIP_HASH_CHECK", "0") != "1":
+                _err = (f"{LIB_PATH} is stale: built from sources {built}, the csrc/ sources hash to {want} "
+                        f"(run `python -m tensordiffeq_amd.csrc.build`)")
+                raise NativeUnavailable(_err)
         except OSError as e:
             _err = f"cannot load {LIB_PATH}: {e}"
             raise NativeUnavailable(_err)
         _lib = lib
         return _lib
+
+
+def library_hash(lib):
+    """Source hash the library was built from (``tdq_src_hash``), or None for an old build."""
+    fn = getattr(lib, "tdq_src_hash", None)
+    if fn is None:
+        return None
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    return fn().decode()
+
+
+def expected_hash():
+    """Hash of the HIP sources next to the library (None when they are not shipped)."""
+    from ..csrc import build as _build
+    if not _build.source_files():
+        return None
+    return _build.source_hash()
 
 
 def available():

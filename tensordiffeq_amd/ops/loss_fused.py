@@ -89,8 +89,8 @@ class FusedLossOp:
         """Run the program on jets ``J``.  ``with_total=False`` skips the total-loss launch (the Adam
         step's bookkeeping kernel sums the terms instead; ``total`` is then stale until it runs).
         ``reduce=False``: only the loss kernel (dJ, SA-weight gradients, block partials); the
-        per-term losses and scalar gradients come from a later :meth:`reduce` (e.g. on a side
-        stream, beside the jet backward)."""
+        per-term losses and scalar gradients are reduced by the fused step tail
+        (``jet_hip.step_tail`` / ``jet_hip.dp_tail_a``)."""
         lib = _lib.load()
         rc = lib.tdq_loss_fused(_lib.ptr(self.code), _lib.ptr(self.consts), _lib.ptr(self.outs),
                                 _lib.ptr(self.groups), _lib.ptr(self.ptrs), self.n_groups, self.n_terms,
@@ -102,11 +102,3 @@ class FusedLossOp:
         _lib.check(rc, "tdq_loss_fused")
         return self.total, self.losses, self.dJ, self.dlam, self.dscal
 
-    def reduce(self, with_total=True):
-        """Block partials -> per-term losses, scalar gradients (and the total) on the CURRENT stream."""
-        lib = _lib.load()
-        rc = lib.tdq_loss_reduce(_lib.ptr(self.partials), self.n_blocks, self.n_terms, self.n_scal,
-                                 _lib.ptr(self.losses), _lib.ptr(self.total), _lib.ptr(self.dscal),
-                                 int(bool(with_total)), _lib.stream_ptr(self.dJ.device))
-        _lib.check(rc, "tdq_loss_reduce")
-        return self.total, self.losses, self.dscal

@@ -84,9 +84,13 @@ def compact_direction(g, hist, hdiag):
 
 
 def eager_lbfgs(opfunc, x, state=None, maxIter=100, learningRate=1.0, do_verbose=True,
-                nCorrection=50, tolFun=1e-12, tolX=1e-12, progress=None, on_eval=None):
-    """Reference-semantics L-BFGS.  Returns ``(x, f_hist, funcEval, best_w, min_loss, best_epoch)``."""
+                nCorrection=50, tolFun=1e-12, tolX=1e-12, progress=None, on_eval=None, stop="fixed"):
+    """Reference-semantics L-BFGS.  Returns ``(x, f_hist, funcEval, best_w, min_loss, best_epoch)``;
+    ``state.reason`` / ``state.nIter`` record why and when it stopped.  ``stop="legacy"``: the
+    reference's effective function-change test ``|f| < tolX`` (optimizers.py:273) instead of
+    ``|f - f_old| < tolX``."""
     state = state if state is not None else Struct()
+    state.reason = "running"
     x = x.detach().clone()
     maxEval = maxIter * 1.25
     f, g = opfunc(x)
@@ -97,6 +101,7 @@ def eager_lbfgs(opfunc, x, state=None, maxIter=100, learningRate=1.0, do_verbose
     if math.isfinite(f_host):
         best_w, min_loss, best_epoch = x.clone(), f_host, -1
     if float(g.abs().sum()) <= tolFun:
+        state.reason, state.nIter = "tolFun at start", 0
         return x, f_hist, func_eval, best_w, min_loss, best_epoch
     hist = _History(nCorrection, x.numel(), x.device, x.dtype)
     d = g_old = None
@@ -120,6 +125,7 @@ def eager_lbfgs(opfunc, x, state=None, maxIter=100, learningRate=1.0, do_verbose
         f_old = f
         gtd, g1 = torch.stack([dot(g, d), g.abs().sum()]).tolist()
         if gtd > -tolX:
+            state.reason = "no descent direction"
             break
         t = min(1.0, 1.0 / g1) if n_iter == 1 else learningRate
         x.add_(d, alpha=t)
@@ -136,12 +142,15 @@ def eager_lbfgs(opfunc, x, state=None, maxIter=100, learningRate=1.0, do_verbose
         if progress is not None:
             progress(n_iter, f_host)
         if math.isnan(f_host):
+            state.reason = "NaN loss"
             break
         if f_host < min_loss:
             best_w, min_loss, best_epoch = x.clone(), f_host, epoch
         if n_iter == maxIter or func_eval >= maxEval:
+            state.reason = "maxIter / maxEval"
             break
-        if g1 <= tolFun or dt1 <= tolX or abs(f_host - f_old_host) < tolX:
+        if g1 <= tolFun or dt1 <= tolX or (abs(f_host) if stop == "legacy" else abs(f_host - f_old_host)) < tolX:
+            state.reason = "tolFun / tolX / function change"
             break
     state.nIter = n_iter
     state.funcEval = func_eval

@@ -34,6 +34,10 @@ NST = 24
 MAXM = 64
 REASONS = {0: "running", 1: "tolFun at start", 2: "NaN loss", 3: "maxIter / maxEval",
            4: "tolFun / tolX / function change", 5: "no descent direction"}
+# function-change stopping test: "fixed" |f - f_old| < tolX (what the reference evidently meant);
+# "legacy" |f| < tolX - what its `tf.abs(f, f_old) < tolX` computes (optimizers.py:273, the second
+# argument of tf.abs is the op name), i.e. in practice never: the run goes on to maxIter
+STOP_MODES = ("fixed", "legacy")
 
 
 def _ceil(a, b):
@@ -48,9 +52,12 @@ class DeviceLBFGS:
     """L-BFGS state for a flat fp32 parameter vector ``x`` (updated in place by :meth:`axpy`)."""
 
     def __init__(self, x, m=50, max_iter=100, lr=0.8, tol_fun=1e-12, tol_x=1e-12, max_eval=None,
-                 record_history=True):
+                 record_history=True, stop="fixed"):
         if not (1 <= m <= MAXM):
             raise ValueError(f"history size must be in [1, {MAXM}]")
+        if stop not in STOP_MODES:
+            raise ValueError(f"stop must be one of {STOP_MODES}")
+        self.stop = stop
         if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 1:
             raise ValueError("x must be a contiguous 1-D float32 tensor")
         self.x = x
@@ -116,7 +123,7 @@ class DeviceLBFGS:
                 _lib.ptr(self.coef), _lib.ptr(self.part), _lib.ptr(self.part2), _lib.ptr(self.fhist),
                 self.p, self.m, self.max_iter, self.nchunks, self.nblk,
                 0 if self.fhist is None else self.fhist.numel(), self.max_eval, self.lr, self.tol_fun,
-                self.tol_x, _lib.stream_ptr(self.x.device))
+                self.tol_x, 1 if self.stop == "legacy" else 0, _lib.stream_ptr(self.x.device))
             _lib.check(rc, "tdq_lbfgs_update")
             return
         with torch.no_grad():
@@ -176,7 +183,8 @@ class DeviceLBFGS:
                     st[BESTEP] = float(n_iter - 1)
                 if n_iter >= self.max_iter or fe >= self.max_eval:
                     done, reason = 1, 3
-                elif g1 <= self.tol_fun or s_[DT1] <= self.tol_x or abs(f - s_[FOLD]) < self.tol_x:
+                elif g1 <= self.tol_fun or s_[DT1] <= self.tol_x or \
+                        (abs(f) if self.stop == "legacy" else abs(f - s_[FOLD])) < self.tol_x:
                     done, reason = 1, 4
         st[F] = f
         st[MINLOSS] = minloss
@@ -267,15 +275,16 @@ class DeviceLBFGS:
 
 
 def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, all_reduce=None,
-             use_graph=None, poll_every=32, on_poll=None):
+             use_graph=None, poll_every=32, on_poll=None, capture_all_reduce=False, stop="fixed"):
     """Run device L-BFGS on ``x`` (in place) for at most ``max_iter`` iterations.
 
     ``evaluate()`` returns ``fg = [grad | loss]`` at the current ``x`` (a float32 device vector;
     it must read ``x`` itself).  ``all_reduce(buf)`` (optional, DP) sums ``fg`` over ranks in
     place between the evaluation and the update.  ``on_poll(opt)`` is called at every host poll
     (progress bars / metrics).  Returns the :class:`DeviceLBFGS` (``best_x``, ``st``,
-    ``fhist``); ``x`` is left at the LAST iterate - callers restore ``best_x``."""
-    opt = DeviceLBFGS(x, m=m, max_iter=max_iter, lr=lr, tol_fun=tol_fun, tol_x=tol_x)
+    ``fhist``); ``x`` is left at the LAST iterate - callers restore ``best_x``.  ``stop``: the
+    function-change test, see :data:`STOP_MODES`."""
+    opt = DeviceLBFGS(x, m=m, max_iter=max_iter, lr=lr, tol_fun=tol_fun, tol_x=tol_x, stop=stop)
     graph_ok = x.is_cuda and opt.native
     use_graph = graph_ok if use_graph is None else (bool(use_graph) and graph_ok)
 
@@ -299,7 +308,9 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
             on_poll(opt)
         return opt
     dev = x.device
-    split = all_reduce is not None
+    # the collective between evaluation and update: captured in the iteration graph (RCCL), or a
+    # host launch between two graphs (gloo)
+    split = all_reduce is not None and not capture_all_reduce
     # one eager iteration on a side stream (lazy allocations / kernel loads), then capture
     side = torch.cuda.Stream(device=dev)
     side.wait_stream(torch.cuda.current_stream(dev))
@@ -313,6 +324,8 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
         with capture_graph(ga, pool=pool):
             opt.axpy()
             fg_static = evaluate()
+            if all_reduce is not None and not split:
+                all_reduce(fg_static)
             if not split:
                 opt.update(fg_static)
         gb = None

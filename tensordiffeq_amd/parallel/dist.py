@@ -15,6 +15,13 @@ Design here:
   all-reduced (SUM).  For the 50k-parameter Allen-Cahn net that is ~196 KiB: a latency-bound
   message, so a single collective per step is the right shape for xGMI's point-to-point links.
 * Parameters are broadcast from rank 0 at start, so every rank starts from identical weights.
+* Forced DP (``TDQ_FORCE_DP=1`` or ``init_distributed(force=True)``): a real process group even at
+  world 1, so the DP machinery - split or single HIP graph around the collective, bucket packing,
+  RCCL itself - runs (and is tested / timed) on a one-GPU box; at world 1 it must reproduce the
+  single-process trajectory.
+* ``graph_collectives``: with RCCL the bucket all-reduce is captured INSIDE the step's HIP graph
+  (one replay per step, no host-launched collective); gloo, or ``TDQ_DP_GRAPH=0``, keeps the
+  two-graph split with the collective launched from the host in between.
 """
 from __future__ import annotations
 
@@ -26,17 +33,25 @@ import torch.distributed as dist
 
 
 class DistContext:
-    def __init__(self, rank=0, world=1, local_rank=0, device=None, backend=None, initialized=False):
+    def __init__(self, rank=0, world=1, local_rank=0, device=None, backend=None, initialized=False,
+                 forced=False):
         self.rank = rank
         self.world = world
         self.local_rank = local_rank
         self.device = device if device is not None else torch.device("cpu")
         self.backend = backend
         self.initialized = initialized
+        self.forced = forced
 
     @property
     def is_distributed(self):
-        return self.world > 1 and self.initialized
+        return self.initialized and (self.world > 1 or self.forced)
+
+    @property
+    def graph_collectives(self):
+        """Capture the per-step all-reduce inside the step's HIP graph (RCCL only)."""
+        return (self.is_distributed and self.backend == "nccl" and self.device.type == "cuda"
+                and os.environ.get("TDQ_DP_GRAPH", "1") != "0")
 
     def barrier(self):
         if self.is_distributed:
@@ -74,11 +89,26 @@ def env_world():
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init_distributed(backend=None, device=None, timeout_s=600):
-    """Initialise (once) from the torchrun environment; returns the process' DistContext."""
+def force_dp_requested():
+    return os.environ.get("TDQ_FORCE_DP", "0") == "1"
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def init_distributed(backend=None, device=None, timeout_s=600, force=None):
+    """Initialise (once) from the torchrun environment; returns the process' DistContext.
+    ``force`` (default ``TDQ_FORCE_DP``): build the process group even at world 1."""
     global _CTX
     if _CTX is not None:
         return _CTX
+    force = force_dp_requested() if force is None else bool(force)
     world = env_world()
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -93,9 +123,9 @@ def init_distributed(backend=None, device=None, timeout_s=600):
     if backend is None:
         backend = "nccl" if device.type == "cuda" else "gloo"
     initialized = False
-    if world > 1:
+    if world > 1 or force:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29500")
+        os.environ.setdefault("MASTER_PORT", "29500" if world > 1 else str(_free_port()))
         if not dist.is_initialized():
             kw = {}
             if backend == "nccl":
@@ -103,7 +133,7 @@ def init_distributed(backend=None, device=None, timeout_s=600):
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         initialized = True
-    _CTX = DistContext(rank, world, local_rank, device, backend, initialized)
+    _CTX = DistContext(rank, world, local_rank, device, backend, initialized, forced=force and world == 1)
     return _CTX
 
 

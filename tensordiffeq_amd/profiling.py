@@ -7,7 +7,9 @@ The reference only has commented-out ``tf.profiler.experimental.start/stop`` aro
         model.fit(tf_iter=200)
 
 or, without code changes, ``TDQ_PROFILE=prof_dir python script.py`` (every ``fit`` of a solver is
-wrapped).  The context runs ``torch.profiler`` (CPU + HIP activities) and writes
+wrapped; call k of the process writes ``prof_dir/fit_<k>/``, so a script that fits several times
+- transfer learning, Adam then a separate L-BFGS fit - keeps every call).  The context runs
+``torch.profiler`` (CPU + HIP activities) and writes
 
 * ``prof_dir/trace.json``  - Chrome / Perfetto trace of host ops and device kernels,
 * ``prof_dir/kernels.txt`` - one row per kernel name: total us, calls, us per call, share
@@ -79,6 +81,9 @@ def kernel_profile(out_dir, rank=None, title=""):
     write_kernel_table(prof, os.path.join(d, "kernels.txt"), title=title)
 
 
+_FIT_CALLS = [0]
+
+
 def env_profile_dir():
     """``TDQ_PROFILE`` (a directory) or None."""
     return os.environ.get("TDQ_PROFILE") or None
@@ -91,5 +96,7 @@ def maybe_profile(title=""):
     if d is None:
         yield None
         return
-    with kernel_profile(d, title=title) as prof:
+    k = _FIT_CALLS[0]
+    _FIT_CALLS[0] += 1
+    with kernel_profile(os.path.join(d, f"fit_{k}"), title=title) as prof:
         yield prof

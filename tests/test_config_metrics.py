@@ -69,23 +69,62 @@ def test_metrics_jsonl(tmp_path):
     m.fit(tf_iter=10, newton_iter=5)
     m.metrics.close()
     recs = read_jsonl(path)
-    adam = [r for r in recs if r["phase"] == "adam"]
+    adam = [r for r in recs if r.get("phase") == "adam"]
     assert [r["epoch"] for r in adam] == [5, 10]
     assert set(adam[-1]["terms"]) == {t.name for t in m.program().terms}
     assert adam[-1]["pts_per_s"] > 0 and math.isfinite(adam[-1]["loss"])
-    assert any(r["phase"] == "lbfgs" for r in recs)
+    assert any(r.get("phase") == "lbfgs" for r in recs)
     assert np.isclose(adam[-1]["loss"], m.losses[9]["Total Loss"], rtol=1e-6)
+    stop = [r for r in recs if r.get("event") == "lbfgs_stop"]
+    assert len(stop) == 1 and stop[0]["n_iter"] <= 5 and stop[0]["reason"]
+    assert m.fit_info["lbfgs"]["reason"] == stop[0]["reason"] and m.fit_info["adam"]["steps"] == 10
 
 
 def test_kernel_profile_writes_trace_and_table(tmp_path, monkeypatch):
     """TDQ_PROFILE wraps fit() in torch.profiler: a Chrome trace and a kernel table per run."""
     from tests.test_solver import compiled
+    from tensordiffeq_amd import profiling
     monkeypatch.setenv("TDQ_PROFILE", str(tmp_path / "prof"))
+    monkeypatch.setattr(profiling, "_FIT_CALLS", [0])
     m = compiled("jet")
     m.fit(tf_iter=3)
-    trace = tmp_path / "prof" / "trace.json"
-    table = tmp_path / "prof" / "kernels.txt"
-    assert trace.exists() and trace.stat().st_size > 0
-    lines = table.read_text().splitlines()
-    assert lines[0].startswith("# CollocationSolverND.fit(tf_iter=3")
-    assert len(lines) > 3 and "%" in lines[2]
+    m.fit(tf_iter=2)   # a second fit keeps its own trace / table
+    for k, n in ((0, 3), (1, 2)):
+        trace = tmp_path / "prof" / f"fit_{k}" / "trace.json"
+        table = tmp_path / "prof" / f"fit_{k}" / "kernels.txt"
+        assert trace.exists() and trace.stat().st_size > 0
+        lines = table.read_text().splitlines()
+        assert lines[0].startswith(f"# CollocationSolverND.fit(tf_iter={n}")
+        assert len(lines) > 3 and "%" in lines[2]
+
+
+def test_adam_nan_raises_with_epoch():
+    """Failure detection: a non-finite loss in the (device-history) Adam loop raises
+    FloatingPointError naming the epoch instead of training on silently."""
+    import pytest
+    import torch
+    from tests.test_solver import compiled
+    m = compiled("jet")
+    m.fit(tf_iter=3)
+    with torch.no_grad():
+        m.u_model.flat[5] = float("nan")
+    with pytest.raises(FloatingPointError, match="epoch 3"):
+        m.fit(tf_iter=4)
+
+
+def test_stale_library_hash_is_refused(monkeypatch):
+    """The loader refuses a libtdq_hip.so whose embedded source hash differs from csrc/."""
+    import pytest
+    from tensordiffeq_amd.ops import _lib
+    if not __import__("os").path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    lib = _lib.load()
+    assert _lib.library_hash(lib) == _lib.expected_hash()
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "_err", None)
+    monkeypatch.setattr(_lib, "expected_hash", lambda: "0000000000000000")
+    with pytest.raises(_lib.NativeUnavailable, match="stale"):
+        _lib.load(required=True)
+    monkeypatch.setenv("TDQ_SKIP_HASH_CHECK", "1")
+    monkeypatch.setattr(_lib, "_err", None)
+    assert _lib.load(required=True) is not None

@@ -196,3 +196,40 @@ def test_discovery_dp_gloo_matches_single_process():
     assert res[0]["var"] == pytest.approx(float(rvar[0].detach()), rel=1e-4, abs=1e-7)
     cw = torch.cat([r["cw"] for r in res])
     assert torch.allclose(cw, ref.col_weights.detach(), atol=1e-5)
+
+
+def _forced_worker(q):
+    os.environ.update(TDQ_FORCE_DP="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TDQ_LBFGS="device")
+    os.environ.pop("MASTER_PORT", None)
+    torch.set_num_threads(1)
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(backend="gloo", device="cpu")
+    assert ctx.is_distributed and ctx.forced and ctx.world == 1 and not ctx.graph_collectives
+    m = _build(True)
+    m.fit(tf_iter=5, newton_iter=4)
+    # plain numbers / numpy: a torch tensor would travel as a shared-memory handle that is gone
+    # once this process exits
+    q.put({"hist": [h["Total Loss"] for h in m.losses], "flat": m.u_model.flat.detach().numpy().copy(),
+           "lbfgs": m.min_loss["l-bfgs"], "red": len(m._get_engine(None, 1).red_idx)})
+    pdist.destroy()
+
+
+@pytest.mark.timeout(300)
+def test_forced_dp_world1_matches_single_process(monkeypatch):
+    """TDQ_FORCE_DP=1: a real process group at world 1 runs the DP step (bucket all-reduce, SA
+    residual weights treated as sharded) and reproduces the single-process trajectory."""
+    monkeypatch.setenv("TDQ_LBFGS", "device")
+    ref = _build(False)
+    ref.fit(tf_iter=5, newton_iter=4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(q,))
+    p.start()
+    res = q.get(timeout=280)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert res["hist"] == pytest.approx([h["Total Loss"] for h in ref.losses], rel=1e-6)
+    assert torch.allclose(torch.from_numpy(res["flat"]), ref.u_model.flat.detach(), rtol=1e-6, atol=1e-7)
+    assert res["lbfgs"] == pytest.approx(ref.min_loss["l-bfgs"], rel=1e-6)
+    assert res["red"] == 2   # theta + the IC's SA weights; residual SA weights stay local

@@ -28,7 +28,7 @@ def _free_port():
 
 def _build(dist, world=1, precision=None):
     import bench
-    return bench.build_problem(N_F // world, world, "hip", torch.device("cuda", 0), dist, precision)
+    return bench.build_problem(N_F, world, "hip", torch.device("cuda", 0), dist, precision)
 
 
 def _worker(rank, world, port, q, precision):
@@ -82,3 +82,48 @@ def test_dp_two_ranks_on_gpu_match_single_process(precision):
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-3)
     assert ((res["flat_after"] - ref_flat).norm() / ref_flat.norm()).item() < 1e-3
     assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=5e-2)
+
+
+def _forced_worker(q, precision, dp_graph):
+    os.environ.update(TDQ_FORCE_DP="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TDQ_DP_GRAPH=dp_graph)
+    os.environ.pop("MASTER_PORT", None)
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(device="cuda:0")       # backend nccl = RCCL
+    assert ctx.backend == "nccl" and ctx.is_distributed and ctx.forced
+    assert ctx.graph_collectives == (dp_graph == "1")
+    m = _build(True, 1, precision)
+    assert m.active_backend == "hip"
+    m.fit(tf_iter=8)
+    eng = m._get_engine(None, 1)
+    res = {"hist": [h["Total Loss"] for h in m.losses], "flat": m.u_model.flat.detach().cpu().numpy().copy(),
+           "one_graph": eng.graph_b is None}
+    m.fit(newton_iter=3)
+    res["lbfgs_loss"] = float(m.min_loss["l-bfgs"])
+    q.put(res)
+    pdist.destroy()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dp_graph", ["1", "0"])
+def test_forced_dp_rccl_world1_matches_single_process(dp_graph):
+    """RCCL on the one-GPU box: TDQ_FORCE_DP=1 builds a real nccl (RCCL) process group at world 1;
+    the DP step (bucket all-reduce captured in the step graph, or launched between two graphs with
+    TDQ_DP_GRAPH=0) and the DP L-BFGS reproduce the single-process trajectory."""
+    precision = "bf16"
+    ref = _build(False, 1, precision)
+    ref.fit(tf_iter=8)
+    ref_hist = [h["Total Loss"] for h in ref.losses]
+    ref_flat = ref.u_model.flat.detach().cpu().clone()
+    ref.fit(newton_iter=3)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(q, precision, dp_graph))
+    p.start()
+    res = q.get(timeout=500)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert res["one_graph"] == (dp_graph == "1")
+    assert res["hist"] == pytest.approx(ref_hist, rel=1e-6)
+    assert torch.allclose(torch.from_numpy(res["flat"]), ref_flat, rtol=1e-6, atol=1e-7)
+    assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=1e-6)

@@ -97,6 +97,51 @@ def test_stopping_tests():
     assert torch.allclose(opt.best_x, torch.full((3,), -1.0 / 3.0))
 
 
+def _offset_quadratic():
+    base = _quadratic(p=20, q=30, seed=5)
+
+    def fg(x):
+        f, g = base(x)
+        return f + 5.0, g   # minimum 5 + f_opt: never |f| < tolX
+    return fg
+
+
+@pytest.mark.parametrize("stop", ["fixed", "legacy"])
+def test_stop_modes(stop):
+    """``stop="fixed"``: |f - f_old| < tolX ends a stagnated run; ``"legacy"``: the reference's
+    effective |f| < tolX (optimizers.py:273) never fires on a loss bounded away from 0, so the
+    run only ends on maxIter or another test.  Host port and device mirror agree on the reason."""
+    fg = _offset_quadratic()
+    x = torch.zeros(20)
+    opt = LD.minimize(_evaluator(fg, x), x, 400, use_graph=False, stop=stop)
+    from tensordiffeq_amd.optimizers.lbfgs import Struct
+    st = Struct()
+    eager_lbfgs(fg, torch.zeros(20), state=st, maxIter=400, learningRate=0.8, stop=stop)
+    if stop == "fixed":
+        assert opt.reason == LD.REASONS[4] and opt.n_iter < 400
+    else:
+        assert opt.reason != LD.REASONS[4]
+    assert st.reason == opt.reason
+
+
+def test_stop_mode_legacy_runs_longer():
+    fg = _offset_quadratic()
+    n = {}
+    for stop in ("fixed", "legacy"):
+        x = torch.zeros(20)
+        n[stop] = LD.minimize(_evaluator(fg, x), x, 400, use_graph=False, stop=stop).n_iter
+    assert n["legacy"] >= n["fixed"]
+
+
+def test_solver_records_lbfgs_stop(monkeypatch):
+    from tests.test_solver import compiled
+    m = compiled("jet", problem="ac", lbfgs_stop="legacy")
+    m.fit(tf_iter=2, newton_iter=4)
+    info = m.fit_info["lbfgs"]
+    assert info["stop"] == "legacy" and info["n_iter"] == 4 and info["reason"] == LD.REASONS[3]
+    assert info["wall_s"] > 0
+
+
 def test_solver_device_lbfgs_matches_host(monkeypatch):
     from tests.test_solver import compiled
     res = {}

@@ -7,7 +7,7 @@ N_F = 4096
 
 def build(dist, world, backend):
     import bench
-    return bench.build_problem(N_F // world, world, backend, torch.device("cuda", 0), dist)
+    return bench.build_problem(N_F, world, backend, torch.device("cuda", 0), dist)
 
 
 def worker(rank, world, port, q, backend, fused):
