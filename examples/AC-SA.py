@@ -70,7 +70,7 @@ def main(argv=None):
                            "min_loss_lbfgs": float(model.min_loss["l-bfgs"]),
                            "adam_s": t1 - t0, "lbfgs_s": t2 - t1, "backend": model.active_backend,
                            "lbfgs_n_iter": model.fit_info.get("lbfgs", {}).get("n_iter"),
-                           "lbfgs_reason": model.fit_info.get("lbfgs", {}).get("reason")}, args.quiet)
+                           "lbfgs_reason": model.fit_info.get("lbfgs", {}).get("reason")}, args.quiet, model=model)
     if args.plot:
         tdq.plotting.plot_solution_domain1D(model, [x, t], ub=np.array([1.0, 1.0]), lb=np.array([-1.0, 0.0]),
                                             Exact_u=U)

@@ -49,7 +49,7 @@ def main(argv=None):
     model.fit(tf_iter=args.iters, newton_iter=args.newton)
     x, t, U = ac_data()
     err, *_ = l2_on_data_grid(model, x, t, U)
-    res = report("AC-baseline", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"])}, args.quiet)
+    res = report("AC-baseline", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"])}, args.quiet, model=model)
     if args.plot:
         tdq.plotting.plot_solution_domain1D(model, [x, t], ub=np.array([1.0, 1.0]), lb=np.array([-1.0, 0.0]),
                                             Exact_u=U)

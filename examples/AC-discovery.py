@@ -44,7 +44,7 @@ def main(argv=None):
     model.fit(tf_iter=args.iters)
     c1, c2 = (float(v.detach()) for v in model.vars)
     return report("AC-discovery", {"c1": c1, "c2": c2, "c1_rel_err": abs(c1 - 1e-4) / 1e-4,
-                                   "c2_rel_err": abs(c2 - 5.0) / 5.0}, args.quiet)
+                                   "c2_rel_err": abs(c2 - 5.0) / 5.0}, args.quiet, model=model)
 
 
 if __name__ == "__main__":

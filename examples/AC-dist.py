@@ -67,7 +67,7 @@ def main(argv=None):
     if model.dist_ctx.rank == 0:
         x, t, U = ac_data()
         res["l2_error"], *_ = l2_on_data_grid(model, x, t, U)
-        report("AC-dist", res, args.quiet)
+        report("AC-dist", res, args.quiet, model=model)
     if world > 1:
         tdq.parallel.destroy()
     return res

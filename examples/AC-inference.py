@@ -39,7 +39,7 @@ def main(argv=None):
         model.tf_optimizer_weights = Adam(lr=0.005, beta_1=.95)
     model.fit(tf_iter=args.iters)
     c1, c2 = (float(v.detach()) for v in model.vars)
-    return report("AC-inference", {"c1": c1, "c2": c2}, args.quiet)
+    return report("AC-inference", {"c1": c1, "c2": c2}, args.quiet, model=model)
 
 
 if __name__ == "__main__":

@@ -70,7 +70,12 @@ def l2_on_data_grid(model, x, t, U):
     return float(tdq.find_L2_error(u_pred, U.T.flatten()[:, None])), X_star, u_pred, f_pred
 
 
-def report(name, res, quiet=False):
+def report(name, res, quiet=False, model=None):
+    """Print (unless quiet) and return ``res``; with ``model``, also which engine ran its loss
+    (``hip`` = the fused MI355X kernels, ``jet`` = torch Taylor jets, ``autograd``)."""
+    if model is not None:
+        prog = model.program()
+        res["backend"] = prog.backend
     if not quiet:
         print(f"[{name}] " + ", ".join(f"{k}={v:.4e}" if isinstance(v, float) else f"{k}={v}"
                                        for k, v in res.items()))

@@ -50,7 +50,7 @@ def main(argv=None):
     model.fit(tf_iter=args.iters, newton_iter=args.newton)
     err, *_ = l2_on_data_grid(model, x, t, U)
     data_err = float(np.sqrt(np.mean((model.predict(np.hstack([x_s, t_s]))[0] - y_s) ** 2)))
-    return report("burgers-assimilate", {"l2_error": err, "obs_rmse": data_err}, args.quiet)
+    return report("burgers-assimilate", {"l2_error": err, "obs_rmse": data_err}, args.quiet, model=model)
 
 
 if __name__ == "__main__":

@@ -54,7 +54,7 @@ def main(argv=None):
     u_star = ((np.sin(math.pi * X) * np.sin(math.pi * Y)) / (2 * math.pi ** 2)).flatten()[:, None]
     u_pred, _ = model.predict(X_star)
     return report("poisson", {"l2_error": float(tdq.find_L2_error(u_pred, u_star)),
-                              "loss": float(model.losses[-1]["Total Loss"])}, args.quiet)
+                              "loss": float(model.losses[-1]["Total Loss"])}, args.quiet, model=model)
 
 
 if __name__ == "__main__":

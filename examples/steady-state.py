@@ -48,7 +48,7 @@ def main(argv=None):
     u_star = (np.sin(math.pi * X) * np.sin(4 * math.pi * Y)).flatten()[:, None]
     u_pred, _ = model.predict(X_star)
     res = report("steady-state", {"l2_error": float(tdq.find_L2_error(u_pred, u_star)),
-                                  "loss": float(model.losses[-1]["Total Loss"])}, args.quiet)
+                                  "loss": float(model.losses[-1]["Total Loss"])}, args.quiet, model=model)
     if args.plot:
         tdq.plotting.plot_solution_domain1D(model, [x, x], ub=np.array([1.0, 1.0]), lb=np.array([-1.0, -1.0]),
                                             Exact_u=(np.sin(math.pi * X) * np.sin(4 * math.pi * Y)).T)

@@ -46,7 +46,7 @@ def main(argv=None):
     model.compile([3, 128, 128, 128, 128, 1], f_model, Domain, BCs, **solver_kw(args))
     model.fit(tf_iter=args.iters, newton_iter=args.newton)
     return report("testing-3d", {"loss": float(model.losses[-1]["Total Loss"]),
-                                 "terms": len(model.losses[-1]) - 1}, args.quiet)
+                                 "terms": len(model.losses[-1]) - 1}, args.quiet, model=model)
 
 
 if __name__ == "__main__":

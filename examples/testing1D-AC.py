@@ -38,7 +38,7 @@ def main(argv=None):
     model.fit(tf_iter=args.iters, newton_iter=args.newton)
     x, t, U = ac_data()
     err, *_ = l2_on_data_grid(model, x, t, U)
-    return report("testing1D-AC", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"])}, args.quiet)
+    return report("testing1D-AC", {"l2_error": err, "loss": float(model.losses[-1]["Total Loss"])}, args.quiet, model=model)
 
 
 if __name__ == "__main__":

@@ -68,7 +68,7 @@ def main(argv=None):
     x, t, U = ac_data()
     err, *_ = l2_on_data_grid(model, x, t, U)
     return report("transfer-learn", {"l2_error": err, "loss_stage1": losses[0], "loss_final": losses[-1]},
-                  args.quiet)
+                  args.quiet, model=model)
 
 
 if __name__ == "__main__":

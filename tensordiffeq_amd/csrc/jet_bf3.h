@@ -100,6 +100,28 @@ __device__ __forceinline__ f32x4 mfma_aa(const bf16x8& ah, const bf16x8& al, con
   return mfma_bf(ah, bh, c);
 }
 
+// "Wide" plans: streams x width tiles > 32 (e.g. a 2-D Laplacian at width 128: 5 streams; the 3-D
+// mixed-derivative periodic model of the reference's examples/testing.py: 7 streams).  Their
+// activation fragments (S * WT / 2 bf16x8 per lane, twice that under LO) plus two accumulator sets
+// do not fit the 256 VGPRs of two waves per SIMD, so wide kernels run ONE wave per SIMD with the
+// whole 512-entry VGPR + AGPR file (MFMA A/B operands may live in AGPRs on gfx950), and the
+// backward keeps 4-wave workgroups.  Under LO (bf16x3) the wave-private fragment stage (S * WT * 512
+// bytes per wave: 224 KiB per workgroup at S = 7) no longer fits the 160 KiB LDS, so it moves to a
+// wave-private region of global scratch (L2-resident: every wave writes its own lines and reads
+// them back after an s_waitcnt), leaving the LDS to the backward's dK images.
+__host__ __device__ constexpr bool bf3_wide(int WT, int S) { return S * WT > 32; }
+__host__ __device__ constexpr int bf3_wpe(int WT, int S, bool lo) { return (lo || bf3_wide(WT, S)) ? 1 : 2; }
+__host__ __device__ constexpr bool bf3_gstage(int WT, int S, bool lo) { return lo && bf3_wide(WT, S); }
+// bf16x4 entries of one wave's fragment stage ([s][kb][hl][lane][2 halves])
+__host__ __device__ constexpr int stage_wave_elems(int WT, int S, bool lo) { return S * (WT / 2) * (lo ? 2 : 1) * 128; }
+
+// the wave's own stage writes have landed before it reads them back (global stage only; an LDS
+// stage is ordered by program order)
+template <bool G>
+__device__ __forceinline__ void stage_fence() {
+  if constexpr (G) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // hi = rne_bf16(x), lo = rne_bf16(x - hi), two values per v_cvt_pk_bf16_f32
 __device__ __forceinline__ void split4(const f32x4 v, bf16x4& hi, bf16x4& lo) {
   u32x2 H, L;
@@ -592,7 +614,8 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (!LAST) {  // wave-private region: program order suffices
+  if (!LAST) {  // wave-private region: program order suffices (LDS) / a vmcnt wait (global stage)
+    stage_fence<bf3_gstage(WT, S, LO)>();
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -604,9 +627,10 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
 }
 
 template <int WT, int S, int NSO, bool LO>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LO ? 1 : 2, LO ? 1 : 2)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(bf3_wpe(WT, S, LO), bf3_wpe(WT, S, LO))))
 jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
-                   float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r) {
+                   float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r,
+                   bf16x4* __restrict__ gstage) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -619,7 +643,9 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const int Lh = d.n_hidden;
   // wave-private staging image of the next layer's B fragments: [s][kb][hl][lane][2 halves]
   constexpr int HL = LO ? 2 : 1;
-  bf16x4* stage = reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * HL * 64 * 2);
+  bf16x4* stage = bf3_gstage(WT, S, LO)
+                      ? gstage + (size_t)(wg * 4 + w) * stage_wave_elems(WT, S, LO)
+                      : reinterpret_cast<bf16x4*>(lds_raw) + (size_t)w * (S * KB * HL * 64 * 2);
   const float* Ko = aux + aux_ko(d, W);
 
   TDQ_TS(0);
@@ -826,14 +852,17 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
 #ifndef TDQ_BWD_WIDE
 #define TDQ_BWD_WIDE 1
 #endif
-__host__ __device__ constexpr int bwd_waves(int WT, bool lo) { return (TDQ_BWD_WIDE && !lo && WT >= 4) ? 8 : 4; }
+// (wide plans: 4 waves - an 8-wave workgroup puts two waves on each SIMD, 256 registers each)
+__host__ __device__ constexpr int bwd_waves(int WT, bool lo, int S) {
+  return (TDQ_BWD_WIDE && !lo && WT >= 4 && !bf3_wide(WT, S)) ? 8 : 4;
+}
 
 template <int WT, int S, int NSO, bool LO>
-__global__ void __launch_bounds__(64 * bwd_waves(WT, LO))
-__attribute__((amdgpu_waves_per_eu(LO ? 1 : 2, LO ? 1 : 2)))
+__global__ void __launch_bounds__(64 * bwd_waves(WT, LO, S))
+__attribute__((amdgpu_waves_per_eu(bf3_wpe(WT, S, LO), bf3_wpe(WT, S, LO))))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
-                   int Ptot, NetDims d, JetSpec sp, int rev, int h0r) {
+                   int Ptot, NetDims d, JetSpec sp, int rev, int h0r, bf16x4* __restrict__ gstage) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int W = 16 * WT;
   constexpr int KB = WT / 2;
@@ -850,7 +879,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #else
   constexpr int CHUNK_SWZ = 1;
 #endif
-  constexpr int NWV = bwd_waves(WT, LO), PTS = 16 * NWV;  // waves / points per workgroup
+  constexpr int NWV = bwd_waves(WT, LO, S), PTS = 16 * NWV;  // waves / points per workgroup
+  constexpr bool GST = bf3_gstage(WT, S, LO);                 // zb stage in global scratch
   constexpr int RS = 144;
   constexpr int IMG = PTS * RS;
   // dK tile ownership: the WT x WT output tiles split into (NWV/2) x 2 blocks, wave w owns block
@@ -867,7 +897,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   constexpr bool DBUF = !LO;
   constexpr int IBUF = 2 * HL * IMG;          // one buffer's images, in bf16
   constexpr int U1 = (DBUF ? 2 : 1) * IBUF / 2;  // images, in floats
-  constexpr int U2 = NWV * S * WT * HL * 128;  // per-wave zb fragment stages (bf16 hi(/lo))
+  constexpr int U2 = GST ? 0 : NWV * S * WT * HL * 128;  // per-wave zb fragment stages (bf16 hi(/lo))
   constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
   static_assert(NWV * (W * TDQ_MAXO + TDQ_MAXO + TDQ_MAXD * W) <= U, "partials must fit the union");
   __bf16* img = reinterpret_cast<__bf16*>(lds);
@@ -896,7 +926,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   constexpr bool SH = slab_half(LO);
   using ST = typename SlabType<SH>::T;
   ST* gs = reinterpret_cast<ST*>(slab) + (size_t)wg * Ptot;
-  bf16x4* stage = reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * HL * 64 * 2);
+  bf16x4* stage = GST ? gstage + (size_t)(wg * NWV + w) * stage_wave_elems(WT, S, LO)
+                      : reinterpret_cast<bf16x4*>(lds) + (size_t)w * (S * KB * HL * 64 * 2);
   auto dw_row = [](int wv, int r) { return NR * (wv >> 1) + r; };
   auto dw_col = [](int wv, int c) { return NC * (wv & 1) + c; };
   // transposed-read lane address inside a 4 x 16 block: row (l & 15) >> 2, column 4 (l & 3)
@@ -1146,6 +1177,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     if (i >= 2) {
       bwd_hidden_d<WT, S, NSO, LO, false>(zh, zl, Ki, Hp, stage, accB + ((i - 1) & 1) * NWV * W, accK0, xrow, sp, d, aux,
                                       h0r != 0, w, l, p, g);
+      stage_fence<GST>();
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -1187,7 +1219,9 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 // ------------------------------------------------------------------------------------------
 // host-side launch templates (instantiated per width class in jet_bf3_w{2,4,8}.hip)
 // ------------------------------------------------------------------------------------------
-inline size_t fwd_bf3_lds(int WT, int S, bool lo) { return (size_t)2 * S * WT * 1024 * (lo ? 2 : 1); }
+inline size_t fwd_bf3_lds(int WT, int S, bool lo) {
+  return bf3_gstage(WT, S, lo) ? 0 : (size_t)2 * S * WT * 1024 * (lo ? 2 : 1);
+}
 
 // backward tile order: reverse (default) or dispatch order (TDQ_BWD_ORDER=forward, for A/B runs)
 inline int bwd_reverse_order() {
@@ -1209,8 +1243,9 @@ inline int h0_recompute() {
 }
 
 inline size_t bwd_bf3_lds(int WT, int S, bool lo) {
-  const int W = 16 * WT, hl = lo ? 2 : 1, nwv = bwd_waves(WT, lo);
-  const size_t u1 = (size_t)(lo ? 1 : 2) * (2 * hl * 16 * nwv * 144) / 2, u2 = (size_t)nwv * S * WT * hl * 128;
+  const int W = 16 * WT, hl = lo ? 2 : 1, nwv = bwd_waves(WT, lo, S);
+  const size_t u1 = (size_t)(lo ? 1 : 2) * (2 * hl * 16 * nwv * 144) / 2,
+               u2 = bf3_gstage(WT, S, lo) ? 0 : (size_t)nwv * S * WT * hl * 128;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
   return (u + 3 * nwv * W) * sizeof(float);
 }
@@ -1228,6 +1263,7 @@ struct Bf3Args {
   JetSpec sp;
   hipStream_t st;
   int lo;            // 1: bf16x3 (operands hi + lo), 0: bf16 (operands rounded to bf16)
+  bf16x4* gstage;    // wide bf16x3 plans: global fragment stage (bf3_gstage), else unused
 };
 
 template <int WT, int S, int NSO, bool LO>
@@ -1241,7 +1277,7 @@ int launch_fwd_bf3_lo(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
-                     a.Hs, a.N, a.d, a.sp, h0_recompute());
+                     a.Hs, a.N, a.d, a.sp, h0_recompute(), a.gstage);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -1253,7 +1289,7 @@ int launch_fwd_bf3(const Bf3Args& a) {
 
 template <int WT, int S, int NSO, bool LO>
 int launch_bwd_bf3_lo(const Bf3Args& a) {
-  constexpr int NWV = bwd_waves(WT, LO);
+  constexpr int NWV = bwd_waves(WT, LO, S);
   const int nwg = (a.N + 16 * NWV - 1) / (16 * NWV);
   const size_t lds = bwd_bf3_lds(WT, S, LO);
   static bool attr = false;
@@ -1263,7 +1299,7 @@ int launch_bwd_bf3_lo(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(64 * NWV), lds, a.st, a.X, a.aux, a.img, a.dJ,
-                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute());
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute(), a.gstage);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -325,8 +325,11 @@ int launch_pack(const float* P, bf16x8* fimg, bf16x8* bimg, float* aux, NetDims 
   return 0;
 }
 
+// S <= 8 streams at every width class (S * WT <= 32: the 2-waves-per-SIMD kernels; beyond: the
+// "wide" one-wave-per-SIMD kernels of jet_bf3.h)
 bool bf3_ok(int WT, int S, int d_in, int d_out, int n_hidden) {
-  return (WT == 2 || WT == 4 || WT == 8) && S * WT <= 32 && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO && n_hidden >= 1;
+  return (WT == 2 || WT == 4 || WT == 8) && S >= 1 && S <= TDQ_MAXS && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO &&
+         n_hidden >= 1;
 }
 
 int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
@@ -342,13 +345,16 @@ int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
 
 extern "C" {
 
-// scratch = saved post-activations Hs | forward A image | backward A image | aux image (floats;
-// -1: unsupported).  The forward packs all three images in one launch; the backward reuses them.
-int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int S) {
+// scratch = saved post-activations Hs | forward A image | backward A image | aux image | (wide
+// bf16x3 plans) the global fragment stage (floats; -1: unsupported).  The forward packs all three
+// images in one launch; the backward reuses them.
+int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int S, int lo) {
   const int WT = width_tiles(width);
   if (WT < 2) return -1;
   const int64_t nwg = (N + 63) / 64;
-  return (int64_t)n_hidden * nwg * S * 4 * WT * 256 + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT);
+  const int64_t stage = bf3_gstage(WT, S, lo != 0) ? nwg * 4 * stage_wave_elems(WT, S, true) * 2 : 0;
+  return (int64_t)n_hidden * nwg * S * 4 * WT * 256 + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT) +
+         stage;
 }
 
 // per-workgroup gradient slabs + reduction partials, in floats
@@ -367,6 +373,14 @@ static inline void scratch_images(float* scratch, int N, int n_hidden, int S, in
   *img = scratch + (int64_t)n_hidden * nwg * S * 4 * WT * 256;
   *bimg = *img + img_floats(WT, n_hidden);
   *aux = *bimg + img_floats(WT, n_hidden);
+}
+
+// the global fragment stage of a wide bf16x3 plan (after the aux image), else nullptr
+static inline bf16x4* scratch_stage(float* scratch, int N, int d_in, int n_hidden, int S, int WT, int lo) {
+  if (!bf3_gstage(WT, S, lo != 0)) return nullptr;
+  float *img, *bimg, *aux;
+  scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+  return reinterpret_cast<bf16x4*>(aux + aux_alloc(d_in, n_hidden, 16 * WT));
 }
 
 // lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16).
@@ -388,7 +402,8 @@ int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch,
     int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
     if (rc) return rc;
   }
-  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo};
+  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
+            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo)};
   return dispatch(true, WT, S, nso, a);
 }
 
@@ -420,7 +435,7 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
   const int chunks = slab_chunks(nwg_b);
   float* slab = work;
@@ -431,7 +446,7 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   (void)img;
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), slab, N,
-            slab_stride(Ptot), d, sp, st, lo};
+            slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo)};
   int rc = dispatch(false, WT, S, nso, a);
   if (rc || !reduce) return rc;
   return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, chunks, (int)slab_half(lo != 0), stream);
@@ -463,7 +478,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
   args.grp[0].g = grad;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   float* part = work + (size_t)nwg_b * Pst;
   TailBook tb;
@@ -507,16 +522,15 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
 // Data-parallel step, first half (before the all-reduce): slab pass 1 + the loss reduction in one
 // launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad.  total
 // (optional): also the summed loss - the L-BFGS objective writes [grad | loss] in place this way.
-int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int d_out, int n_hidden, int lo,
+int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
                       float* total, void* stream) {
   const int WT = width_tiles(width);
-  // the S-independent part of the geometry check of the sibling entry points (one stream)
-  if (!bf3_ok(WT, 1, d_in, d_out, n_hidden) || N < 1 || n_lblocks < 0 || n_terms < 0 || n_scal < 0)
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1 || n_lblocks < 0 || n_terms < 0 || n_scal < 0)
     return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d_in, width, d_out, n_hidden);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0), nwg_b = (N + pts_b - 1) / pts_b;
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   float* part = work + (size_t)nwg_b * Pst;
   TailBook tb{};

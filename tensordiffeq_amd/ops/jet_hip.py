@@ -32,7 +32,8 @@ def stream_spec(plan):
 def _fns(lib, cfg):
     if cfg["precision"] in ("bf16x3", "bf16"):
         return (lib.tdq_jet_fwd_bf3, lib.tdq_jet_bwd_bf3,
-                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["d_in"], cfg["width"], cfg["n_hidden"], cfg["S"]),
+                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["d_in"], cfg["width"], cfg["n_hidden"], cfg["S"],
+                                                         *_lo_args(cfg)),
                 lambda N: lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
     return (lib.tdq_jet_fwd, lib.tdq_jet_bwd,
             lambda N: lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], cfg["S"], 0),
@@ -167,7 +168,7 @@ def dp_tail_a(saved, work, grad, fop, total=None):
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
-                               cfg["n_hidden"], *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
+                               cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
                                fop.n_scal, _lib.ptr(fop.losses), _lib.ptr(fop.dscal), _lib.ptr(total),
                                _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")

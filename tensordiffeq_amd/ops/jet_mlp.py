@@ -78,8 +78,6 @@ def hip_config(net, plan, precision=None):
             WT = 8
         else:
             raise ValueError("hidden width > 128")
-    if S * WT > 32:
-        raise ValueError(f"streams x width tiles = {S * WT} > 32 (register budget)")
     if d_in > 8 or d_out > 4:
         raise ValueError("input width > 8 or output width > 4")
     precision = precision or _precision
@@ -87,6 +85,11 @@ def hip_config(net, plan, precision=None):
         raise ValueError(f"precision {precision!r} not in {PRECISIONS}")
     if precision in ("bf16x3", "bf16") and WT < 2:
         precision = "fp32"
+    # split-bf16 kernels: any S <= 8 at every width class (S x WT > 32: the one-wave-per-SIMD
+    # "wide" kernels, csrc/jet_bf3.h); the exact-fp32 family keeps the 2-wave register budget
+    if precision == "fp32" and S * WT > 32:
+        raise ValueError(f"fp32 kernels: streams x width tiles = {S * WT} > 32 (register budget); "
+                         f"use precision bf16x3 or bf16")
     return {"d_in": d_in, "d_out": d_out, "width": hidden[0], "WT": WT, "S": S,
             "n_hidden": len(hidden), "precision": precision}
 

@@ -1,5 +1,7 @@
 """Every ported example on the MI355X (a few iterations each): the run finishes with finite
-numbers, and where the example reports its backend, the HIP kernels were used."""
+numbers and its loss ran on the HIP kernels (every example reports its backend; none uses a
+custom network, so "hip" is required everywhere - incl. the 3-D testing.py plan with 7 jet
+streams, a "wide" kernel plan)."""
 import importlib.util
 import math
 import os
@@ -40,5 +42,4 @@ def test_example_runs_on_gpu(name, monkeypatch):
     for k, v in res.items():
         if isinstance(v, float):
             assert math.isfinite(v), (name, k, v)
-    if "backend" in res:
-        assert res["backend"] == "hip", (name, res["backend"])
+    assert res.get("backend") == "hip", (name, res.get("backend"))

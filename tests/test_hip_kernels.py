@@ -32,6 +32,12 @@ CASES = [
     ([2, 128, 1], [], 70),                                          # value only, 1 hidden layer
     ([2, 128, 128, 128, 1], [(0,), (1,)], 64),                     # first order only
     ([3, 40, 40, 40, 1], [(0, 0), (1, 1), (2, 2), (0, 1)], 257),    # S=8, WT=4... (S*WT=32)
+    # "wide" plans (S * WT > 32): one wave per SIMD; bf16x3 stages fragments in global scratch
+    ([2, 128, 128, 128, 128, 1], [(0, 0), (1, 1)], 1000),          # 2-D Laplacian at width 128, S=5
+    ([3, 128, 128, 128, 128, 1], [(0,), (1,), (2,), (0, 0), (1, 1), (0, 1)], 777),  # testing.py, S=7
+    ([3, 96, 96, 96, 1], [(0, 0), (1, 1), (2, 2), (0, 1)], 300),   # S=8, padded WT=8
+    ([2, 128, 128, 1], [(0, 0), (1, 1), (0, 1)], 200),             # S=6, 2 hidden layers
+    ([4, 128, 128, 128, 1], [(0,), (1,), (2,), (3,)], 150),         # S=5, first order only
 ]
 
 
@@ -60,6 +66,7 @@ def test_jet_forward_matches_torch(sizes, reqs, N, prec):
     assert J.shape == Jref.shape
     scale = Jref.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
     err = ((J.double() - Jref).abs() / scale).max().item()
+    print(f"KERNEL_ERR fwd {prec} {sizes} S={plan.S} {err:.3e}")
     assert err < TOL_FWD[prec], err
 
 
@@ -104,6 +111,7 @@ def test_jet_backward_matches_autograd(sizes, reqs, N, prec):
     (Jr * G).sum().backward()
     g_ref = p64.grad
     rel = ((g_hip - g_ref).norm() / g_ref.norm()).item()
+    print(f"KERNEL_ERR bwd {prec} {sizes} S={plan.S} {rel:.3e}")
     assert rel < TOL_BWD[prec], rel
     # every parameter block (per-layer kernels and biases) individually, not just the norm
     off = 0
@@ -330,7 +338,7 @@ def test_step_book_and_adam_snapshot_match_torch():
     assert torch.allclose(a[2].cpu(), b[2], rtol=1e-5, atol=1e-6)
 
 
-def _ac_sa_model(prec, n_f=3000):
+def _ac_sa_model(prec, n_f=3000, sizes=(2, 128, 128, 128, 128, 1)):
     import math
     import numpy as np
     import tensordiffeq_amd as tdq
@@ -352,7 +360,7 @@ def _ac_sa_model(prec, n_f=3000):
 
     m = tdq.CollocationSolverND(verbose=False)
     g = torch.Generator().manual_seed(1)
-    m.compile([2, 128, 128, 128, 128, 1], f_model, D,
+    m.compile(list(sizes), f_model, D,
               [IC(D, [lambda x: x ** 2 * np.cos(math.pi * x)], var=[["x"]]), periodicBC(D, ["x"], [deriv_model])],
               Adaptive_type="self-adaptive", dict_adaptive={"residual": [True], "BCs": [True, False]},
               init_weights={"residual": [torch.rand(n_f, 1, generator=g)],
@@ -361,15 +369,52 @@ def _ac_sa_model(prec, n_f=3000):
     return m
 
 
+def _poisson_model(prec, n_f=3000, sizes=(2, 128, 128, 128, 128, 1)):
+    """2-D Poisson u_xx + u_yy = -2 pi^2 sin(pi x) sin(pi y), zero Dirichlet on the unit square:
+    5 jet streams - at width 128 a "wide" plan."""
+    import math
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.boundaries import DomainND, dirichletBC
+    tdq.set_seed(0)
+    D = DomainND(["x", "y"])
+    D.add("x", [0.0, 1.0], 101)
+    D.add("y", [0.0, 1.0], 101)
+    D.generate_collocation_points(n_f)
+
+    def f_model(u_model, x, y):
+        u = u_model(torch.cat([x, y], 1))
+        u_xx = tdq.grad(tdq.grad(u, x), x)
+        u_yy = tdq.grad(tdq.grad(u, y), y)
+        return u_xx + u_yy + 2 * math.pi ** 2 * torch.sin(math.pi * x) * torch.sin(math.pi * y)
+
+    bcs = [dirichletBC(D, val=0.0, var=v, target=t) for v in ("x", "y") for t in ("upper", "lower")]
+    m = tdq.CollocationSolverND(verbose=False)
+    m.compile(list(sizes), f_model, D, bcs, backend="hip", device="cuda", precision=prec)
+    return m
+
+
+TAIL_GEOMS = [
+    ("ac", (2, 128, 128, 128, 128, 1)),   # flagship: WT=8, width == W
+    ("ac", (2, 20, 20, 20, 1)),           # WT=2, padded width
+    ("ac", (2, 50, 50, 1)),               # WT=4, padded (bf16: 8-wave backward)
+    ("ac", (2, 32, 1)),                   # one hidden layer
+    ("poisson", (2, 128, 128, 128, 128, 1)),  # wide plan (S=5)
+]
+
+
+@pytest.mark.parametrize("problem,sizes", TAIL_GEOMS)
 @pytest.mark.parametrize("prec", ["bf16", "bf16x3"])
-def test_fused_step_tail_matches_unfused(prec, monkeypatch):
+def test_fused_step_tail_matches_unfused(prec, problem, sizes, monkeypatch):
     """The two-launch step tail (slab + loss reduction + bookkeeping, then reduction fused into
     Adam with the weight images rewritten in place) reproduces the seven-launch step bit for bit:
     parameters, SA weights, loss history, best loss / epoch / weights - across two fit() calls
-    with the parameters changed in between (the images are re-packed before the first replay)."""
+    with the parameters changed in between (the images are re-packed before the first replay).
+    Geometries: every width class incl. padded widths, one hidden layer, a wide plan."""
+    build = _ac_sa_model if problem == "ac" else _poisson_model
+
     def run(fused_tail):
         monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
-        m = _ac_sa_model(prec)
+        m = build(prec, sizes=sizes)
         m.fit(tf_iter=25)
         with torch.no_grad():
             m.u_model.flat.mul_(0.97)
@@ -377,6 +422,7 @@ def test_fused_step_tail_matches_unfused(prec, monkeypatch):
         return m
 
     a = run(True)
+    assert a._get_engine(None, 1)._tail_eligible()
     b = run(False)
     assert torch.equal(a.u_model.flat, b.u_model.flat)
     for x, y in zip(a.lambdas, b.lambdas):
@@ -391,13 +437,54 @@ def test_fused_step_tail_matches_unfused(prec, monkeypatch):
     assert (u1 == u2).all()
 
 
-@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
-def test_fused_lbfgs_objective_matches_unfused(prec, monkeypatch):
-    """The L-BFGS objective writing ``[grad | loss]`` in place through the fused tail gives the same
-    device L-BFGS trajectory, bit for bit, as the loss-reduce / total / slab / concatenate path."""
+@pytest.mark.parametrize("prec", ["bf16", "bf16x3"])
+def test_fused_step_tail_discovery_matches_unfused(prec, monkeypatch):
+    """DiscoveryModel (PDE coefficients as extra scalars through dscal, SA collocation weights)
+    with and without the fused step tail: identical trajectories."""
+    import numpy as np
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.models import DiscoveryModel
+
     def run(fused_tail):
         monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
-        m = _ac_sa_model(prec)
+        tdq.set_seed(0)
+        rng = np.random.default_rng(0)
+        X = rng.uniform(-1, 1, (2000, 2)).astype(np.float32)
+        X[:, 1] = (X[:, 1] + 1) / 2
+        u = (X[:, :1] ** 2 * np.cos(np.pi * X[:, :1])).astype(np.float32)
+        params = [tdq.Variable(0.0), tdq.Variable(0.0)]
+
+        def f_model(u_model, var, x, t):
+            uu = u_model(torch.cat([x, t], 1))
+            u_xx = tdq.grad(tdq.grad(uu, x), x)
+            return tdq.grad(uu, t) - var[0] * u_xx + var[1] * uu * uu * uu - var[1] * uu
+
+        m = DiscoveryModel(verbose=False)
+        m.compile([2, 64, 64, 64, 1], f_model, [X[:, :1], X[:, 1:]], u, params,
+                  col_weights=torch.rand(2000, 1, generator=torch.Generator().manual_seed(0)),
+                  backend="hip", device="cuda", precision=prec)
+        m.fit(tf_iter=30)
+        return m
+
+    a = run(True)
+    b = run(False)
+    assert torch.equal(a.u_model.flat, b.u_model.flat)
+    for x, y in zip(a.vars, b.vars):
+        assert torch.equal(x, y)
+    assert torch.equal(a.col_weights, b.col_weights)
+
+
+@pytest.mark.parametrize("problem,sizes", [("ac", (2, 128, 128, 128, 128, 1)), ("ac", (2, 20, 20, 20, 1)),
+                                           ("poisson", (2, 128, 128, 128, 128, 1))])
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+def test_fused_lbfgs_objective_matches_unfused(prec, problem, sizes, monkeypatch):
+    """The L-BFGS objective writing ``[grad | loss]`` in place through the fused tail gives the same
+    device L-BFGS trajectory, bit for bit, as the loss-reduce / total / slab / concatenate path."""
+    build = _ac_sa_model if problem == "ac" else _poisson_model
+
+    def run(fused_tail):
+        monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
+        m = build(prec, sizes=sizes)
         m.fit(tf_iter=5, newton_iter=30)
         return m
 
