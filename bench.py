@@ -125,6 +125,12 @@ def time_steps(eng, ctx, device, steps, warmup, min_warmup_s):
         eng.run(max(10, warmup))
         n_warm += max(10, warmup)
         sync()
+    # room in the device loss history for the timed steps: a re-allocation would re-capture the
+    # step graph inside the timed region; one more (untimed) step replays the final graph
+    eng._ensure_hist(steps + 2)
+    eng.run(1)
+    n_warm += 1
+    sync()
     warm_s = time.perf_counter() - t_w
     ctx.barrier()
     sync()
@@ -191,7 +197,8 @@ def main(argv=None):
     ap.add_argument("--acc-iters", type=int, default=10000)
     ap.add_argument("--acc-newton", type=int, default=10000)
     ap.add_argument("--newton-precision", default="bf16x3")
-    ap.add_argument("--lbfgs-stop", default=None, choices=["fixed", "legacy"])
+    ap.add_argument("--lbfgs-stop", default=None, choices=["fixed", "legacy"],
+                    help="L-BFGS function-change test (default: the library's, legacy = the reference's)")
     ap.add_argument("--force-dp", action="store_true",
                     help="also time the DP step at world 1 (RCCL process group, single GPU only)")
     ap.add_argument("--precision", default="bf16", choices=["bf16x3", "bf16", "fp32"],

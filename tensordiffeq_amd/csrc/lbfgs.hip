@@ -90,14 +90,30 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
     for (int q = 0; q < NV; ++q) v[q] = ((red[q] + red[NV + q]) + red[2 * NV + q]) + red[3 * NV + q];
 }
 
+// partial loads of the fused kernels' last-arriving block: relaxed agent-scope atomics = sc1 loads
+// that bypass this CU's L1 (the producers stored with sc1, MI355X_MICROARCH.md hand-off table)
+template <bool SC1>
+__device__ __forceinline__ double part_ld(const double* p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <bool SC1>
+__device__ __forceinline__ void part_st(double* p, double v) {
+  if constexpr (SC1)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
 __device__ __forceinline__ bool slot_valid(int i, int head, int k, int m) { return ((i - head + m) % m) < k; }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) lbfgs_dots_kernel(const float* __restrict__ fg, const float* __restrict__ g_old,
-                                                         const float* __restrict__ d, const float* __restrict__ S,
-                                                         const float* __restrict__ Y, const double* __restrict__ st,
-                                                         double* __restrict__ part, LbCfg c) {
-  __shared__ double red[4 * LB_NF];
+// the partial sums of one (chunk, slot) block of the dots grid -> part (thread 0 stores them)
+template <bool SC1>
+__device__ __forceinline__ void lbfgs_dots_body(const float* __restrict__ fg, const float* __restrict__ g_old,
+                                                const float* __restrict__ d, const float* __restrict__ S,
+                                                const float* __restrict__ Y, const double* __restrict__ st,
+                                                double* __restrict__ part, const LbCfg& c, double* red) {
   const int i = blockIdx.y, ch = blockIdx.x;
   const int lo = (int)(((long long)c.p * ch) / c.nchunks), hi = (int)(((long long)c.p * (ch + 1)) / c.nchunks);
   const float tf = (float)st[LB_T];
@@ -134,18 +150,26 @@ __global__ void __launch_bounds__(256) lbfgs_dots_kernel(const float* __restrict
   if (threadIdx.x == 0) {
     double* o = part + ((size_t)ch * (c.m + 1) + i) * LB_NF;
 #pragma unroll
-    for (int q = 0; q < LB_NF; ++q) o[q] = a[q];
+    for (int q = 0; q < LB_NF; ++q) part_st<SC1>(&o[q], a[q]);
   }
+}
+
+__global__ void __launch_bounds__(256) lbfgs_dots_kernel(const float* __restrict__ fg, const float* __restrict__ g_old,
+                                                         const float* __restrict__ d, const float* __restrict__ S,
+                                                         const float* __restrict__ Y, const double* __restrict__ st,
+                                                         double* __restrict__ part, LbCfg c) {
+  __shared__ double red[4 * LB_NF];
+  lbfgs_dots_body<false>(fg, g_old, d, S, Y, st, part, c, red);
 }
 
 // ---------------------------------------------------------------------------------------------
 // dynamic LDS (doubles): dots[(m+1)*5] | Rc[m*m] | YYc[m*m] | aC[64] | bC[64] | uS[64] | pS[64]
-__global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restrict__ fg, const double* __restrict__ part,
-                                                          double* __restrict__ st, double* __restrict__ SY,
-                                                          double* __restrict__ YY, double* __restrict__ coef,
-                                                          float* __restrict__ fhist, LbCfg c) {
-  extern __shared__ __attribute__((aligned(16))) double lb_lds[];
-  __shared__ int flag[6];  // go, n_iter, pushed, slot, k, head
+template <bool SC1>
+__device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, const double* __restrict__ part,
+                                                 double* __restrict__ st, double* __restrict__ SY,
+                                                 double* __restrict__ YY, double* __restrict__ coef,
+                                                 float* __restrict__ fhist, const LbCfg& c, double* lb_lds,
+                                                 int* flag) {
   const int tid = threadIdx.x, m = c.m;
   double* dots = lb_lds;
   double* Rc = dots + (m + 1) * LB_NF;
@@ -154,19 +178,15 @@ __global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restric
   double* bC = aC + 64;
   double* uS = bC + 64;
   double* pS = uS + 64;
-  if (st[LB_ACTIVE] == 0.0) {
-    if (tid == 0) st[LB_BEST] = 0.0;
-    return;
-  }
   // 1. reduce the chunk partials (fixed order: deterministic)
   for (int v = tid; v < (m + 1) * LB_NF; v += 256) {
     double a0 = 0.0, a1 = 0.0;
     int ch = 0;
     for (; ch + 1 < c.nchunks; ch += 2) {
-      a0 += part[(size_t)ch * (m + 1) * LB_NF + v];
-      a1 += part[(size_t)(ch + 1) * (m + 1) * LB_NF + v];
+      a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
+      a1 += part_ld<SC1>(&part[(size_t)(ch + 1) * (m + 1) * LB_NF + v]);
     }
-    if (ch < c.nchunks) a0 += part[(size_t)ch * (m + 1) * LB_NF + v];
+    if (ch < c.nchunks) a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
     dots[v] = a0 + a1;
   }
   __syncthreads();
@@ -325,6 +345,19 @@ __global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restric
   if (tid == 0) coef[2 * m] = -gam;
 }
 
+__global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restrict__ fg, const double* __restrict__ part,
+                                                          double* __restrict__ st, double* __restrict__ SY,
+                                                          double* __restrict__ YY, double* __restrict__ coef,
+                                                          float* __restrict__ fhist, LbCfg c) {
+  extern __shared__ __attribute__((aligned(16))) double lb_lds[];
+  __shared__ int flag[6];  // go, n_iter, pushed, slot, k, head
+  if (st[LB_ACTIVE] == 0.0) {
+    if (threadIdx.x == 0) st[LB_BEST] = 0.0;
+    return;
+  }
+  lbfgs_logic_body<false>(fg, part, st, SY, YY, coef, fhist, c, lb_lds, flag);
+}
+
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) lbfgs_dir_kernel(const float* __restrict__ x, const float* __restrict__ fg,
                                                         float* __restrict__ g_old, float* __restrict__ d,
@@ -405,6 +438,139 @@ __global__ void __launch_bounds__(256) lbfgs_axpy_kernel(float* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused update: TWO launches per iteration instead of dots -> logic -> dir -> step -> axpy.
+//   lbfgs_dots_logic  the dots grid; every block stores its partials write-through (sc1), waits
+//                     for them, and draws a ticket (agent-scope atomic add); the block that draws
+//                     the last ticket runs the logic on the partials (sc1 loads) and re-arms the
+//                     ticket.  (Hand-off protocol: MI355X_MICROARCH.md, inter-workgroup table row 1.)
+//   lbfgs_dir_step    the direction pass, plus the step taken speculatively: t of the NEXT step
+//                     is known before g.d is (min(1, 1/|g|_1) on the first iteration, else the
+//                     fixed lr), so every element does x += t d right after computing d (old x
+//                     kept in x_prev); the last-ticket block reduces g.d / |d|_1 and runs the
+//                     descent test - in the rare stop case it restores x from x_prev, so the
+//                     trajectory is bit-identical to the five-launch path.
+// The order of every reduction is the five-launch path's: same values, bit for bit.
+__global__ void __launch_bounds__(256) lbfgs_dots_logic_kernel(const float* __restrict__ fg,
+                                                               const float* __restrict__ g_old,
+                                                               const float* __restrict__ d, const float* __restrict__ S,
+                                                               const float* __restrict__ Y, double* __restrict__ st,
+                                                               double* __restrict__ part, double* __restrict__ SY,
+                                                               double* __restrict__ YY, double* __restrict__ coef,
+                                                               float* __restrict__ fhist, int* __restrict__ ticket,
+                                                               LbCfg c) {
+  extern __shared__ __attribute__((aligned(16))) double lb_lds[];
+  __shared__ double red[4 * LB_NF];
+  __shared__ int flag[6];
+  __shared__ int last;
+  if (st[LB_ACTIVE] == 0.0) {  // every block sees the same value: only the last block changes it
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st[LB_BEST] = 0.0;
+    return;
+  }
+  lbfgs_dots_body<true>(fg, g_old, d, S, Y, st, part, c, red);
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's sc1 partial stores have landed
+    const int nb = (int)(gridDim.x * gridDim.y);
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == nb - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  lbfgs_logic_body<true>(fg, part, st, SY, YY, coef, fhist, c, lb_lds, flag);
+}
+
+__global__ void __launch_bounds__(256) lbfgs_dir_step_kernel(float* __restrict__ x, const float* __restrict__ fg,
+                                                             float* __restrict__ g_old, float* __restrict__ d,
+                                                             float* __restrict__ S, float* __restrict__ Y,
+                                                             float* __restrict__ best_x, float* __restrict__ x_prev,
+                                                             double* __restrict__ st, const double* __restrict__ coef,
+                                                             double* __restrict__ part2, int* __restrict__ ticket,
+                                                             LbCfg c) {
+  __shared__ double red[8];
+  __shared__ int last, stop;
+  const bool best = st[LB_BEST] != 0.0, active = st[LB_ACTIVE] != 0.0;
+  const int n_iter = (int)st[LB_NITER], pushed = (int)st[LB_PUSHED], slot = (int)st[LB_SLOT];
+  const int k = (int)st[LB_K], head = (int)st[LB_HEAD], m = c.m;
+  const float tf = (float)st[LB_T];
+  // the next step's length (the five-launch lbfgs_step_kernel's formula)
+  const double tnext = (n_iter == 1) ? fmin(1.0, 1.0 / st[LB_G1]) : c.lr;
+  const float tn = (float)tnext;
+  const double cG = coef[2 * m];
+  double acc[2] = {0.0, 0.0};
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < c.p; j += gridDim.x * 256) {
+    const float xj = x[j];
+    if (best) best_x[j] = xj;
+    if (!active) continue;
+    const float g = fg[j];
+    double dn = cG * g;
+    if (n_iter > 1) {
+      const float s = tf * d[j], y = g - g_old[j];
+      if (pushed) {
+        S[(size_t)slot * c.p + j] = s;
+        Y[(size_t)slot * c.p + j] = y;
+      }
+      for (int q = 0; q < k; ++q) {
+        const int i = (head + q) % m;
+        const bool nw = pushed && i == slot;
+        const double si = nw ? (double)s : (double)S[(size_t)i * c.p + j];
+        const double yi = nw ? (double)y : (double)Y[(size_t)i * c.p + j];
+        dn += coef[i] * si + coef[m + i] * yi;
+      }
+    }
+    const float df = (float)dn;
+    g_old[j] = g;
+    d[j] = df;
+    // speculative step, undone below if the descent test fails.  Both x stores are write-through
+    // (sc1): a plain store would leave a dirty line in this XCD's L2 whose write-back at kernel
+    // end could land after the last block's restore of the same element.
+    __hip_atomic_store(&x_prev[j], xj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&x[j], fmaf(tn, df, xj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    acc[0] += (double)g * df;
+    acc[1] += fabs((double)df);
+  }
+  if (!active) return;  // uniform: no ticket, nothing to reduce
+  block_sum<2>(acc, red);
+  if (threadIdx.x == 0) {
+    part_st<true>(&part2[2 * blockIdx.x], acc[0]);
+    part_st<true>(&part2[2 * blockIdx.x + 1], acc[1]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  double a2[2] = {0.0, 0.0};
+  for (int b = threadIdx.x; b < c.nblk; b += 256) {
+    a2[0] += part_ld<true>(&part2[2 * b]);
+    a2[1] += part_ld<true>(&part2[2 * b + 1]);
+  }
+  __syncthreads();  // red is reused
+  block_sum<2>(a2, red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double gtd = a2[0];
+    st[LB_GTD] = gtd;
+    stop = gtd > -c.tol_x;
+    if (stop) {  // cannot make progress along d (reference optimizers.py:224)
+      st[LB_ACTIVE] = 0.0;
+      st[LB_REASON] = (double)LB_R_GTD;
+    } else {
+      st[LB_T] = tnext;
+      st[LB_DT1] = a2[1] * tnext;
+      st[LB_FOLD] = st[LB_F];
+    }
+  }
+  __syncthreads();
+  if (stop) {  // undo the speculative step: x stays where the reference leaves it
+    // every block stored x_prev / x write-through and drained them before its ticket (vmcnt(0)
+    // above): sc1 loads see them, sc1 stores overwrite the speculative x in memory
+    for (int j = threadIdx.x; j < c.p; j += 256)
+      __hip_atomic_store(&x[j], __hip_atomic_load(&x_prev[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 extern "C" {
 
 int tdq_lbfgs_nst() { return LB_NST; }
@@ -436,6 +602,34 @@ int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, fl
                      c);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(lbfgs_step_kernel, dim3(1), dim3(256), 0, s, part2, st, c);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// The same update in two launches (lbfgs_dots_logic + lbfgs_dir_step, see above); it also takes
+// the step (no tdq_lbfgs_axpy).  ticket: 2 ints, zero on the first call (re-armed by the kernels);
+// x_prev: p floats.
+int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
+                           float* x_prev, double* st, double* SY, double* YY, double* coef, double* part, double* part2,
+                           float* fhist, int* ticket, int p, int m, int max_iter, int nchunks, int nblk, int fhist_len,
+                           double max_eval, double lr, double tol_fun, double tol_x, int legacy_stop, void* stream) {
+  if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
+  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m + 4 * 64) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgs_dots_logic_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(((LB_MAXM + 1) * LB_NF + 2 * LB_MAXM * LB_MAXM + 4 * 64) * sizeof(double)));
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(lbfgs_dots_logic_kernel, dim3(nchunks, m + 1), dim3(256), lds, s, fg, g_old, d, S, Y, st, part, SY,
+                     YY, coef, fhist, ticket, c);
+  TDQ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lbfgs_dir_step_kernel, dim3(nblk), dim3(256), 0, s, x, fg, g_old, d, S, Y, best_x, x_prev, st,
+                     coef, part2, ticket + 1, c);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -104,10 +104,14 @@ class AdamEngine:
         self.moments = [[o.state_for(t) for t in g.tensors] for o, g in zip(self.opts, self.groups)]
 
     def _ensure_hist(self, n):
+        """Room in the device loss history for ``n`` more steps.  A new buffer invalidates the
+        captured step (it writes its row through the buffer's address), so the history grows
+        geometrically: repeated short ``fit`` / ``run`` calls re-capture O(log steps) times."""
         st = self.state
         need = int(st["epoch_host"]) + int(n) + 1
         if st["hist"] is None or st["hist"].shape[0] < need:
-            new = torch.full((max(need, 16), 1 + len(self.term_names)), float("nan"),
+            old = 0 if st["hist"] is None else st["hist"].shape[0]
+            new = torch.full((max(need, 2 * old, 16), 1 + len(self.term_names)), float("nan"),
                              device=self.device)
             if st["hist"] is not None:
                 new[: st["hist"].shape[0]] = st["hist"]

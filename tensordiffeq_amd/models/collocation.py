@@ -478,7 +478,7 @@ class CollocationSolverND:
     def _fit_lbfgs_body(self, newton_iter, newton_eager):
         """Run L-BFGS; returns ``{"impl", "n_iter", "func_evals", "reason", "stop"}``."""
         ctx = self.dist_ctx
-        stop = getattr(getattr(self, "config", None), "lbfgs_stop", "fixed")
+        stop = getattr(getattr(self, "config", None), "lbfgs_stop", "legacy")
         if self.verbose and ctx.rank == 0:
             print("Starting L-BFGS training")
         eng = self._get_lbfgs_engine()

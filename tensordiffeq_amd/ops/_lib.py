@@ -58,6 +58,7 @@ def _declare(lib):
         "tdq_lbfgs_nst": (I, []),
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
+        "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

@@ -8,7 +8,11 @@ on the GPU and one iteration is a fixed sequence of kernel launches (``csrc/lbfg
 
     axpy(x += t d)  ->  evaluate fg = [grad | loss] at x  ->  [DP: all-reduce fg]  ->  update(fg)
 
-so the whole iteration is captured once as a HIP graph and replayed.  The host reads one flag
+so the whole iteration is captured once as a HIP graph and replayed.  By default the update is TWO
+launches (``tdq_lbfgs_update_fused``: dots + logic, then direction + descent test + the step
+itself, each finished by the block that draws the last ticket) instead of five (dots, logic,
+direction, step, axpy); ``TDQ_LBFGS_FUSED=0`` keeps the five-launch path - both give the same
+trajectory bit for bit (GPU test).  The host reads one flag
 every ``poll_every`` iterations instead of ~6 scalars per iteration (reference host syncs at
 optimizers.py:173,224,256-276,290); once a stopping test fires every kernel turns into a no-op,
 so replays past convergence change nothing.  Under DP every rank runs the identical deterministic
@@ -72,6 +76,8 @@ class DeviceLBFGS:
         self.native = x.is_cuda and _lib.available()
         if x.is_cuda and not self.native:
             _lib.require_on_gpu()
+        import os
+        self.fused = self.native and os.environ.get("TDQ_LBFGS_FUSED", "1") != "0"
         f32 = dict(device=dev, dtype=torch.float32)
         f64 = dict(device=dev, dtype=torch.float64)
         self.g_old = torch.zeros(p, **f32)
@@ -88,6 +94,8 @@ class DeviceLBFGS:
         self.part = torch.zeros(self.nchunks * (self.m + 1) * 5, **f64)
         self.part2 = torch.zeros(2 * self.nblk, **f64)
         self.fhist = torch.full((self.max_iter + 1,), float("nan"), **f32) if record_history else None
+        self.x_prev = torch.empty(p, **f32) if self.fused else None
+        self.ticket = torch.zeros(2, dtype=torch.int32, device=dev) if self.fused else None
         self.reset()
 
     def reset(self):
@@ -115,6 +123,18 @@ class DeviceLBFGS:
             raise ValueError(f"fg must be a contiguous float32 vector of {self.p + 1} elements")
         if fg.device != self.x.device:
             raise ValueError("fg and x must live on the same device")
+        if self.fused:
+            lib = _lib.load()
+            rc = lib.tdq_lbfgs_update_fused(
+                _lib.ptr(self.x), _lib.ptr(fg), _lib.ptr(self.g_old), _lib.ptr(self.d), _lib.ptr(self.S),
+                _lib.ptr(self.Y), _lib.ptr(self.best_x), _lib.ptr(self.x_prev), _lib.ptr(self.st), _lib.ptr(self.SY),
+                _lib.ptr(self.YY), _lib.ptr(self.coef), _lib.ptr(self.part), _lib.ptr(self.part2),
+                _lib.ptr(self.fhist), _lib.ptr(self.ticket),
+                self.p, self.m, self.max_iter, self.nchunks, self.nblk,
+                0 if self.fhist is None else self.fhist.numel(), self.max_eval, self.lr, self.tol_fun,
+                self.tol_x, 1 if self.stop == "legacy" else 0, _lib.stream_ptr(self.x.device))
+            _lib.check(rc, "tdq_lbfgs_update_fused")
+            return
         if self.native:
             lib = _lib.load()
             rc = lib.tdq_lbfgs_update(
@@ -130,7 +150,10 @@ class DeviceLBFGS:
             self._update_torch(fg)
 
     def axpy(self):
-        """``x += t d`` (no-op once stopped)."""
+        """``x += t d`` (no-op once stopped; also a no-op on the fused path, whose update already
+        took the step)."""
+        if self.fused:
+            return
         if self.native:
             lib = _lib.load()
             rc = lib.tdq_lbfgs_axpy(_lib.ptr(self.x), _lib.ptr(self.d), _lib.ptr(self.st), self.p,

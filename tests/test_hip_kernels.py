@@ -17,8 +17,12 @@ pytestmark = pytest.mark.gpu
 # max error relative to each stream's scale (forward) / relative gradient norm (backward).
 # bf16x3: every GEMM product carries ~2^-16 relative error (split-bf16 MFMA, csrc/jet_bf3.hip);
 # bf16: weights and activations rounded to bf16 (2^-9 relative), fp32 accumulation.
-TOL_FWD = {"fp32": 2e-5, "bf16x3": 2e-4, "bf16": 8e-2}
-TOL_BWD = {"fp32": 5e-5, "bf16x3": 5e-4, "bf16": 1e-2}
+# Bounds are ~2-3x the largest error measured over CASES on MI355X (profiles/r3_kernel_errors.txt:
+# fwd fp32 3.1e-6, bf16x3 1.0e-4, bf16 3.3e-2 (4.7e-2 for the 8-hidden-layer Burgers net);
+# bwd fp32 4.7e-7, bf16x3 8.3e-6, bf16 5.5e-3).
+TOL_FWD = {"fp32": 8e-6, "bf16x3": 2.5e-4, "bf16": 8e-2}
+TOL_BWD = {"fp32": 1.5e-6, "bf16x3": 2.5e-5, "bf16": 1.4e-2}
+TOL_FWD_BF16_SHALLOW = 5e-2   # bf16 forward bound for nets with <= 4 hidden layers (measured <= 3.3e-2)
 PRECS = ["fp32", "bf16x3", "bf16"]
 
 CASES = [
@@ -67,7 +71,8 @@ def test_jet_forward_matches_torch(sizes, reqs, N, prec):
     scale = Jref.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
     err = ((J.double() - Jref).abs() / scale).max().item()
     print(f"KERNEL_ERR fwd {prec} {sizes} S={plan.S} {err:.3e}")
-    assert err < TOL_FWD[prec], err
+    tol = TOL_FWD_BF16_SHALLOW if (prec == "bf16" and len(sizes) <= 6) else TOL_FWD[prec]
+    assert err < tol, err
 
 
 @pytest.mark.parametrize("prec", PRECS)
@@ -239,13 +244,15 @@ def test_solver_hip_matches_jet_backend(prec):
     la, ga = a.grad()
     lb, gb = b.grad()
     tl = {"fp32": 1.0, "bf16x3": 10.0, "bf16": 300.0}[prec]
-    assert abs(la.item() - lb.item()) / abs(lb.item()) < 1e-5 * tl
-    for x, y in zip(ga, gb):
-        assert ((x - y).norm() / y.norm().clamp_min(1e-12)).item() < 1e-4 * tl
+    e_loss = abs(la.item() - lb.item()) / abs(lb.item())
+    e_grad = max(((x - y).norm() / y.norm().clamp_min(1e-12)).item() for x, y in zip(ga, gb))
     a.fit(tf_iter=20)
     b.fit(tf_iter=20)
     la, lb = a.losses[-1]["Total Loss"], b.losses[-1]["Total Loss"]
-    assert abs(la - lb) / abs(lb) < 1e-3 * tl, (la, lb)
+    e_fit = abs(la - lb) / abs(lb)
+    print(f"SOLVER_ERR {prec} loss {e_loss:.3e} grad {e_grad:.3e} fit20 {e_fit:.3e}")
+    assert e_loss < 1e-5 * tl and e_grad < 1e-4 * tl
+    assert e_fit < 1e-3 * tl, (la, lb)
 
 
 def test_mixed_plan_high_order_periodic():

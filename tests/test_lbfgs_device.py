@@ -263,3 +263,44 @@ def test_solver_device_lbfgs_on_hip_path(monkeypatch):
         m.fit(newton_iter=30)
         res[impl] = m.min_loss["l-bfgs"]
     assert res["device"] == pytest.approx(res["host"], rel=5e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_fused_update_matches_five_launch_path(use_graph, monkeypatch):
+    """The two-launch update (dots + logic, direction + descent test + step, each finished by the
+    last-ticket block) reproduces the five-launch path bit for bit: iterate, loss history, best
+    iterate, stop reason - incl. the history-ring wrap-around."""
+    fg = _quadratic(p=3000, q=4000, seed=4, device="cuda")
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TDQ_LBFGS_FUSED", fused)
+        x = torch.zeros(3000, device="cuda")
+        opt = LD.minimize(_evaluator(fg, x), x, 80, m=12, use_graph=use_graph, poll_every=9)
+        torch.cuda.synchronize()
+        assert opt.fused == (fused == "1")
+        outs.append((x.clone(), opt.history(), opt.n_iter, opt.best_x.clone(), opt.reason, opt.st.clone()))
+    a, b = outs
+    assert a[2] == b[2] and a[4] == b[4]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[3], b[3])
+    assert a[1] == b[1]
+    assert torch.equal(a[5], b[5])
+
+
+@pytest.mark.gpu
+def test_fused_update_descent_stop_restores_x(monkeypatch):
+    """A gradient the direction cannot descend along (g.d > -tolX from the first step): the fused
+    path stops with the same reason and leaves x where the five-launch path does (the speculative
+    step is undone)."""
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TDQ_LBFGS_FUSED", fused)
+        x = torch.ones(5000, device="cuda")
+        # tiny gradient: |g|_1 > tolFun but g.d = -|g|^2 > -tolX
+        evaluate = lambda: torch.cat([torch.full((5000,), 1e-9, device="cuda"),
+                                      torch.ones(1, device="cuda")]).contiguous()
+        opt = LD.minimize(evaluate, x, 10, use_graph=False)
+        torch.cuda.synchronize()
+        outs.append((x.clone(), opt.reason, opt.n_iter))
+    assert outs[0][1] == outs[1][1] == LD.REASONS[5]
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][0], torch.ones(5000, device="cuda"))
