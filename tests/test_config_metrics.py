@@ -128,3 +128,14 @@ def test_stale_library_hash_is_refused(monkeypatch):
     monkeypatch.setenv("TDQ_SKIP_HASH_CHECK", "1")
     monkeypatch.setattr(_lib, "_err", None)
     assert _lib.load(required=True) is not None
+
+
+def test_lint_subset_clean():
+    """The reference CI's flake8 subset (E9, F63, F7, F82 - tools/lint.py) over the whole repo."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("tdq_lint", os.path.join(root, "tools", "lint.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.main([]) == 0
