@@ -391,8 +391,10 @@ int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch,
   if (N <= 0) return 0;
   const int WT = width_tiles(width);
   JetSpec sp;
+  // geometry first: spec holds 3 S ints, parse it only for a valid S (tools/asan/host_check.cpp)
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int nso = spec_nso(S, spec);
-  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
+  if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* Hs = scratch;
@@ -431,8 +433,10 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   if (N <= 0) return 0;
   const int WT = width_tiles(width);
   JetSpec sp;
+  // geometry first: spec holds 3 S ints, parse it only for a valid S (tools/asan/host_check.cpp)
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int nso = spec_nso(S, spec);
-  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
+  if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows

@@ -8,4 +8,5 @@ python tools/lint.py
 python -c "import __graft_entry__ as g; g.build()"
 python -c "import tensordiffeq_amd as tdq, tensordiffeq; from tensordiffeq_amd.ops import _lib; \
 lib = _lib.load(); assert _lib.library_hash(lib) == _lib.expected_hash(); print('import ok', tdq.__name__)"
+python tools/asan_host_check.py   # host-side ASan + UBSan of the native library (~2.5 min)
 python -m pytest tests -x -q -m "not gpu"

@@ -1,0 +1,36 @@
+"""L-BFGS iteration profile target: the flagship AC-SA problem, a few Adam steps, then ``--iters``
+device L-BFGS iterations in the L-BFGS precision (bf16x3).  Run under rocprofv3 --kernel-trace
+--stats (tools/gpu_runs/r3_d.sh); prints the wall time per iteration."""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=500)
+    ap.add_argument("--npts", type=int, default=50000)
+    a = ap.parse_args()
+    import torch
+    import bench
+    m = bench.build_problem(a.npts, 1, "hip", torch.device("cuda", 0), False, "bf16", newton_precision="bf16x3")
+    m.fit(tf_iter=20)
+    m.fit(newton_iter=20)   # capture + warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.fit(newton_iter=a.iters)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    info = m.fit_info["lbfgs"]
+    print(json.dumps({"iters": info["n_iter"], "reason": info["reason"], "wall_s": dt,
+                      "ms_per_iter": 1e3 * dt / max(1, info["n_iter"]),
+                      "fused_update": os.environ.get("TDQ_LBFGS_FUSED", "1")}))
+
+
+if __name__ == "__main__":
+    main()
