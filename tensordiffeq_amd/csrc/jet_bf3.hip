@@ -405,7 +405,7 @@ int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch,
     if (rc) return rc;
   }
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
-            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo)};
+            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), nullptr};
   return dispatch(true, WT, S, nso, a);
 }
 
@@ -447,10 +447,10 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   float *img, *bimg, *aux;
   scratch_images(const_cast<float*>(Hs), N, n_hidden, S, WT, &img, &bimg, &aux);
   (void)P;
-  (void)img;
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), slab, N,
-            slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo)};
+            slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo),
+            reinterpret_cast<const bf16x8*>(img)};
   int rc = dispatch(false, WT, S, nso, a);
   if (rc || !reduce) return rc;
   return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, chunks, (int)slab_half(lo != 0), stream);

@@ -290,19 +290,6 @@ class AdamEngine:
         self._tail_saved = saved
         return fop.total
 
-    def _dp_tail_phase_a(self):
-        """DP graph half before the all-reduce (fused-tail kernels; see :meth:`_tail_eligible`)."""
-        from .ops import jet_hip
-        prog = self.program
-        fop = prog.fused_op
-        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision, pack=False)
-        fop(J, with_total=False, reduce=False)
-        grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
-        jet_hip.dp_tail_a(saved, work, grad, fop)
-        self._sum_terms = True
-        self._tail_saved = saved
-        return fop.total, self._fused_grads(fop, grad, fop.dlam, fop.dscal), fop.losses
-
     def _dp_tail_phase_b(self, loss, grads, terms):
         """DP graph half after the all-reduce: bookkeeping, then Adam + snapshot + weight images."""
         from .ops import jet_hip
@@ -370,12 +357,46 @@ class AdamEngine:
 
     def _dp_half_a(self, tail):
         """DP step up to the collective: loss + gradients, packed into the static bucket."""
-        loss, grads, terms = self._dp_tail_phase_a() if tail else self._phase_a(for_step=True)
+        if tail:
+            return self._dp_half_a_inplace()
+        loss, grads, terms = self._phase_a(for_step=True)
         red_idx = self.red_idx
         red = [grads[i] for i in red_idx]
         terms = _term_list(terms)
         self._bucket = _Bucket(red, 1 + len(terms))
         self._bucket_buf = self._bucket.pack(red, [loss] + terms)
+        self._grads_static = grads
+        self._red_idx = red_idx
+
+    def _dp_half_a_inplace(self):
+        """Fused-tail DP step up to the collective with the kernels writing straight into the
+        bucket ``[grad theta | other reduced grads | loss | terms]``: slab pass 2 lands in the
+        theta slice, the loss reduction in the scalar slice, so only the (small) other reduced
+        gradients are copied - no concatenation of the 50k-element theta gradient per step."""
+        from .ops import jet_hip
+        prog = self.program
+        fop = prog.fused_op
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision, pack=False)
+        fop(J, with_total=False, reduce=False)
+        n_p = self.flat.numel()
+        red_idx = self.red_idx
+        if not red_idx or red_idx[0] != 0:
+            raise RuntimeError("DP bucket: theta must be the first reduced tensor")
+        others = [i for i in red_idx[1:]]
+        sizes = [self.wrt[i].numel() for i in others]
+        n_e, n_t = sum(sizes), fop.n_terms
+        buf = torch.empty(n_p + n_e + 1 + n_t, dtype=torch.float32, device=self.device)
+        grad_view = buf[:n_p]
+        grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=grad_view)
+        jet_hip.dp_tail_a(saved, work, grad_view, fop, total=buf[n_p + n_e:n_p + n_e + 1],
+                          losses=buf[n_p + n_e + 1:])
+        grads = self._fused_grads(fop, grad_view, fop.dlam, fop.dscal)
+        if others:
+            torch.cat([grads[i].reshape(-1) for i in others], out=buf[n_p:n_p + n_e])
+        self._sum_terms = True
+        self._tail_saved = saved
+        self._bucket = _Bucket([grads[i] for i in red_idx], 1 + n_t)
+        self._bucket_buf = buf
         self._grads_static = grads
         self._red_idx = red_idx
 

@@ -161,15 +161,17 @@ class JetMLPFunction(torch.autograd.Function):
         return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None
 
 
-def dp_tail_a(saved, work, grad, fop, total=None):
+def dp_tail_a(saved, work, grad, fop, total=None, losses=None):
     """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
     slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``).  ``total`` (a 1-element
-    view): also write the summed loss there."""
+    view): also write the summed loss there; ``losses`` (an ``n_terms`` view, default
+    ``fop.losses``): where the per-term losses go - both can point into the all-reduce bucket."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
+    losses = fop.losses if losses is None else losses
     rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
                                cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
-                               fop.n_scal, _lib.ptr(fop.losses), _lib.ptr(fop.dscal), _lib.ptr(total),
+                               fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total),
                                _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")
 
