@@ -412,10 +412,12 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 // them tile by tile on the matrix cores from h_{Lh-2} (which it reads anyway for dK_{Lh-1}) or,
 // for Lh = 2, from x through h0_jet - the same MFMA sequence and tanh-jet code as the forward, so
 // the same bits (Lh = 1: layer 0 is still saved).
-// The forward is bound by its saved-activation stores (profiles/r3_pmc_bf16.txt: 217 MB at
-// 3.8 TB/s); this drops 1 of its 3 full layers (-30 % of the bytes).  -DTDQ_RECOMPUTE_TOP=0: save.
+// It drops 1 of the forward's 3 full saved layers (-30 % of its 217 MB of stores,
+// profiles/r3_pmc_bf16.txt), but measured on MI355X (AC-SA bf16 step, profiles/r3_e_ab.txt) the
+// forward only went 57 -> 54 us while the backward grew 137 -> 157 us: off by default,
+// -DTDQ_RECOMPUTE_TOP=1 builds it.
 #ifndef TDQ_RECOMPUTE_TOP
-#define TDQ_RECOMPUTE_TOP 1
+#define TDQ_RECOMPUTE_TOP 0
 #endif
 template <int WT, bool LO>
 __host__ __device__ constexpr int hs_wave_floats(int S) {
@@ -1123,7 +1125,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   __syncthreads();
   if (w == 2) {
     const int ko = off_layer(d, Lh);
-    for (int e = l; e < d.width * d.d_out; e += 64) {
+    for (int e = l; e < hw(d, Lh - 1) * d.d_out; e += 64) {
       const int f = e / d.d_out, q = e - f * d.d_out;
       const int k = f * TDQ_MAXO + q, st = W * TDQ_MAXO;
       float a = accKo[k];
@@ -1135,7 +1137,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       float a = accBo[l];
 #pragma unroll
       for (int v = 1; v < NWV; ++v) a += accBo[v * TDQ_MAXO + l];
-      slab_put(gs + ko + d.width * d.d_out + l, a);
+      slab_put(gs + ko + hw(d, Lh - 1) * d.d_out + l, a);
     }
   }
   TDQ_TS(1);
@@ -1167,8 +1169,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       __bf16* const im = img + (DBUF ? (s & 1) * IBUF : 0);
       if (s == 0 && w == 0) {  // bias of layer i: partials of all waves landed before this barrier
         const float* accBi = accB + (i & 1) * NWV * W;
-        const int bo = off_layer(d, i) + d.width * d.width;
-        for (int f = l; f < d.width; f += 64) {
+        const int bo = off_layer(d, i) + hw(d, i - 1) * hw(d, i);
+        for (int f = l; f < hw(d, i); f += 64) {
           float a = accBi[f];
 #pragma unroll
           for (int v = 1; v < NWV; ++v) a += accBi[v * W + f];
@@ -1236,7 +1238,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       // (and their exec masks) out of the layer loop, where they stay live and spill
       asm volatile("" : "+v"(in0), "+v"(out0));
       ST* gk = gs + off_layer(d, i);
-      if (d.width == W) {
+      if (d.uniform && d.width == W) {
         const Tl G = tl_make(gk, 0);
         constexpr int EB = (int)sizeof(ST);  // slab entry bytes
         const int voff = (in0 * W + out0) * EB;
@@ -1261,7 +1263,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const int in = in0 + 16 * r + c, out = out0 + 16 * c2;
-              if (in < d.width && out < d.width) slab_put(gk + in * d.width + out, dw[r][c2][c]);
+              if (in < hw(d, i - 1) && out < hw(d, i)) slab_put(gk + in * hw(d, i) + out, dw[r][c2][c]);
             }
       }
     }
@@ -1293,16 +1295,16 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   __syncthreads();
   if (w == 0) {
     const float* accB0 = accB + 2 * NWV * W;
-    const int bo = d.d_in * d.width;
-    for (int f = l; f < d.width; f += 64) {
+    const int bo = d.d_in * hw(d, 0);
+    for (int f = l; f < hw(d, 0); f += 64) {
       float a = accB0[f];
 #pragma unroll
       for (int v = 1; v < NWV; ++v) a += accB0[v * W + f];
       slab_put(gs + bo + f, a);
     }
   } else if (w == 1) {
-    for (int e = l; e < d.d_in * d.width; e += 64) {
-      const int j = e / d.width, f = e - j * d.width;
+    for (int e = l; e < d.d_in * hw(d, 0); e += 64) {
+      const int j = e / hw(d, 0), f = e - j * hw(d, 0);
       const int k = j * W + f;
       float a = accK0[k];
 #pragma unroll

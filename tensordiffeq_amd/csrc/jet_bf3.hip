@@ -32,7 +32,8 @@ __device__ __forceinline__ void pack_frag(const float* __restrict__ P, bf16x8* _
     for (int j = 0; j < 8; ++j) {
       const int kf = 32 * kb + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
       const int in = transposed ? kf : row, out = transposed ? row : kf;
-      const float v = (in < d.width && out < d.width) ? K[in * d.width + out] : 0.f;
+      const int win = hw(d, layer - 1), wout = hw(d, layer);
+      const float v = (in < win && out < wout) ? K[in * wout + out] : 0.f;
       const __bf16 h = (__bf16)v;
       hi[j] = h;
       lo[j] = (__bf16)(v - (float)h);
@@ -47,21 +48,22 @@ __device__ __forceinline__ void pack_aux(const float* __restrict__ P, float* __r
                                          int W, int e) {
   {
     float v = 0.f;
+    const int w0 = hw(d, 0), wl = hw(d, d.n_hidden - 1);
     if (e < aux_b0(d, W)) {  // K0 [d_in][W]
       const int j = e / W, f = e - j * W;
-      if (f < d.width) v = P[j * d.width + f];
+      if (f < w0) v = P[j * w0 + f];
     } else if (e < aux_bh(d, W)) {  // b0
       const int f = e - aux_b0(d, W);
-      if (f < d.width) v = P[d.d_in * d.width + f];
+      if (f < w0) v = P[d.d_in * w0 + f];
     } else if (e < aux_ko(d, W)) {  // hidden biases
       const int r = e - aux_bh(d, W), i = r / W + 1, f = r - (i - 1) * W;
-      if (f < d.width) v = P[off_layer(d, i) + d.width * d.width + f];
+      if (f < hw(d, i)) v = P[off_layer(d, i) + hw(d, i - 1) * hw(d, i) + f];
     } else if (e < aux_bo(d, W)) {  // Ko [W][4]
       const int r = e - aux_ko(d, W), f = r >> 2, q = r & 3;
-      if (f < d.width && q < d.d_out) v = P[off_layer(d, d.n_hidden) + f * d.d_out + q];
+      if (f < wl && q < d.d_out) v = P[off_layer(d, d.n_hidden) + f * d.d_out + q];
     } else {  // bo [4]
       const int q = e - aux_bo(d, W);
-      if (q < d.d_out) v = P[off_layer(d, d.n_hidden) + d.width * d.d_out + q];
+      if (q < d.d_out) v = P[off_layer(d, d.n_hidden) + wl * d.d_out + q];
     }
     aux[e] = v;
   }
@@ -172,7 +174,7 @@ __device__ __forceinline__ void img_put(__bf16* __restrict__ img, int layer, int
 // flat (Keras-order) parameter e with new value v -> its slot in the images (inverse of pack_all)
 __device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti) {
   const NetDims& d = ti.d;
-  const int W = 16 * ti.WT, w = d.width;
+  const int W = 16 * ti.WT, w = hw(d, 0);
   const int n0 = d.d_in * w;
   if (e < n0) {
     const int j = e / w;
@@ -183,25 +185,26 @@ __device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti)
     ti.aux[aux_b0(d, W) + (e - n0)] = v;
     return;
   }
-  const int r = e - (n0 + w), L = w * w + w;
-  if (r < (d.n_hidden - 1) * L) {
-    const int i = r / L + 1, q = r - (i - 1) * L;
-    if (q < w * w) {
-      const int in = q / w, out = q - in * w;
+  if (e < off_layer(d, d.n_hidden)) {  // hidden layer i >= 1: kernel [w_{i-1}][w_i], bias [w_i]
+    int i = 1;
+    while (i + 1 < d.n_hidden && e >= off_layer(d, i + 1)) ++i;
+    const int q = e - off_layer(d, i), wi = hw(d, i - 1), wo = hw(d, i);
+    if (q < wi * wo) {
+      const int in = q / wo, out = q - in * wo;
       const __bf16 hi = (__bf16)v, lo = (__bf16)(v - (float)hi);
       img_put(ti.fimg, i, out, in, ti.WT, hi, lo);  // forward: A[row = out][k = in]
       img_put(ti.bimg, i, in, out, ti.WT, hi, lo);  // backward: A[row = in][k = out]
     } else {
-      ti.aux[aux_bh(d, W) + (i - 1) * W + (q - w * w)] = v;
+      ti.aux[aux_bh(d, W) + (i - 1) * W + (q - wi * wo)] = v;
     }
     return;
   }
-  const int r2 = r - (d.n_hidden - 1) * L;
-  if (r2 < w * d.d_out) {
+  const int r2 = e - off_layer(d, d.n_hidden), wl = hw(d, d.n_hidden - 1);
+  if (r2 < wl * d.d_out) {
     const int f = r2 / d.d_out;
     ti.aux[aux_ko(d, W) + f * 4 + (r2 - f * d.d_out)] = v;
   } else {
-    ti.aux[aux_bo(d, W) + (r2 - w * d.d_out)] = v;
+    ti.aux[aux_bo(d, W) + (r2 - wl * d.d_out)] = v;
   }
 }
 
@@ -348,8 +351,10 @@ extern "C" {
 // scratch = saved post-activations Hs | forward A image | backward A image | aux image | (wide
 // bf16x3 plans) the global fragment stage (floats; -1: unsupported).  The forward packs all three
 // images in one launch; the backward reuses them.
-int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int S, int lo) {
-  const int WT = width_tiles(width);
+int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, const int* widths, int n_hidden, int S, int lo) {
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, 1, n_hidden)) return -1;
+  const int WT = width_tiles(d.width);
   if (WT < 2) return -1;
   const int64_t nwg = (N + 63) / 64;
   const int64_t stage = bf3_gstage(WT, S, lo != 0) ? nwg * 4 * stage_wave_elems(WT, S, true) * 2 : 0;
@@ -358,11 +363,13 @@ int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int
 }
 
 // per-workgroup gradient slabs + reduction partials, in floats
-int64_t tdq_jet_bf3_slab_floats(int N, int d_in, int width, int d_out, int n_hidden) {
-  const int WT = width_tiles(width);
+int64_t tdq_jet_bf3_slab_floats(int N, int d_in, const int* widths, int d_out, int n_hidden) {
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return -1;
+  const int WT = width_tiles(d.width);
   if (WT < 2) return -1;
   const int nwg = (N + 63) / 64;
-  const int64_t P = slab_stride(param_count(d_in, width, d_out, n_hidden));
+  const int64_t P = slab_stride(param_count(d));
   return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
 
@@ -386,16 +393,17 @@ static inline bf16x4* scratch_stage(float* scratch, int N, int d_in, int n_hidde
 // lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16).
 // pack = 0: the weight images in scratch are already current (written by the previous step's
 // tail_adam), so the forward skips its pack launch.
-int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
+int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch, int N, int d_in, const int* widths,
                        int d_out, int n_hidden, int S, const int* spec, int lo, int pack, void* stream) {
   if (N <= 0) return 0;
-  const int WT = width_tiles(width);
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
   JetSpec sp;
   // geometry first: spec holds 3 S ints, parse it only for a valid S (tools/asan/host_check.cpp)
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int nso = spec_nso(S, spec);
   if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
-  NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* Hs = scratch;
   float *img, *bimg, *aux;
@@ -409,17 +417,18 @@ int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch,
   return dispatch(true, WT, S, nso, a);
 }
 
-int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width,
+int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, const int* widths,
                     int d_out, int n_hidden, int S, const int* spec, int lo, void* stream) {
-  return tdq_jet_fwd_bf3_ex(X, P, J, scratch, N, d_in, width, d_out, n_hidden, S, spec, lo, 1, stream);
+  return tdq_jet_fwd_bf3_ex(X, P, J, scratch, N, d_in, widths, d_out, n_hidden, S, spec, lo, 1, stream);
 }
 
 // the weight images of a forward scratch, packed from P (one launch)
-int tdq_jet_bf3_pack(const float* P, float* scratch, int N, int d_in, int width, int d_out, int n_hidden, int S,
+int tdq_jet_bf3_pack(const float* P, float* scratch, int N, int d_in, const int* widths, int d_out, int n_hidden, int S,
                      void* stream) {
-  const int WT = width_tiles(width);
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
-  NetDims d{d_in, width, d_out, n_hidden};
   float *img, *bimg, *aux;
   scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
   return launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT,
@@ -428,19 +437,20 @@ int tdq_jet_bf3_pack(const float* P, float* scratch, int N, int d_in, int width,
 
 // reduce = 0: only the backward kernel (gradient slabs in work); tdq_step_tail_bf3 reduces them
 int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
-                       int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo, int reduce,
+                       int N, int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo, int reduce,
                        void* stream) {
   if (N <= 0) return 0;
-  const int WT = width_tiles(width);
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
   JetSpec sp;
   // geometry first: spec holds 3 S ints, parse it only for a valid S (tools/asan/host_check.cpp)
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int nso = spec_nso(S, spec);
   if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
-  NetDims d{d_in, width, d_out, n_hidden};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
-  const int Ptot = param_count(d_in, width, d_out, n_hidden);
+  const int Ptot = param_count(d);
   const int chunks = slab_chunks(nwg_b);
   float* slab = work;
   // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
@@ -457,28 +467,30 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
 }
 
 int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
-                    int N, int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo,
+                    int N, int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo,
                     void* stream) {
-  return tdq_jet_bwd_bf3_ex(X, P, dJ, Hs, work, grad, N, d_in, width, d_out, n_hidden, S, spec, lo, 1, stream);
+  return tdq_jet_bwd_bf3_ex(X, P, dJ, Hs, work, grad, N, d_in, widths, d_out, n_hidden, S, spec, lo, 1, stream);
 }
 
 // The end of a single-process Adam step in two launches (see the file comment).  work: the
 // backward's gradient slabs (tdq_jet_bwd_bf3_ex with reduce = 0); grad: receives the reduced theta
 // gradient; scratch: the forward's scratch whose images are rewritten for the next step (nullptr:
 // leave them).  groups[0] must be theta (n == parameter count); its g pointer is replaced by grad.
-int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in, int width, int d_out, int n_hidden,
+int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in, const int* widths, int d_out, int n_hidden,
                       int S, int lo, const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses,
                       float* total, float* dscal, float* hist, int64_t hist_rows, int64_t* epoch, float* best_loss,
                       int64_t* best_epoch, int* improved, double* const* counters, int ncnt, const void* groups,
                       int ngroups, float* snap, void* stream) {
-  const int WT = width_tiles(width);
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || ncnt < 0 || ncnt > TDQ_MAX_COUNTERS || n_lblocks < 0 ||
       n_terms < 0 || n_scal < 0)
     return (int)hipErrorInvalidValue;
   AdamArgs args;
   if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, TDQ_TAIL_ELEM != 0))
     return (int)hipErrorInvalidValue;
-  const int Ptot = param_count(d_in, width, d_out, n_hidden);
+  const int Ptot = param_count(d);
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
   args.grp[0].g = grad;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -505,7 +517,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
                      nqb, (int)slab_half(lo != 0), tb);
   TDQ_CHECK_LAUNCH();
-  TailImg ti{nullptr, nullptr, nullptr, NetDims{d_in, width, d_out, n_hidden}, WT};
+  TailImg ti{nullptr, nullptr, nullptr, d, WT};
   if (scratch != nullptr) {
     float *img, *bimg, *aux;
     scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
@@ -526,14 +538,16 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
 // Data-parallel step, first half (before the all-reduce): slab pass 1 + the loss reduction in one
 // launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad.  total
 // (optional): also the summed loss - the L-BFGS objective writes [grad | loss] in place this way.
-int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int d_out, int n_hidden, int S, int lo,
+int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
                       float* total, void* stream) {
-  const int WT = width_tiles(width);
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1 || n_lblocks < 0 || n_terms < 0 || n_scal < 0)
     return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int Ptot = param_count(d_in, width, d_out, n_hidden);
+  const int Ptot = param_count(d);
   const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   float* part = work + (size_t)nwg_b * Pst;
@@ -557,15 +571,17 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int 
 // Data-parallel step, second half (after the all-reduce and tdq_step_book): Adam over every group
 // with theta's gradient read from groups[0].g (the all-reduced bucket), the best-weights snapshot
 // and the next step's weight images written into the forward scratch.
-int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, int width, int d_out, int n_hidden, int S,
+int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_out, int n_hidden, int S,
                       const void* groups, int ngroups, const int* improved, float* snap, void* stream) {
-  const int WT = width_tiles(width);
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   AdamArgs args;
   if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, TDQ_TAIL_ELEM != 0))
     return (int)hipErrorInvalidValue;
-  if (args.grp[0].n != param_count(d_in, width, d_out, n_hidden)) return (int)hipErrorInvalidValue;
-  TailImg ti{nullptr, nullptr, nullptr, NetDims{d_in, width, d_out, n_hidden}, WT};
+  if (args.grp[0].n != param_count(d)) return (int)hipErrorInvalidValue;
+  TailImg ti{nullptr, nullptr, nullptr, d, WT};
   if (scratch != nullptr) {
     float *img, *bimg, *aux;
     scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);

@@ -17,14 +17,50 @@ struct JetSpec {
   int ia[TDQ_MAXS], ib[TDQ_MAXS];  // type 2: the same factors as stream indices (memory addressing only)
 };
 
+#define TDQ_MAXL 16  // hidden layers
+
+// Network geometry.  Hidden layers may have different widths (the reference's neural_net takes
+// any layer list, tensordiffeq/networks.py:10-20): the kernels pad every hidden layer to the
+// widest one's W = 16 WT features (zero weights and biases -> the padded units are exactly 0 in
+// every jet stream and never reach a gradient slab); `lw` / `lo` map the flat Keras-order buffer.
 struct NetDims {
-  int d_in, width, d_out, n_hidden;
+  int d_in, width, d_out, n_hidden;  // width: the WIDEST hidden layer
+  int lw[TDQ_MAXL];                  // hidden layer widths
+  int lo[TDQ_MAXL + 1];              // flat offset of dense layer i (0: input -> hidden 0; n_hidden: output)
+  int uniform;                       // every hidden layer is `width` wide
 };
 
-__device__ __forceinline__ int off_layer(const NetDims& d, int i) {
-  // start of dense layer i (>= 1) in the flat Keras-order buffer
-  return d.d_in * d.width + d.width + (i - 1) * (d.width * d.width + d.width);
+// start of dense layer i (>= 1) in the flat Keras-order buffer
+__host__ __device__ __forceinline__ int off_layer(const NetDims& d, int i) { return d.lo[i]; }
+// width of hidden layer i (its kernel is [lw[i-1]][lw[i]] for i >= 1)
+__host__ __device__ __forceinline__ int hw(const NetDims& d, int i) { return d.lw[i]; }
+
+// widths: n_hidden hidden widths (nullptr: all `width`); false on an unsupported geometry
+static inline bool make_dims(NetDims& d, int d_in, const int* widths, int width, int d_out, int n_hidden) {
+  if (n_hidden < 1 || n_hidden > TDQ_MAXL || d_in < 1 || d_out < 1) return false;
+  d.d_in = d_in;
+  d.d_out = d_out;
+  d.n_hidden = n_hidden;
+  int mx = 0, off = 0, prev = d_in;
+  for (int i = 0; i < TDQ_MAXL; ++i) d.lw[i] = 0;
+  for (int i = 0; i < n_hidden; ++i) {
+    const int w = widths ? widths[i] : width;
+    if (w < 1) return false;
+    d.lw[i] = w;
+    d.lo[i] = off;
+    off += prev * w + w;
+    prev = w;
+    mx = w > mx ? w : mx;
+  }
+  d.lo[n_hidden] = off;
+  for (int i = n_hidden + 1; i <= TDQ_MAXL; ++i) d.lo[i] = off;
+  d.width = mx;
+  d.uniform = 1;
+  for (int i = 0; i < n_hidden; ++i) d.uniform &= d.lw[i] == mx;
+  return true;
 }
+
+static inline int param_count(const NetDims& d) { return d.lo[d.n_hidden] + d.lw[d.n_hidden - 1] * d.d_out + d.d_out; }
 
 __device__ __forceinline__ size_t zs_index(int layer, int nwg, int wg, int S, int s, int w, int WT,
                                            int t, int lane) {
@@ -44,6 +80,13 @@ static inline int width_tiles(int width) {
 
 static inline int param_count(int d_in, int width, int d_out, int n_hidden) {
   return d_in * width + width + (n_hidden - 1) * (width * width + width) + width * d_out + d_out;
+}
+
+// NetDims of an equal-width network (the exact-fp32 family, jet_mlp.hip)
+static inline NetDims uniform_dims(int d_in, int width, int d_out, int n_hidden) {
+  NetDims d;
+  make_dims(d, d_in, nullptr, width, d_out, n_hidden);
+  return d;
 }
 
 // spec: 3 ints per stream (type, a, b): type 1 -> a = input variable; type 2 -> a, b = stream

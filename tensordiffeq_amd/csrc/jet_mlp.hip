@@ -734,7 +734,7 @@ int tdq_jet_fwd(const float* X, const float* P, float* J, float* scratch, int N,
   JetSpec sp;
   if (WT < 0 || S * WT > 32 || d_in > TDQ_MAXD || d_out > TDQ_MAXO || n_hidden < 1 || !make_spec(S, spec, sp))
     return (int)hipErrorInvalidValue;
-  NetDims d{d_in, width, d_out, n_hidden};
+  NetDims d = uniform_dims(d_in, width, d_out, n_hidden);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t nwg = (N + 63) / 64;
   float* Zs = scratch;
@@ -751,7 +751,7 @@ int tdq_jet_bwd(const float* X, const float* P, const float* dJ, const float* Zs
   JetSpec sp;
   if (WT < 0 || S * WT > 32 || d_in > TDQ_MAXD || d_out > TDQ_MAXO || n_hidden < 1 || !make_spec(S, spec, sp))
     return (int)hipErrorInvalidValue;
-  NetDims d{d_in, width, d_out, n_hidden};
+  NetDims d = uniform_dims(d_in, width, d_out, n_hidden);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nwg = (N + 63) / 64;
   const int Ptot = param_count(d_in, width, d_out, n_hidden);

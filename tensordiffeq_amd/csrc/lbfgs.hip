@@ -107,6 +107,41 @@ __device__ __forceinline__ void part_st(double* p, double v) {
 
 __device__ __forceinline__ bool slot_valid(int i, int head, int k, int m) { return ((i - head + m) % m) < k; }
 
+// lane `q` (wave-uniform) of a double, through two v_readlane_b32
+__device__ __forceinline__ double readlane_d(double v, int q) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, q), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), q);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// d_j = cG g_j + sum_i (cS_i s_ij + cY_i y_ij) over the k history pairs (oldest first), four
+// independent partial sums so the 2k strided loads overlap; shared by both update paths (same
+// summation order, so the same bits)
+__device__ __forceinline__ double dir_elem(const float* __restrict__ S, const float* __restrict__ Y,
+                                           const double* __restrict__ coef, int j, int p, int k, int head, int m,
+                                           int pushed, int slot, float s, float y, double dn) {
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  int q = 0;
+  for (; q + 3 < k; q += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = (head + q + u) % m;
+      const bool nw = pushed && i == slot;
+      const double si = nw ? (double)s : (double)S[(size_t)i * p + j];
+      const double yi = nw ? (double)y : (double)Y[(size_t)i * p + j];
+      acc[u] += coef[i] * si + coef[m + i] * yi;
+    }
+  }
+  for (; q < k; ++q) {
+    const int i = (head + q) % m;
+    const bool nw = pushed && i == slot;
+    const double si = nw ? (double)s : (double)S[(size_t)i * p + j];
+    const double yi = nw ? (double)y : (double)Y[(size_t)i * p + j];
+    acc[0] += coef[i] * si + coef[m + i] * yi;
+  }
+  return dn + ((acc[0] + acc[1]) + (acc[2] + acc[3]));
+}
+
 // ---------------------------------------------------------------------------------------------
 // the partial sums of one (chunk, slot) block of the dots grid -> part (thread 0 stores them)
 template <bool SC1>
@@ -308,11 +343,16 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   // 5. compact product on wave 0 (lane j = chronological pair j):
   //    R u = S^T g ; rhs = D u + gam Y^T Y u - gam Y^T g ; R^T p1 = rhs ;
   //    H g = gam g + S p1 - gam Y u   ->   d = -H g
+  //    Both substitutions are k sequential steps on one wave: each step's pivot is broadcast with
+  //    v_readlane (uniform q; a ds_bpermute shuffle costs ~10x its latency) and multiplied by the
+  //    pivot's reciprocal, computed for every lane in parallel up front (no fp64 division on the
+  //    dependent chain): the logic kernel went from ~22 us to a few us per iteration.
   if (tid < 64) {
     const int j = tid;
+    const double rdj = j < k ? 1.0 / Rc[j * m + j] : 0.0;
     double r = j < k ? aC[j] : 0.0, u = 0.0;
     for (int q = k - 1; q >= 0; --q) {  // back substitution
-      const double uq = __shfl(r, q, 64) / Rc[q * m + q];
+      const double uq = readlane_d(r, q) * readlane_d(rdj, q);
       if (j == q) u = uq;
       if (j < q) r -= Rc[j * m + q] * uq;
     }
@@ -321,6 +361,7 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   __syncthreads();
   if (tid < 64) {
     const int j = tid;
+    const double rdj = j < k ? 1.0 / Rc[j * m + j] : 0.0;
     double rhs = 0.0;
     if (j < k) {
       double yu = 0.0;
@@ -329,7 +370,7 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
     }
     double rr = rhs, p1 = 0.0;
     for (int q = 0; q < k; ++q) {  // forward substitution with R^T
-      const double pq = __shfl(rr, q, 64) / Rc[q * m + q];
+      const double pq = readlane_d(rr, q) * readlane_d(rdj, q);
       if (j == q) p1 = pq;
       if (j > q && j < k) rr -= Rc[q * m + j] * pq;
     }
@@ -383,13 +424,7 @@ __global__ void __launch_bounds__(256) lbfgs_dir_kernel(const float* __restrict_
         S[(size_t)slot * c.p + j] = s;
         Y[(size_t)slot * c.p + j] = y;
       }
-      for (int q = 0; q < k; ++q) {
-        const int i = (head + q) % m;
-        const bool nw = pushed && i == slot;
-        const double si = nw ? (double)s : (double)S[(size_t)i * c.p + j];
-        const double yi = nw ? (double)y : (double)Y[(size_t)i * c.p + j];
-        dn += coef[i] * si + coef[m + i] * yi;
-      }
+      dn = dir_elem(S, Y, coef, j, c.p, k, head, m, pushed, slot, s, y, dn);
     }
     const float df = (float)dn;
     g_old[j] = g;
@@ -509,13 +544,7 @@ __global__ void __launch_bounds__(256) lbfgs_dir_step_kernel(float* __restrict__
         S[(size_t)slot * c.p + j] = s;
         Y[(size_t)slot * c.p + j] = y;
       }
-      for (int q = 0; q < k; ++q) {
-        const int i = (head + q) % m;
-        const bool nw = pushed && i == slot;
-        const double si = nw ? (double)s : (double)S[(size_t)i * c.p + j];
-        const double yi = nw ? (double)y : (double)Y[(size_t)i * c.p + j];
-        dn += coef[i] * si + coef[m + i] * yi;
-      }
+      dn = dir_elem(S, Y, coef, j, c.p, k, head, m, pushed, slot, s, y, dn);
     }
     const float df = (float)dn;
     g_old[j] = g;

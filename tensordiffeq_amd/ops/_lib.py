@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lock = threading.Lock()
 _lib = None
@@ -39,17 +39,18 @@ def _declare(lib):
         "tdq_jet_bwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P]),
         "tdq_jet_scratch_floats": (L, [I, I, I, I, I]),
         "tdq_jet_slab_floats": (L, [I, I, I, I, I]),
-        "tdq_jet_fwd_bf3": (I, [P, P, P, P, I, I, I, I, I, I, P, I, P]),
-        "tdq_jet_bwd_bf3": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, I, P]),
-        "tdq_jet_fwd_bf3_ex": (I, [P, P, P, P, I, I, I, I, I, I, P, I, I, P]),
-        "tdq_jet_bwd_bf3_ex": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, I, I, P]),
-        "tdq_jet_bf3_pack": (I, [P, P, I, I, I, I, I, I, P]),
-        "tdq_step_tail_bf3": (I, [P, P, P] + [I] * 7 + [P, I, I, I, P, P, P] + [P, L, P, P, P, P]
+        # split-bf16 family: `widths` = pointer to the n_hidden hidden-layer widths
+        "tdq_jet_fwd_bf3": (I, [P, P, P, P, I, I, P, I, I, I, P, I, P]),
+        "tdq_jet_bwd_bf3": (I, [P, P, P, P, P, P, I, I, P, I, I, I, P, I, P]),
+        "tdq_jet_fwd_bf3_ex": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, P]),
+        "tdq_jet_bwd_bf3_ex": (I, [P, P, P, P, P, P, I, I, P, I, I, I, P, I, I, P]),
+        "tdq_jet_bf3_pack": (I, [P, P, I, I, P, I, I, I, P]),
+        "tdq_step_tail_bf3": (I, [P, P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P] + [P, L, P, P, P, P]
                               + [P, I, P, I, P, P]),
-        "tdq_dp_tail_a_bf3": (I, [P, P] + [I] * 7 + [P, I, I, I, P, P, P, P]),
-        "tdq_dp_tail_b_bf3": (I, [P] + [I] * 6 + [P, I, P, P, P]),
-        "tdq_jet_bf3_scratch_floats": (L, [I, I, I, I, I, I]),
-        "tdq_jet_bf3_slab_floats": (L, [I, I, I, I, I]),
+        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, P]),
+        "tdq_dp_tail_b_bf3": (I, [P, I, I, P, I, I, I, P, I, P, P, P]),
+        "tdq_jet_bf3_scratch_floats": (L, [I, I, P, I, I, I]),
+        "tdq_jet_bf3_slab_floats": (L, [I, I, P, I, I]),
         "tdq_adam_multi": (I, [P, I, P, P, P]),
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),

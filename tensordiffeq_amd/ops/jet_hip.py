@@ -29,12 +29,21 @@ def stream_spec(plan):
     return out
 
 
+def _warg(cfg):
+    """The width argument of a kernel entry point: a pointer to the hidden-layer widths for the
+    split-bf16 family (any widths, padded to the widest), the single width for exact fp32."""
+    if cfg["precision"] in ("bf16x3", "bf16"):
+        w = cfg["widths"]
+        return (ctypes.c_int * len(w))(*w)
+    return cfg["width"]
+
+
 def _fns(lib, cfg):
     if cfg["precision"] in ("bf16x3", "bf16"):
         return (lib.tdq_jet_fwd_bf3, lib.tdq_jet_bwd_bf3,
-                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["d_in"], cfg["width"], cfg["n_hidden"], cfg["S"],
+                lambda N: lib.tdq_jet_bf3_scratch_floats(N, cfg["d_in"], _warg(cfg), cfg["n_hidden"], cfg["S"],
                                                          *_lo_args(cfg)),
-                lambda N: lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
+                lambda N: lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"]))
     return (lib.tdq_jet_fwd, lib.tdq_jet_bwd,
             lambda N: lib.tdq_jet_scratch_floats(N, cfg["width"], cfg["n_hidden"], cfg["S"], 0),
             lambda N: lib.tdq_jet_slab_floats(N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"]))
@@ -71,11 +80,11 @@ def forward_raw(X, P, net, plan, precision=None, pack=True):
     scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
     if not pack and cfg["precision"] in ("bf16x3", "bf16"):
         rc = lib.tdq_jet_fwd_bf3_ex(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
-                                    cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), 0,
+                                    _warg(cfg), cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), 0,
                                     _lib.stream_ptr(X.device))
     else:
         rc = fwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), N, cfg["d_in"],
-                 cfg["width"], cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
+                 _warg(cfg), cfg["d_out"], cfg["n_hidden"], S, spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
     _lib.check(rc, f"tdq_jet_fwd[{cfg['precision']}]")
     return J, (X, P, scratch, cfg, spec, S)
 
@@ -98,12 +107,12 @@ def backward_raw(saved, dJ, reduce=True, grad=None):
         if not is_split_bf16(cfg):
             raise ValueError("backward_raw(reduce=False) needs a split-bf16 precision")
         rc = lib.tdq_jet_bwd_bf3_ex(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
-                                    _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"],
+                                    _lib.ptr(grad), N, cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"],
                                     S, spec_c, *_lo_args(cfg), 0, _lib.stream_ptr(X.device))
         _lib.check(rc, f"tdq_jet_bwd_bf3_ex[{cfg['precision']}]")
         return grad, work
     rc = bwd(_lib.ptr(X), _lib.ptr(P), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work),
-                         _lib.ptr(grad), N, cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S,
+                         _lib.ptr(grad), N, cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], S,
                          spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
     _lib.check(rc, f"tdq_jet_bwd[{cfg['precision']}]")
     return grad
@@ -117,7 +126,7 @@ def pack_images(saved):
     """Re-pack the weight images of a forward scratch from the current parameters (one launch)."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
-    rc = lib.tdq_jet_bf3_pack(_lib.ptr(P), _lib.ptr(scratch), X.shape[0], cfg["d_in"], cfg["width"],
+    rc = lib.tdq_jet_bf3_pack(_lib.ptr(P), _lib.ptr(scratch), X.shape[0], cfg["d_in"], _warg(cfg),
                               cfg["d_out"], cfg["n_hidden"], S, _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_jet_bf3_pack")
 
@@ -134,7 +143,7 @@ def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, sna
     carr = (ctypes.c_void_p * max(1, len(counters)))(*[c.data_ptr() for c in counters])
     rc = lib.tdq_step_tail_bf3(
         _lib.ptr(work), _lib.ptr(grad), _lib.ptr(scratch) if write_images else None,
-        X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"], cfg["n_hidden"], S, *_lo_args(cfg),
+        X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], S, *_lo_args(cfg),
         _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms, fop.n_scal,
         _lib.ptr(fop.losses), _lib.ptr(fop.total), _lib.ptr(fop.dscal),
         _lib.ptr(hist), int(hist.shape[0]), _lib.ptr(book["epoch"]), _lib.ptr(book["best_loss"]),
@@ -169,7 +178,7 @@ def dp_tail_a(saved, work, grad, fop, total=None, losses=None):
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     losses = fop.losses if losses is None else losses
-    rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
+    rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"],
                                cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
                                fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total),
                                _lib.stream_ptr(X.device))
@@ -182,7 +191,7 @@ def dp_tail_b(saved, group_array, n_groups, improved, snapshot):
     next step's weight images (``tdq_dp_tail_b_bf3``)."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
-    rc = lib.tdq_dp_tail_b_bf3(_lib.ptr(scratch), X.shape[0], cfg["d_in"], cfg["width"], cfg["d_out"],
+    rc = lib.tdq_dp_tail_b_bf3(_lib.ptr(scratch), X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"],
                                cfg["n_hidden"], S, ctypes.cast(group_array, ctypes.c_void_p), n_groups,
                                _lib.ptr(improved), _lib.ptr(snapshot), _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_b_bf3")

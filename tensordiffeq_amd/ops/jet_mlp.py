@@ -62,14 +62,15 @@ def hip_config(net, plan, precision=None):
     hidden = sizes[1:-1]
     if len(hidden) < 1:
         raise ValueError("needs at least one hidden layer")
-    if len(set(hidden)) != 1:
-        raise ValueError("hidden widths must be equal")
+    if len(hidden) > 16:
+        raise ValueError("more than 16 hidden layers")
     if plan.order > 2:
         raise ValueError("derivative order > 2")
     S = plan.S
     if S > MAX_S:
         raise ValueError(f"{S} streams > {MAX_S}")
-    wpad = _pad16(hidden[0])
+    uniform = len(set(hidden)) == 1
+    wpad = _pad16(max(hidden))
     WT = wpad // 16
     if WT not in (1, 2, 4, 8):
         if WT == 3:
@@ -90,7 +91,13 @@ def hip_config(net, plan, precision=None):
     if precision == "fp32" and S * WT > 32:
         raise ValueError(f"fp32 kernels: streams x width tiles = {S * WT} > 32 (register budget); "
                          f"use precision bf16x3 or bf16")
-    return {"d_in": d_in, "d_out": d_out, "width": hidden[0], "WT": WT, "S": S,
+    if precision == "fp32" and not uniform:
+        # the split-bf16 kernels pad unequal hidden layers to the widest; the exact-fp32 family
+        # takes equal widths only
+        if WT < 2:
+            raise ValueError("unequal hidden widths <= 16: no kernel family")
+        precision = "bf16x3"
+    return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
             "n_hidden": len(hidden), "precision": precision}
 
 

@@ -42,6 +42,10 @@ CASES = [
     ([3, 96, 96, 96, 1], [(0, 0), (1, 1), (2, 2), (0, 1)], 300),   # S=8, padded WT=8
     ([2, 128, 128, 1], [(0, 0), (1, 1), (0, 1)], 200),             # S=6, 2 hidden layers
     ([4, 128, 128, 128, 1], [(0,), (1,), (2,), (3,)], 150),         # S=5, first order only
+    # unequal hidden widths (the reference's neural_net takes any layer list): padded to the widest
+    ([2, 64, 128, 32, 1], [(0,), (1,), (0, 0)], 500),              # AC plan, W = 128
+    ([3, 50, 20, 80, 40, 2], [(0,), (1, 1), (2,)], 301),           # padded widths, d_out = 2
+    ([2, 128, 96, 1], [(0, 0), (1, 1)], 200),                      # wide plan (S=5), 2 hidden layers
 ]
 
 
@@ -345,7 +349,7 @@ def test_step_book_and_adam_snapshot_match_torch():
     assert torch.allclose(a[2].cpu(), b[2], rtol=1e-5, atol=1e-6)
 
 
-def _ac_sa_model(prec, n_f=3000, sizes=(2, 128, 128, 128, 128, 1)):
+def _ac_sa_model(prec, n_f=3000, sizes=(2, 128, 128, 128, 128, 1), backend="hip"):
     import math
     import numpy as np
     import tensordiffeq_amd as tdq
@@ -372,7 +376,7 @@ def _ac_sa_model(prec, n_f=3000, sizes=(2, 128, 128, 128, 128, 1)):
               Adaptive_type="self-adaptive", dict_adaptive={"residual": [True], "BCs": [True, False]},
               init_weights={"residual": [torch.rand(n_f, 1, generator=g)],
                             "BCs": [100 * torch.rand(512, 1, generator=g), None]},
-              backend="hip", device="cuda", precision=prec)
+              backend=backend, device="cuda", precision=prec)
     return m
 
 
@@ -402,6 +406,7 @@ def _poisson_model(prec, n_f=3000, sizes=(2, 128, 128, 128, 128, 1)):
 
 TAIL_GEOMS = [
     ("ac", (2, 128, 128, 128, 128, 1)),   # flagship: WT=8, width == W
+    ("ac", (2, 64, 128, 96, 1)),          # unequal hidden widths (padded to 128)
     ("ac", (2, 20, 20, 20, 1)),           # WT=2, padded width
     ("ac", (2, 50, 50, 1)),               # WT=4, padded (bf16: 8-wave backward)
     ("ac", (2, 32, 1)),                   # one hidden layer
@@ -504,3 +509,23 @@ def test_fused_lbfgs_objective_matches_unfused(prec, problem, sizes, monkeypatch
 def np_isfinite(v):
     import math
     return math.isfinite(float(v))
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+def test_solver_unequal_widths_hip_matches_jet(prec):
+    """A network with unequal hidden widths trains on the HIP kernels (padded to the widest layer)
+    and matches the torch jet engine's loss and gradients."""
+    sizes = (2, 64, 128, 96, 1)
+    a = _ac_sa_model(prec, sizes=sizes)
+    b = _ac_sa_model(prec, sizes=sizes, backend="jet")
+    assert a.active_backend == "hip" and b.active_backend == "jet"
+    with torch.no_grad():
+        b.u_model.flat.copy_(a.u_model.flat)
+    la, ga = a.grad()
+    lb, gb = b.grad()
+    tol = {"bf16x3": 1e-4, "bf16": 3e-2}[prec]
+    assert abs(la.item() - lb.item()) / abs(lb.item()) < tol
+    for x, y in zip(ga, gb):
+        assert ((x - y).norm() / y.norm().clamp_min(1e-12)).item() < 10 * tol
+    a.fit(tf_iter=10)
+    assert all(np_isfinite(r["Total Loss"]) for r in a.losses)

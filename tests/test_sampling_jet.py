@@ -88,3 +88,18 @@ def test_jet_gradients_match_autograd():
     f = (torch.stack([u, ux, ut, uxx]) * G).sum()
     g2 = torch.autograd.grad(f, p2)[0]
     assert torch.allclose(g1, g2, atol=1e-10)
+
+
+def test_hip_config_unequal_widths():
+    """Unequal hidden widths are served by the split-bf16 kernels (padded to the widest layer);
+    an exact-fp32 request with unequal widths is promoted to bf16x3."""
+    from tensordiffeq_amd.jet import JetPlan
+    from tensordiffeq_amd.models.networks import TanhMLP
+    from tensordiffeq_amd.ops.jet_mlp import hip_config
+    net = TanhMLP([2, 64, 128, 32, 1], device="cpu")
+    plan = JetPlan([(0,), (1,), (0, 0)], 2)
+    cfg = hip_config(net, plan, "bf16")
+    assert cfg["WT"] == 8 and cfg["widths"] == (64, 128, 32) and cfg["width"] == 128
+    assert hip_config(net, plan, "fp32")["precision"] == "bf16x3"
+    cfg = hip_config(TanhMLP([2, 128, 128, 128, 128, 1], device="cpu"), JetPlan([(0, 0), (1, 1)], 2), "bf16")
+    assert cfg["S"] == 5 and cfg["WT"] == 8   # a wide plan

@@ -25,15 +25,15 @@ TDQ_STUB(bf3_bwd_w4)
 TDQ_STUB(bf3_bwd_w8)
 
 extern "C" {
-int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, int width, int n_hidden, int S, int lo);
-int64_t tdq_jet_bf3_slab_floats(int N, int d_in, int width, int d_out, int n_hidden);
+int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, const int* widths, int n_hidden, int S, int lo);
+int64_t tdq_jet_bf3_slab_floats(int N, int d_in, const int* widths, int d_out, int n_hidden);
 int64_t tdq_jet_scratch_floats(int N, int width, int n_hidden, int S, int unused);
 int64_t tdq_jet_slab_floats(int N, int d_in, int width, int d_out, int n_hidden);
-int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, int width, int d_out,
+int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, const int* widths, int d_out,
                     int n_hidden, int S, const int* spec, int lo, void* stream);
 int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad, int N,
-                    int d_in, int width, int d_out, int n_hidden, int S, const int* spec, int lo, void* stream);
-int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, int width, int d_out, int n_hidden, int S, int lo,
+                    int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo, void* stream);
+int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
                       float* total, void* stream);
 int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
@@ -60,15 +60,16 @@ int main() {
     for (int S = 1; S <= 8; ++S)
       for (int lo = 0; lo < 2; ++lo) {
         int64_t prev = 0;
+        const int ws[4] = {width, width, width / 2 + 1, width};  // unequal hidden widths too
         for (int N : {1, 63, 64, 65, 1000, 50000, 10000000}) {
-          const int64_t a = tdq_jet_bf3_scratch_floats(N, 3, width, 4, S, lo);
+          const int64_t a = tdq_jet_bf3_scratch_floats(N, 3, ws, 4, S, lo);
           if (width <= 16) {
             CHECK(a == -1);
             continue;
           }
           CHECK(a > 0 && a >= prev);
           prev = a;
-          CHECK(tdq_jet_bf3_slab_floats(N, 3, width, 1, 4) > 0);
+          CHECK(tdq_jet_bf3_slab_floats(N, 3, ws, 1, 4) > 0);
         }
         CHECK(tdq_jet_scratch_floats(1000, width, 3, S, 0) > 0);
         CHECK(tdq_jet_slab_floats(1000, 2, width, 1, 3) > 0);
@@ -85,15 +86,17 @@ int main() {
   // entry points reject bad geometry before launching anything (dummy device pointers)
   std::vector<float> dummy(64);
   float* f = dummy.data();
-  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, 128, 1, 4, 9, spec_ok, 0, nullptr) != 0);   // S = 9
-  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, 300, 1, 4, 4, spec_ok, 0, nullptr) != 0);   // width 300
-  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 9, 128, 1, 4, 4, spec_ok, 0, nullptr) != 0);   // d_in 9
-  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, 128, 5, 4, 4, spec_ok, 0, nullptr) != 0);   // d_out 5
-  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, 128, 1, 4, 3, spec_bad, 0, nullptr) != 0);  // bad spec
-  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 0, 2, 128, 1, 4, 4, spec_ok, 0, nullptr) == 0);     // N = 0: no-op
-  CHECK(tdq_jet_bwd_bf3(f, f, f, f, f, f, 100, 2, 128, 1, 0, 4, spec_ok, 1, nullptr) != 0);  // no hidden layer
-  CHECK(tdq_dp_tail_a_bf3(f, f, 100, 2, 128, 1, 4, 9, 0, f, 1, 1, 0, f, f, f, nullptr) != 0);
-  CHECK(tdq_dp_tail_a_bf3(f, f, 0, 2, 128, 1, 4, 4, 0, f, 1, 1, 0, f, f, f, nullptr) != 0);
+  const int w128[4] = {128, 128, 128, 128}, w300[4] = {300, 300, 300, 300};
+  CHECK(tdq_jet_bf3_scratch_floats(100, 2, w128, 17, 4, 0) == -1);  // more than TDQ_MAXL layers
+  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, w128, 1, 4, 9, spec_ok, 0, nullptr) != 0);   // S = 9
+  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, w300, 1, 4, 4, spec_ok, 0, nullptr) != 0);   // width 300
+  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 9, w128, 1, 4, 4, spec_ok, 0, nullptr) != 0);   // d_in 9
+  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, w128, 5, 4, 4, spec_ok, 0, nullptr) != 0);   // d_out 5
+  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, w128, 1, 4, 3, spec_bad, 0, nullptr) != 0);  // bad spec
+  CHECK(tdq_jet_fwd_bf3(f, f, f, f, 0, 2, w128, 1, 4, 4, spec_ok, 0, nullptr) == 0);     // N = 0: no-op
+  CHECK(tdq_jet_bwd_bf3(f, f, f, f, f, f, 100, 2, w128, 1, 0, 4, spec_ok, 1, nullptr) != 0);  // no hidden layer
+  CHECK(tdq_dp_tail_a_bf3(f, f, 100, 2, w128, 1, 4, 9, 0, f, 1, 1, 0, f, f, f, nullptr) != 0);
+  CHECK(tdq_dp_tail_a_bf3(f, f, 0, 2, w128, 1, 4, 4, 0, f, 1, 1, 0, f, f, f, nullptr) != 0);
   double* dd = reinterpret_cast<double*>(f);
   int tk[2] = {0, 0};
   CHECK(tdq_lbfgs_update_fused(f, f, f, f, f, f, f, f, dd, dd, dd, dd, dd, dd, f, tk, 100, 65, 10, 1, 1, 0, 12.5,

@@ -61,8 +61,8 @@ def main():
     ts = torch.zeros(nwg * 4 * 64, dtype=torch.int64, device="cuda")
     lib.tdq_set_timing_buffer(ts.data_ptr())
     J = torch.empty(S, N, 1, device="cuda")
-    scr = torch.empty(lib.tdq_jet_bf3_scratch_floats(N, 2, 128, 4, S, 1), device="cuda")
-    work = torch.empty(lib.tdq_jet_bf3_slab_floats(N, 2, 128, 1, 4), device="cuda")
+    scr = torch.empty(lib.tdq_jet_bf3_scratch_floats(N, 2, (ctypes.c_int * 4)(128, 128, 128, 128), 4, S, 1), device="cuda")
+    work = torch.empty(lib.tdq_jet_bf3_slab_floats(N, 2, (ctypes.c_int * 4)(128, 128, 128, 128), 1, 4), device="cuda")
     grad = torch.empty_like(net.flat)
     dJ = torch.randn(S, N, 1, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
