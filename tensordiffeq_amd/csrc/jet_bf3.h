@@ -379,10 +379,16 @@ struct Tl {
 __device__ __forceinline__ Tl tl_make(const void* uniform_base, int lane) {
   return Tl{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_base), 0, 0x7fffffff, 0x00020000), lane * 16};
 }
-#ifdef TDQ_TEMPORAL_STORES
-#define TDQ_POL_ST 0
+// Round 3 (profiles/r3_f_ab.txt): precision bf16 is faster with default-policy stores (0.2155-0.2175
+// vs 0.2235-0.2243 ms per AC-SA step; a pure 217 MB store stream: 38 us default vs 60 us nt,
+// tools/microbench/store_bw.hip), bf16x3 stays faster with nt stores (0.451-0.455 vs 0.480-0.481).
+// -DTDQ_TEMPORAL_STORES: default policy for both; -DTDQ_NT_STORES: nt for both.
+#if defined(TDQ_TEMPORAL_STORES)
+#define TDQ_POL_ST_LO(LO) 0
+#elif defined(TDQ_NT_STORES)
+#define TDQ_POL_ST_LO(LO) 2
 #else
-#define TDQ_POL_ST 2  // nt
+#define TDQ_POL_ST_LO(LO) ((LO) ? 2 : 0)
 #endif
 #ifdef TDQ_TEMPORAL_LOADS
 #define TDQ_POL_LD 0
@@ -443,14 +449,14 @@ __device__ __forceinline__ void hs_store(const Tl& T, int s, int t, const f32x4&
   if constexpr (TDQ_HS_HALF(LO)) {
     if (s == 0 && !TDQ_HS_V16) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_half_off<WT>(0, t),
-                                             TDQ_POL_ST);
+                                             TDQ_POL_ST_LO(LO));
       return;
     }
     const u32x2v u = s == 0 ? __builtin_bit_cast(u32x2v, __builtin_convertvector(v, f16x4))
                             : __builtin_bit_cast(u32x2v, __builtin_convertvector(v, bf16x4));
-    __builtin_amdgcn_raw_buffer_store_b64(u, T.r, T.v >> 1, hs_half_off<WT>(s, t), TDQ_POL_ST);
+    __builtin_amdgcn_raw_buffer_store_b64(u, T.r, T.v >> 1, hs_half_off<WT>(s, t), TDQ_POL_ST_LO(LO));
   } else {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_ST);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), T.r, T.v, hs_off(s, t, WT) * 4, TDQ_POL_ST_LO(LO));
   }
 }
 template <int WT, bool LO, int POL>

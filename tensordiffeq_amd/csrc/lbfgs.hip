@@ -347,14 +347,23 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   //    v_readlane (uniform q; a ds_bpermute shuffle costs ~10x its latency) and multiplied by the
   //    pivot's reciprocal, computed for every lane in parallel up front (no fp64 division on the
   //    dependent chain): the logic kernel went from ~22 us to a few us per iteration.
+  //    The lane's row (back) / column (forward) of R is read into registers first and the
+  //    substitution loops are unrolled over the 64 possible pairs, so each step's dependent chain
+  //    is readlane -> mul -> fma with no memory access on it.
   if (tid < 64) {
     const int j = tid;
     const double rdj = j < k ? 1.0 / Rc[j * m + j] : 0.0;
+    double row[LB_MAXM];
+#pragma unroll
+    for (int q = 0; q < LB_MAXM; ++q) row[q] = (q < k && j < k) ? Rc[j * m + q] : 0.0;
     double r = j < k ? aC[j] : 0.0, u = 0.0;
-    for (int q = k - 1; q >= 0; --q) {  // back substitution
-      const double uq = readlane_d(r, q) * readlane_d(rdj, q);
-      if (j == q) u = uq;
-      if (j < q) r -= Rc[j * m + q] * uq;
+#pragma unroll
+    for (int q = LB_MAXM - 1; q >= 0; --q) {  // back substitution
+      if (q < k) {
+        const double uq = readlane_d(r, q) * readlane_d(rdj, q);
+        if (j == q) u = uq;
+        if (j < q) r -= row[q] * uq;
+      }
     }
     uS[j] = j < k ? u : 0.0;
   }
@@ -368,11 +377,17 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
       for (int q = 0; q < k; ++q) yu += YYc[j * m + q] * uS[q];
       rhs = Rc[j * m + j] * uS[j] + gam * yu - gam * bC[j];
     }
+    double col[LB_MAXM];
+#pragma unroll
+    for (int q = 0; q < LB_MAXM; ++q) col[q] = (q < k && j < k) ? Rc[q * m + j] : 0.0;
     double rr = rhs, p1 = 0.0;
-    for (int q = 0; q < k; ++q) {  // forward substitution with R^T
-      const double pq = readlane_d(rr, q) * readlane_d(rdj, q);
-      if (j == q) p1 = pq;
-      if (j > q && j < k) rr -= Rc[q * m + j] * pq;
+#pragma unroll
+    for (int q = 0; q < LB_MAXM; ++q) {  // forward substitution with R^T
+      if (q < k) {
+        const double pq = readlane_d(rr, q) * readlane_d(rdj, q);
+        if (j == q) p1 = pq;
+        if (j > q && j < k) rr -= col[q] * pq;
+      }
     }
     pS[j] = j < k ? p1 : 0.0;
   }
