@@ -217,6 +217,16 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   for (int v = tid; v < (m + 1) * LB_NF; v += 256) {
     double a0 = 0.0, a1 = 0.0;
     int ch = 0;
+    for (; ch + 7 < c.nchunks; ch += 8) {  // eight loads in flight, the same summation order
+      double q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = part_ld<SC1>(&part[(size_t)(ch + u) * (m + 1) * LB_NF + v]);
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        a0 += q[u];
+        a1 += q[u + 1];
+      }
+    }
     for (; ch + 1 < c.nchunks; ch += 2) {
       a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
       a1 += part_ld<SC1>(&part[(size_t)(ch + 1) * (m + 1) * LB_NF + v]);
@@ -327,11 +337,28 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   }
   __syncthreads();
   // 4. chronological k x k blocks and right-hand sides into LDS
-  for (int e = tid; e < k * k; e += 256) {
-    const int a = e / k, b = e - a * k;
-    const int ia = (head + a) % m, ib = (head + b) % m;
-    Rc[a * m + b] = a <= b ? SY[ia * m + ib] : 0.0;
-    YYc[a * m + b] = YY[ia * m + ib];
+  //    (four elements per thread and round: their eight global loads are in flight together)
+  for (int e0 = tid; e0 < k * k; e0 += 4 * 256) {
+    double sy[4], yy[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      if (e < k * k) {
+        const int a = e / k, b = e - a * k;
+        const int ia = (head + a) % m, ib = (head + b) % m;
+        sy[u] = SY[ia * m + ib];
+        yy[u] = YY[ia * m + ib];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      if (e < k * k) {
+        const int a = e / k, b = e - a * k;
+        Rc[a * m + b] = a <= b ? sy[u] : 0.0;
+        YYc[a * m + b] = yy[u];
+      }
+    }
   }
   if (tid < k) {
     const int ij = (head + tid) % m;

@@ -31,6 +31,16 @@ def _build(dist):
     return m
 
 
+def _np(t):
+    """Queue payloads travel as numpy: a torch tensor would be sent as a shared-memory handle that
+    disappears once the sending process exits (FileNotFoundError in the receiver)."""
+    return t.detach().cpu().numpy().copy()
+
+
+def _t(a):
+    return torch.from_numpy(a)
+
+
 def _worker(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -42,12 +52,12 @@ def _worker(rank, world, port, q):
     eng = m._get_engine(None, 10)
     loss, grads, terms = eng._phase_a()
     loss, grads, terms = eng._reduce(loss, grads, terms)
-    res = {"loss": float(loss), "gflat": grads[0].clone(), "glam_bc": grads[2].clone()}
+    res = {"loss": float(loss), "gflat": _np(grads[0]), "glam_bc": _np(grads[2])}
     m.fit(tf_iter=5)
-    res["flat_after"] = m.u_model.flat.detach().clone()
+    res["flat_after"] = _np(m.u_model.flat)
     res["hist"] = [h["Total Loss"] for h in m.losses]
     m.fit(newton_iter=3)
-    res["flat_lbfgs"] = m.u_model.flat.detach().clone()
+    res["flat_lbfgs"] = _np(m.u_model.flat)
     if rank == 0:
         q.put(res)
     ctx.barrier()
@@ -77,11 +87,11 @@ def test_dp_gloo_matches_single_process(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res["loss"] == pytest.approx(float(loss), rel=1e-5)
-    assert torch.allclose(res["gflat"], grads[0], rtol=1e-4, atol=1e-6)
-    assert torch.allclose(res["glam_bc"], grads[2], rtol=1e-4, atol=1e-7)
+    assert torch.allclose(_t(res["gflat"]), grads[0], rtol=1e-4, atol=1e-6)
+    assert torch.allclose(_t(res["glam_bc"]), grads[2], rtol=1e-4, atol=1e-7)
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-4)
-    assert torch.allclose(res["flat_after"], ref_flat, atol=1e-5)
-    assert torch.allclose(res["flat_lbfgs"], ref_lbfgs, atol=1e-4)
+    assert torch.allclose(_t(res["flat_after"]), ref_flat, atol=1e-5)
+    assert torch.allclose(_t(res["flat_lbfgs"]), ref_lbfgs, atol=1e-4)
 
 
 def _worker_batched(rank, world, port, q):
@@ -95,8 +105,8 @@ def _worker_batched(rank, world, port, q):
     batches = m.minibatches(50)
     m.fit(tf_iter=2, batch_sz=50)
     q.put({"rank": rank, "n_local": m.X_f_local.shape[0], "batches": batches,
-           "epochs": int(m._state["epoch_host"]), "flat": m.u_model.flat.detach().clone(),
-           "lam": m.lambdas[0].detach().clone()})
+           "epochs": int(m._state["epoch_host"]), "flat": _np(m.u_model.flat),
+           "lam": _np(m.lambdas[0])})
     ctx.barrier()
     pdist.destroy()
 
@@ -118,7 +128,7 @@ def test_dp_minibatch_uneven_shards():
     assert [r["n_local"] for r in res] == [151, 150]
     assert res[0]["batches"] == res[1]["batches"] == [(0, 50), (50, 100), (100, 150)]
     assert res[0]["epochs"] == res[1]["epochs"] == 6
-    assert torch.equal(res[0]["flat"], res[1]["flat"])
+    assert (res[0]["flat"] == res[1]["flat"]).all()
     assert res[0]["lam"].shape == (151, 1) and res[1]["lam"].shape == (150, 1)
 
 
@@ -168,8 +178,8 @@ def _worker_discovery(rank, world, port, q):
     ctx = pdist.init_distributed(backend="gloo", device="cpu")
     m, var = _build_discovery(True)
     m.fit(tf_iter=4)
-    res = {"rank": rank, "flat": m.u_model.flat.detach().clone(), "var": float(var[0].detach()),
-           "cw": m.col_weights.detach().clone(), "lo": m._lo, "hi": m._hi}
+    res = {"rank": rank, "flat": _np(m.u_model.flat), "var": float(var[0].detach()),
+           "cw": _np(m.col_weights), "lo": m._lo, "hi": m._hi}
     q.put(res)
     ctx.barrier()
     pdist.destroy()
@@ -191,10 +201,10 @@ def test_discovery_dp_gloo_matches_single_process():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert torch.equal(res[0]["flat"], res[1]["flat"])
-    assert torch.allclose(res[0]["flat"], ref.u_model.flat.detach(), atol=1e-5)
+    assert (res[0]["flat"] == res[1]["flat"]).all()
+    assert torch.allclose(_t(res[0]["flat"]), ref.u_model.flat.detach(), atol=1e-5)
     assert res[0]["var"] == pytest.approx(float(rvar[0].detach()), rel=1e-4, abs=1e-7)
-    cw = torch.cat([r["cw"] for r in res])
+    cw = torch.cat([_t(r["cw"]) for r in res])
     assert torch.allclose(cw, ref.col_weights.detach(), atol=1e-5)
 
 
