@@ -6,18 +6,19 @@
 // the same HIP graph as the loss/gradient evaluation, and the host reads nothing until it polls
 // the "active" flag every few dozen iterations:
 //
-//   lbfgs_dots   grid (chunks, m + 1): every dot product the iteration needs in ONE pass over the
-//                history ring - per slot i: s_i.g, y_i.g, s_i.y, y_i.y, s.y_i - and for the new pair
-//                s.y, y.y, s.g, y.g plus |g|_1 (s = t d, y = g - g_old formed on the fly); fp64
-//                partial sums per chunk;
+//   lbfgs_dots   grid (chunks, slot groups of LB_G): every dot product the iteration needs in ONE
+//                pass over the history ring - per slot i: s_i.g, y_i.g, s_i.y, y_i.y, s.y_i - and for
+//                the new pair s.y, y.y, s.g, y.g plus |g|_1 (s = t d, y = g - g_old formed on the
+//                fly); fp64 partial sums per chunk;
 //   lbfgs_logic  one workgroup: reduces the partials in fixed order, runs the post-evaluation tests
 //                (NaN, best iterate, maxIter / maxEval, tolFun / tolX / |f - f_old|), the curvature
 //                test y.s > 1e-10 with ring push (H0 = y.s / y.y), keeps S^T Y and Y^T Y current by
 //                one new row + column per push, and turns the compact representation of Byrd,
 //                Nocedal & Schnabel (1994) into per-slot coefficients with two k x k triangular
-//                solves (one lane per history pair, R and Y^T Y in LDS);
-//   lbfgs_dir    elementwise: stores the pushed pair into the ring, d = cG g + sum_i (cS_i s_i +
-//                cY_i y_i), g_old = g, best-weights snapshot, partials of g.d and |d|_1;
+//                solves (one wave, one lane per history pair, rows in registers);
+//   lbfgs_dir    64-element tiles, the history sum split over the block's 4 waves: stores the
+//                pushed pair into the ring, d = cG g + sum_i (cS_i s_i + cY_i y_i), g_old = g,
+//                best-weights snapshot, partials of g.d and |d|_1;
 //   lbfgs_step   one workgroup: descent test g.d > -tolX, step t = min(1, 1/|g|_1) on the first
 //                iteration else the fixed learning rate (0.8, reference fit.py:67), f_old = f;
 //   lbfgs_axpy   x += t d (launched in front of the next evaluation).
@@ -114,78 +115,128 @@ __device__ __forceinline__ double readlane_d(double v, int q) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
-// d_j = cG g_j + sum_i (cS_i s_ij + cY_i y_ij) over the k history pairs (oldest first), four
-// independent partial sums so the 2k strided loads overlap; shared by both update paths (same
-// summation order, so the same bits)
-__device__ __forceinline__ double dir_elem(const float* __restrict__ S, const float* __restrict__ Y,
-                                           const double* __restrict__ coef, int j, int p, int k, int head, int m,
-                                           int pushed, int slot, float s, float y, double dn) {
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  int q = 0;
-  for (; q + 3 < k; q += 4) {
+// d_j = cG g_j + sum_q (cS_q s_qj + cY_q y_qj) over the k history pairs (chronological q): the
+// four waves of a direction block share one 64-element tile, wave w sums the pairs of quarter w
+// (at most LB_MAXM / 4, every load of it in flight together), and wave 0 adds the quarters in
+// fixed order.  Shared by both update paths (same summation order, so the same bits).
+__device__ __forceinline__ double dir_quarter(const float* __restrict__ S, const float* __restrict__ Y,
+                                              const double* __restrict__ coef, int j, int p, int k, int head, int m,
+                                              int pushed, int slot, float tf, float g, float dj, float oj, int w) {
+  const int q0 = (w * k) >> 2, q1 = ((w + 1) * k) >> 2;
+  double acc[2] = {0.0, 0.0};
+  // branch-free so every load of the quarter is in flight together: past the quarter's end the
+  // first pair is re-read and masked out; the pushed slot's row is read (this block has not
+  // overwritten it yet) and replaced by the new pair
+  constexpr int NQ = LB_MAXM / 4;
+  int ir[NQ];
+  float sl[NQ], yl[NQ];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = (head + q + u) % m;
-      const bool nw = pushed && i == slot;
-      const double si = nw ? (double)s : (double)S[(size_t)i * p + j];
-      const double yi = nw ? (double)y : (double)Y[(size_t)i * p + j];
-      acc[u] += coef[i] * si + coef[m + i] * yi;
-    }
+  for (int t = 0; t < NQ; ++t) {
+    int i = head + (q0 + t < q1 ? q0 + t : q0);
+    if (i >= m) i -= m;
+    ir[t] = i;
+    // uniform row bases (scalar registers) + the lane's 32-bit element offset
+    sl[t] = (S + (size_t)i * p)[j];
+    yl[t] = (Y + (size_t)i * p)[j];
   }
-  for (; q < k; ++q) {
-    const int i = (head + q) % m;
+  const float s = tf * dj, y = g - oj;  // the new pair (after the loads: nothing waits on them)
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const int i = ir[t];
     const bool nw = pushed && i == slot;
-    const double si = nw ? (double)s : (double)S[(size_t)i * p + j];
-    const double yi = nw ? (double)y : (double)Y[(size_t)i * p + j];
-    acc[0] += coef[i] * si + coef[m + i] * yi;
+    const double si = nw ? (double)s : (double)sl[t];
+    const double yi = nw ? (double)y : (double)yl[t];
+    const double v = coef[i] * si + coef[m + i] * yi;
+    acc[t & 1] += (q0 + t < q1) ? v : 0.0;
   }
-  return dn + ((acc[0] + acc[1]) + (acc[2] + acc[3]));
+  return acc[0] + acc[1];
 }
 
 // ---------------------------------------------------------------------------------------------
-// the partial sums of one (chunk, slot) block of the dots grid -> part (thread 0 stores them)
+// the partial sums of one (chunk, slot group) block of the dots grid -> part (thread 0 stores
+// them).  A block covers LB_G history slots (the new pair is slot m); a thread takes LB_R
+// elements per round and issues every load of the round (g, d, g_old and the 2 LB_G history
+// values of each element) before the first use, so a round costs one memory latency.  Each
+// slot's sum runs over its elements in a fixed order shared by both update paths.
+#define LB_G 1
+#define LB_R 8
 template <bool SC1>
 __device__ __forceinline__ void lbfgs_dots_body(const float* __restrict__ fg, const float* __restrict__ g_old,
                                                 const float* __restrict__ d, const float* __restrict__ S,
                                                 const float* __restrict__ Y, const double* __restrict__ st,
                                                 double* __restrict__ part, const LbCfg& c, double* red) {
-  const int i = blockIdx.y, ch = blockIdx.x;
+  const int i0 = blockIdx.y * LB_G, ch = blockIdx.x;
   const int lo = (int)(((long long)c.p * ch) / c.nchunks), hi = (int)(((long long)c.p * (ch + 1)) / c.nchunks);
   const float tf = (float)st[LB_T];
   const int k = (int)st[LB_K], head = (int)st[LB_HEAD];
-  const bool run = st[LB_ACTIVE] != 0.0 && (i == c.m || slot_valid(i, head, k, c.m));
-  double a[LB_NF] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (run) {
-    if (i == c.m) {
-      for (int j = lo + (int)threadIdx.x; j < hi; j += 256) {
-        const float g = fg[j];
-        const float s = tf * d[j], y = g - g_old[j];
-        a[0] += (double)s * y;
-        a[1] += (double)y * y;
-        a[2] += (double)s * g;
-        a[3] += (double)y * g;
-        a[4] += fabs((double)g);
+  const bool active = st[LB_ACTIVE] != 0.0;
+  bool run[LB_G];
+  const float* Si[LB_G];
+  const float* Yi[LB_G];
+#pragma unroll
+  for (int u = 0; u < LB_G; ++u) {
+    const int i = i0 + u;
+    run[u] = active && i < c.m && slot_valid(i, head, k, c.m);
+    Si[u] = S + (size_t)(run[u] ? i : 0) * c.p;  // row 0 for idle slots: the loads stay unconditional
+    Yi[u] = Y + (size_t)(run[u] ? i : 0) * c.p;
+  }
+  const bool newp = active && i0 <= c.m && c.m < i0 + LB_G;  // this group holds the new pair
+  double a[LB_G][LB_NF];
+#pragma unroll
+  for (int u = 0; u < LB_G; ++u)
+#pragma unroll
+    for (int q = 0; q < LB_NF; ++q) a[u][q] = 0.0;
+  for (int j0 = lo + (int)threadIdx.x; j0 < hi; j0 += 256 * LB_R) {
+    float gv[LB_R], dv[LB_R], ov[LB_R], sv[LB_G][LB_R], yv[LB_G][LB_R];
+#pragma unroll
+    for (int r = 0; r < LB_R; ++r) {
+      const int j = min(j0 + 256 * r, hi - 1);  // clamped: past the chunk's end masked below
+      gv[r] = fg[j];
+      dv[r] = d[j];
+      ov[r] = g_old[j];
+#pragma unroll
+      for (int u = 0; u < LB_G; ++u) {
+        sv[u][r] = Si[u][j];
+        yv[u][r] = Yi[u][j];
       }
-    } else {
-      const float* Si = S + (size_t)i * c.p;
-      const float* Yi = Y + (size_t)i * c.p;
-      for (int j = lo + (int)threadIdx.x; j < hi; j += 256) {
-        const float g = fg[j];
-        const float s = tf * d[j], y = g - g_old[j];
-        const double si = Si[j], yi = Yi[j];
-        a[0] += si * g;
-        a[1] += yi * g;
-        a[2] += si * y;
-        a[3] += yi * y;
-        a[4] += (double)s * yi;
+    }
+#pragma unroll
+    for (int r = 0; r < LB_R; ++r) {
+      if (j0 + 256 * r >= hi) break;
+      const float g = gv[r];
+      const float s = tf * dv[r], y = g - ov[r];
+#pragma unroll
+      for (int u = 0; u < LB_G; ++u) {
+        if (i0 + u == c.m) {
+          if (newp) {
+            a[u][0] += (double)s * y;
+            a[u][1] += (double)y * y;
+            a[u][2] += (double)s * g;
+            a[u][3] += (double)y * g;
+            a[u][4] += fabs((double)g);
+          }
+        } else if (run[u]) {
+          const double si = sv[u][r], yi = yv[u][r];
+          a[u][0] += si * g;
+          a[u][1] += yi * g;
+          a[u][2] += si * y;
+          a[u][3] += yi * y;
+          a[u][4] += (double)s * yi;
+        }
       }
     }
   }
-  block_sum<LB_NF>(a, red);
+  double* flat = &a[0][0];
+  block_sum<LB_G * LB_NF>(*reinterpret_cast<double(*)[LB_G * LB_NF]>(flat), red);
   if (threadIdx.x == 0) {
-    double* o = part + ((size_t)ch * (c.m + 1) + i) * LB_NF;
 #pragma unroll
-    for (int q = 0; q < LB_NF; ++q) part_st<SC1>(&o[q], a[q]);
+    for (int u = 0; u < LB_G; ++u) {
+      const int i = i0 + u;
+      if (i > c.m) break;
+      double* o = part + ((size_t)ch * (c.m + 1) + i) * LB_NF;
+#pragma unroll
+      for (int q = 0; q < LB_NF; ++q) part_st<SC1>(&o[q], a[u][q]);
+    }
   }
 }
 
@@ -193,239 +244,243 @@ __global__ void __launch_bounds__(256) lbfgs_dots_kernel(const float* __restrict
                                                          const float* __restrict__ d, const float* __restrict__ S,
                                                          const float* __restrict__ Y, const double* __restrict__ st,
                                                          double* __restrict__ part, LbCfg c) {
-  __shared__ double red[4 * LB_NF];
+  __shared__ double red[4 * LB_G * LB_NF];
   lbfgs_dots_body<false>(fg, g_old, d, S, Y, st, part, c, red);
 }
 
 // ---------------------------------------------------------------------------------------------
-// dynamic LDS (doubles): dots[(m+1)*5] | Rc[m*m] | YYc[m*m] | aC[64] | bC[64] | uS[64] | pS[64]
+// S^T Y and Y^T Y live in global memory by PHYSICAL ring slot (m x m each).  The logic copies both
+// into LDS while it reduces the dot partials (every load of a thread issued before the first
+// store), patches the pushed slot's row and column in both copies, and solves from LDS.
+//
+// dynamic LDS (doubles): dots[(m+1)*5] | SYl[m*m] | YYl[m*m]
+__host__ __device__ inline size_t lbfgs_logic_lds(int m) { return ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m) * 8; }
+
 template <bool SC1>
 __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, const double* __restrict__ part,
                                                  double* __restrict__ st, double* __restrict__ SY,
                                                  double* __restrict__ YY, double* __restrict__ coef,
-                                                 float* __restrict__ fhist, const LbCfg& c, double* lb_lds,
-                                                 int* flag) {
-  const int tid = threadIdx.x, m = c.m;
+                                                 float* __restrict__ fhist, const LbCfg& c, double* lb_lds) {
+  const int tid = threadIdx.x, m = c.m, mm = m * m;
   double* dots = lb_lds;
-  double* Rc = dots + (m + 1) * LB_NF;
-  double* YYc = Rc + m * m;
-  double* aC = YYc + m * m;
-  double* bC = aC + 64;
-  double* uS = bC + 64;
-  double* pS = uS + 64;
-  // 1. reduce the chunk partials (fixed order: deterministic)
-  for (int v = tid; v < (m + 1) * LB_NF; v += 256) {
-    double a0 = 0.0, a1 = 0.0;
-    int ch = 0;
-    for (; ch + 7 < c.nchunks; ch += 8) {  // eight loads in flight, the same summation order
-      double q[8];
+  double* SYl = dots + (m + 1) * LB_NF;
+  double* YYl = SYl + mm;
+  // 1. copy S^T Y / Y^T Y into LDS and reduce the chunk partials (fixed order: deterministic)
+  {
+    constexpr int NE = (LB_MAXM * LB_MAXM + 255) / 256;
+    double sv[NE], yv[NE];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) q[u] = part_ld<SC1>(&part[(size_t)(ch + u) * (m + 1) * LB_NF + v]);
+    for (int r = 0; r < NE; ++r) {
+      const int e = min(tid + 256 * r, mm - 1);
+      sv[r] = SY[e];
+      yv[r] = YY[e];
+    }
+    for (int v = tid; v < (m + 1) * LB_NF; v += 256) {
+      double a0 = 0.0, a1 = 0.0;
+      int ch = 0;
+      for (; ch + 15 < c.nchunks; ch += 16) {  // sixteen loads in flight
+        double q[16];
 #pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        a0 += q[u];
-        a1 += q[u + 1];
+        for (int u = 0; u < 16; ++u) q[u] = part_ld<SC1>(&part[(size_t)(ch + u) * (m + 1) * LB_NF + v]);
+#pragma unroll
+        for (int u = 0; u < 16; u += 2) {
+          a0 += q[u];
+          a1 += q[u + 1];
+        }
+      }
+      if (ch + 7 < c.nchunks) {
+        double q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = part_ld<SC1>(&part[(size_t)(ch + u) * (m + 1) * LB_NF + v]);
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+          a0 += q[u];
+          a1 += q[u + 1];
+        }
+        ch += 8;
+      }
+      for (; ch + 1 < c.nchunks; ch += 2) {
+        a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
+        a1 += part_ld<SC1>(&part[(size_t)(ch + 1) * (m + 1) * LB_NF + v]);
+      }
+      if (ch < c.nchunks) a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
+      dots[v] = a0 + a1;
+    }
+#pragma unroll
+    for (int r = 0; r < NE; ++r) {
+      const int e = tid + 256 * r;
+      if (e < mm) {
+        SYl[e] = sv[r];
+        YYl[e] = yv[r];
       }
     }
-    for (; ch + 1 < c.nchunks; ch += 2) {
-      a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
-      a1 += part_ld<SC1>(&part[(size_t)(ch + 1) * (m + 1) * LB_NF + v]);
-    }
-    if (ch < c.nchunks) a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
-    dots[v] = a0 + a1;
   }
   __syncthreads();
+  // everything below runs on wave 0: the scalar logic is evaluated by every lane (uniform values,
+  // lane 0 stores), the pair coefficients with one lane per history pair - no further barriers
+  // (LDS accesses of one wave complete in program order; the wavefront fences below only keep
+  // the compiler from reordering them)
+  if (tid >= 64) return;
+  const int lane = tid;
+  const bool L0 = lane == 0;
   // 2. post-evaluation tests of the previous step (reference optimizers.py:241-296, with the
   //    B9 fixes of eager_lbfgs), then the curvature test and ring push (optimizers.py:168-185)
-  if (tid == 0) {
-    const double* sc = dots + m * LB_NF;  // s.y, y.y, s.g, y.g, |g|_1
-    const double f = (double)fg[c.p];
-    int n_iter = (int)st[LB_NITER];
-    int best = 0, done = 0, reason = LB_R_RUN;
-    double minloss = st[LB_MINLOSS];
-    st[LB_G1] = sc[4];
-    if (n_iter == 0) {
-      if (fhist != nullptr && c.fhist_len > 0) fhist[0] = (float)f;
-      if (isfinite(f)) {
+  const double* sc = dots + m * LB_NF;  // s.y, y.y, s.g, y.g, |g|_1
+  const double f = (double)fg[c.p];
+  int n_iter = (int)st[LB_NITER];
+  const double fe0 = st[LB_FEVAL], dt1 = st[LB_DT1], fold = st[LB_FOLD], hd_old = st[LB_HDIAG];
+  double minloss = st[LB_MINLOSS];
+  int k = (int)st[LB_K], head = (int)st[LB_HEAD];
+  int best = 0, done = 0, reason = LB_R_RUN;
+  if (L0) st[LB_G1] = sc[4];
+  if (n_iter == 0) {
+    if (L0 && fhist != nullptr && c.fhist_len > 0) fhist[0] = (float)f;
+    if (isfinite(f)) {
+      best = 1;
+      minloss = f;
+      if (L0) st[LB_BESTEP] = -1.0;
+    }
+    if (sc[4] <= c.tol_fun) {
+      done = 1;
+      reason = LB_R_TOLFUN0;
+    }
+  } else {
+    const double fe = fe0 + 1.0;
+    if (L0) st[LB_FEVAL] = fe;
+    if (L0 && fhist != nullptr && n_iter < c.fhist_len) fhist[n_iter] = (float)f;
+    if (isnan(f)) {
+      done = 1;
+      reason = LB_R_NAN;
+    } else {
+      if (f < minloss) {
         best = 1;
         minloss = f;
-        st[LB_BESTEP] = -1.0;
+        if (L0) st[LB_BESTEP] = (double)(n_iter - 1);
       }
-      if (sc[4] <= c.tol_fun) {
+      if (n_iter >= c.max_iter || fe >= c.max_eval) {
         done = 1;
-        reason = LB_R_TOLFUN0;
-      }
-    } else {
-      const double fe = st[LB_FEVAL] + 1.0;
-      st[LB_FEVAL] = fe;
-      if (fhist != nullptr && n_iter < c.fhist_len) fhist[n_iter] = (float)f;
-      if (isnan(f)) {
+        reason = LB_R_MAXITER;
+      } else if (sc[4] <= c.tol_fun || dt1 <= c.tol_x || (c.legacy_stop ? fabs(f) : fabs(f - fold)) < c.tol_x) {
         done = 1;
-        reason = LB_R_NAN;
-      } else {
-        if (f < minloss) {
-          best = 1;
-          minloss = f;
-          st[LB_BESTEP] = (double)(n_iter - 1);
-        }
-        if (n_iter >= c.max_iter || fe >= c.max_eval) {
-          done = 1;
-          reason = LB_R_MAXITER;
-        } else if (sc[4] <= c.tol_fun || st[LB_DT1] <= c.tol_x ||
-                   (c.legacy_stop ? fabs(f) : fabs(f - st[LB_FOLD])) < c.tol_x) {
-          done = 1;
-          reason = LB_R_TOL;
-        }
+        reason = LB_R_TOL;
       }
     }
+  }
+  if (L0) {
     st[LB_F] = f;
     st[LB_MINLOSS] = minloss;
     st[LB_BEST] = (double)best;
-    int pushed = 0, slot = -1;
-    int k = (int)st[LB_K], head = (int)st[LB_HEAD];
-    if (done) {
+  }
+  int pushed = 0, slot = -1;
+  double hd = hd_old;
+  const double ys = sc[0], yy = sc[1];
+  if (done) {
+    if (L0) {
       st[LB_ACTIVE] = 0.0;
       st[LB_REASON] = (double)reason;
-    } else {
-      n_iter += 1;
-      st[LB_NITER] = (double)n_iter;
-      if (n_iter > 1) {
-        const double ys = sc[0], yy = sc[1];
-        if (ys > 1e-10) {
-          if (k == m) {
-            slot = head;
-            head = (head + 1) % m;
-          } else {
-            slot = (head + k) % m;
-            k += 1;
-          }
-          st[LB_K] = (double)k;
-          st[LB_HEAD] = (double)head;
-          st[LB_HDIAG] = ys / yy;
-          SY[slot * m + slot] = ys;
-          YY[slot * m + slot] = yy;
-          pushed = 1;
-        }
-      }
+      st[LB_PUSHED] = 0.0;
+      st[LB_SLOT] = -1.0;
     }
-    st[LB_PUSHED] = (double)pushed;
-    st[LB_SLOT] = (double)slot;
-    flag[0] = !done;
-    flag[1] = n_iter;
-    flag[2] = pushed;
-    flag[3] = slot;
-    flag[4] = k;
-    flag[5] = head;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  const int n_iter = flag[1], pushed = flag[2], slot = flag[3], k = flag[4], head = flag[5];
-  const double gam = n_iter == 1 ? 1.0 : st[LB_HDIAG];
-  if (n_iter == 1 || k == 0) {  // d = -H0 g (first iteration: H0 = I)
-    for (int v = tid; v < 2 * m; v += 256) coef[v] = 0.0;
-    if (tid == 0) coef[2 * m] = -gam;
     return;
   }
-  // 3. new row / column of S^T Y and Y^T Y (physical slot indices; every other valid slot was
-  //    valid before the push, so its dots are current)
-  if (pushed && tid < m && tid != slot && slot_valid(tid, head, k, m)) {
-    const double* dj = dots + tid * LB_NF;
-    SY[slot * m + tid] = dj[4];  // s_new . y_j
-    SY[tid * m + slot] = dj[2];  // s_j . y_new
-    YY[tid * m + slot] = dj[3];
-    YY[slot * m + tid] = dj[3];
-  }
-  __syncthreads();
-  // 4. chronological k x k blocks and right-hand sides into LDS
-  //    (four elements per thread and round: their eight global loads are in flight together)
-  for (int e0 = tid; e0 < k * k; e0 += 4 * 256) {
-    double sy[4], yy[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256;
-      if (e < k * k) {
-        const int a = e / k, b = e - a * k;
-        const int ia = (head + a) % m, ib = (head + b) % m;
-        sy[u] = SY[ia * m + ib];
-        yy[u] = YY[ia * m + ib];
-      }
+  n_iter += 1;
+  if (n_iter > 1 && ys > 1e-10) {
+    if (k == m) {
+      slot = head;
+      head = (head + 1) % m;
+    } else {
+      slot = (head + k) % m;
+      k += 1;
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256;
-      if (e < k * k) {
-        const int a = e / k, b = e - a * k;
-        Rc[a * m + b] = a <= b ? sy[u] : 0.0;
-        YYc[a * m + b] = yy[u];
-      }
-    }
+    hd = ys / yy;
+    pushed = 1;
   }
-  if (tid < k) {
-    const int ij = (head + tid) % m;
-    const bool nw = pushed && ij == slot;
-    aC[tid] = nw ? dots[m * LB_NF + 2] : dots[ij * LB_NF + 0];  // s_j . g
-    bC[tid] = nw ? dots[m * LB_NF + 3] : dots[ij * LB_NF + 1];  // y_j . g
+  if (L0) {
+    st[LB_NITER] = (double)n_iter;
+    st[LB_K] = (double)k;
+    st[LB_HEAD] = (double)head;
+    st[LB_HDIAG] = hd;
+    st[LB_PUSHED] = (double)pushed;
+    st[LB_SLOT] = (double)slot;
   }
-  __syncthreads();
-  // 5. compact product on wave 0 (lane j = chronological pair j):
+  const double gam = n_iter == 1 ? 1.0 : hd;
+  // 3. the pushed slot's row / column of S^T Y and Y^T Y, in memory (later iterations) and LDS
+  if (pushed && lane < m && slot_valid(lane, head, k, m)) {
+    const int j = lane;
+    const double* dj = dots + j * LB_NF;
+    const double snj = j == slot ? ys : dj[4], sjn = j == slot ? ys : dj[2], yj = j == slot ? yy : dj[3];
+    SY[slot * m + j] = snj;  // s_new . y_j
+    SY[j * m + slot] = sjn;  // s_j . y_new
+    YY[j * m + slot] = yj;
+    YY[slot * m + j] = yj;
+    SYl[slot * m + j] = snj;
+    SYl[j * m + slot] = sjn;
+    YYl[j * m + slot] = yj;
+    YYl[slot * m + j] = yj;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (n_iter == 1 || k == 0) {  // d = -H0 g (first iteration: H0 = I)
+    for (int v = lane; v < 2 * m; v += 64) coef[v] = 0.0;
+    if (L0) coef[2 * m] = -gam;
+    return;
+  }
+  // 4. compact product (lane j = chronological pair j, physical slot ij):
   //    R u = S^T g ; rhs = D u + gam Y^T Y u - gam Y^T g ; R^T p1 = rhs ;
   //    H g = gam g + S p1 - gam Y u   ->   d = -H g
-  //    Both substitutions are k sequential steps on one wave: each step's pivot is broadcast with
-  //    v_readlane (uniform q; a ds_bpermute shuffle costs ~10x its latency) and multiplied by the
-  //    pivot's reciprocal, computed for every lane in parallel up front (no fp64 division on the
-  //    dependent chain): the logic kernel went from ~22 us to a few us per iteration.
-  //    The lane's row (back) / column (forward) of R is read into registers first and the
-  //    substitution loops are unrolled over the 64 possible pairs, so each step's dependent chain
-  //    is readlane -> mul -> fma with no memory access on it.
-  if (tid < 64) {
-    const int j = tid;
-    const double rdj = j < k ? 1.0 / Rc[j * m + j] : 0.0;
-    double row[LB_MAXM];
-#pragma unroll
-    for (int q = 0; q < LB_MAXM; ++q) row[q] = (q < k && j < k) ? Rc[j * m + q] : 0.0;
-    double r = j < k ? aC[j] : 0.0, u = 0.0;
-#pragma unroll
-    for (int q = LB_MAXM - 1; q >= 0; --q) {  // back substitution
-      if (q < k) {
-        const double uq = readlane_d(r, q) * readlane_d(rdj, q);
-        if (j == q) u = uq;
-        if (j < q) r -= row[q] * uq;
-      }
-    }
-    uS[j] = j < k ? u : 0.0;
+  //    R = upper triangle of S^T Y in chronological order.  Each substitution step broadcasts its
+  //    pivot with v_readlane (uniform q) and multiplies by the pivot's reciprocal, computed for
+  //    every lane up front; the LDS operands of a step do not depend on the chain, so the
+  //    8-step unrolled groups keep them ahead of it.
+  const int j = lane;
+  const bool jv = j < k;
+  int ij = head + j;
+  if (ij >= m) ij -= m;
+  ij = jv ? ij : 0;
+  const double rjj = SYl[ij * m + ij];
+  const double rdj = jv ? 1.0 / rjj : 0.0;
+  const bool nwj = pushed && ij == slot;
+  double r = jv ? (nwj ? dots[m * LB_NF + 2] : dots[ij * LB_NF + 0]) : 0.0;  // s_j . g
+  double u = 0.0;
+  // back substitution: q = k-1 .. 0 ; R[j][q] = SYl[ij][iq]
+  int iq = head + k - 1;
+  if (iq >= m) iq -= m;
+#pragma unroll 8
+  for (int q = k - 1; q >= 0; --q) {
+    const double rq = SYl[ij * m + iq];
+    const double uq = readlane_d(r, q) * readlane_d(rdj, q);
+    if (j == q) u = uq;
+    if (j < q) r -= rq * uq;
+    iq = iq == 0 ? m - 1 : iq - 1;
   }
-  __syncthreads();
-  if (tid < 64) {
-    const int j = tid;
-    const double rdj = j < k ? 1.0 / Rc[j * m + j] : 0.0;
-    double rhs = 0.0;
-    if (j < k) {
-      double yu = 0.0;
-      for (int q = 0; q < k; ++q) yu += YYc[j * m + q] * uS[q];
-      rhs = Rc[j * m + j] * uS[j] + gam * yu - gam * bC[j];
-    }
-    double col[LB_MAXM];
-#pragma unroll
-    for (int q = 0; q < LB_MAXM; ++q) col[q] = (q < k && j < k) ? Rc[q * m + j] : 0.0;
-    double rr = rhs, p1 = 0.0;
-#pragma unroll
-    for (int q = 0; q < LB_MAXM; ++q) {  // forward substitution with R^T
-      if (q < k) {
-        const double pq = readlane_d(rr, q) * readlane_d(rdj, q);
-        if (j == q) p1 = pq;
-        if (j > q && j < k) rr -= col[q] * pq;
-      }
-    }
-    pS[j] = j < k ? p1 : 0.0;
+  // rhs = R[j][j] u_j + gam (Y^T Y u)_j - gam y_j.g
+  double yu = 0.0;
+  iq = head;
+#pragma unroll 8
+  for (int q = 0; q < k; ++q) {
+    yu += YYl[iq * m + ij] * readlane_d(u, q);
+    iq = iq + 1 == m ? 0 : iq + 1;
   }
-  __syncthreads();
-  for (int v = tid; v < m; v += 256) {  // per PHYSICAL slot
-    const int cidx = (v - head + m) % m;
-    const bool in = cidx < k;
-    coef[v] = in ? -pS[cidx] : 0.0;
-    coef[m + v] = in ? gam * uS[cidx] : 0.0;
+  const double bj = jv ? (nwj ? dots[m * LB_NF + 3] : dots[ij * LB_NF + 1]) : 0.0;  // y_j . g
+  double rr = jv ? rjj * u + gam * yu - gam * bj : 0.0;
+  // forward substitution with R^T: R[q][j] = SYl[iq][ij]
+  double p1 = 0.0;
+  iq = head;
+#pragma unroll 8
+  for (int q = 0; q < k; ++q) {
+    const double cq = SYl[iq * m + ij];
+    const double pq = readlane_d(rr, q) * readlane_d(rdj, q);
+    if (j == q) p1 = pq;
+    if (j > q && jv) rr -= cq * pq;
+    iq = iq + 1 == m ? 0 : iq + 1;
   }
-  if (tid == 0) coef[2 * m] = -gam;
+  // 5. per PHYSICAL slot
+  if (jv) {
+    coef[ij] = -p1;
+    coef[m + ij] = gam * u;
+  }
+  for (int v = lane; v < m; v += 64)
+    if (((v - head + m) % m) >= k) coef[v] = coef[m + v] = 0.0;
+  if (L0) coef[2 * m] = -gam;
 }
 
 __global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restrict__ fg, const double* __restrict__ part,
@@ -433,46 +488,58 @@ __global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restric
                                                           double* __restrict__ YY, double* __restrict__ coef,
                                                           float* __restrict__ fhist, LbCfg c) {
   extern __shared__ __attribute__((aligned(16))) double lb_lds[];
-  __shared__ int flag[6];  // go, n_iter, pushed, slot, k, head
   if (st[LB_ACTIVE] == 0.0) {
     if (threadIdx.x == 0) st[LB_BEST] = 0.0;
     return;
   }
-  lbfgs_logic_body<false>(fg, part, st, SY, YY, coef, fhist, c, lb_lds, flag);
+  lbfgs_logic_body<false>(fg, part, st, SY, YY, coef, fhist, c, lb_lds);
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) lbfgs_dir_kernel(const float* __restrict__ x, const float* __restrict__ fg,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) lbfgs_dir_kernel(const float* __restrict__ x, const float* __restrict__ fg,
                                                         float* __restrict__ g_old, float* __restrict__ d,
                                                         float* __restrict__ S, float* __restrict__ Y,
                                                         float* __restrict__ best_x, const double* __restrict__ st,
                                                         const double* __restrict__ coef, double* __restrict__ part2,
                                                         LbCfg c) {
   __shared__ double red[8];
+  __shared__ double qs[4][64];
   const bool best = st[LB_BEST] != 0.0, active = st[LB_ACTIVE] != 0.0;
   const int n_iter = (int)st[LB_NITER], pushed = (int)st[LB_PUSHED], slot = (int)st[LB_SLOT];
   const int k = (int)st[LB_K], head = (int)st[LB_HEAD], m = c.m;
   const float tf = (float)st[LB_T];
   const double cG = coef[2 * m];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // w: wave-uniform
   double acc[2] = {0.0, 0.0};
-  for (int j = blockIdx.x * 256 + threadIdx.x; j < c.p; j += gridDim.x * 256) {
-    if (best) best_x[j] = x[j];
-    if (!active) continue;
-    const float g = fg[j];
-    double dn = cG * g;
-    if (n_iter > 1) {
-      const float s = tf * d[j], y = g - g_old[j];
-      if (pushed) {
-        S[(size_t)slot * c.p + j] = s;
-        Y[(size_t)slot * c.p + j] = y;
+  for (int jb = blockIdx.x * 64; jb < c.p; jb += gridDim.x * 64) {
+    const int j = jb + l;
+    const bool in = j < c.p;
+    const int jc = in ? j : c.p - 1;  // unconditional loads: all in flight before the first use
+    const float g = fg[jc], dj = d[jc], oj = g_old[jc], xj = x[jc];
+    // branch-free (k = 0 before the first push: every pair masked; rows stay in range)
+    const double qv = dir_quarter(S, Y, coef, jc, c.p, k, head, m, pushed, slot, tf, g, dj, oj, w);
+    qs[w][l] = (active && n_iter > 1) ? qv : 0.0;
+    const float s = tf * dj, y = g - oj;
+    __syncthreads();
+    if (w == 0 && in) {
+      if (best) best_x[j] = xj;
+      if (active) {
+        double dn = cG * g;
+        if (n_iter > 1) {
+          if (pushed) {
+            S[(size_t)slot * c.p + j] = s;
+            Y[(size_t)slot * c.p + j] = y;
+          }
+          dn += (qs[0][l] + qs[1][l]) + (qs[2][l] + qs[3][l]);
+        }
+        const float df = (float)dn;
+        g_old[j] = g;
+        d[j] = df;
+        acc[0] += (double)g * df;
+        acc[1] += fabs((double)df);
       }
-      dn = dir_elem(S, Y, coef, j, c.p, k, head, m, pushed, slot, s, y, dn);
     }
-    const float df = (float)dn;
-    g_old[j] = g;
-    d[j] = df;
-    acc[0] += (double)g * df;
-    acc[1] += fabs((double)df);
+    __syncthreads();  // qs is rewritten by the next tile
   }
   block_sum<2>(acc, red);
   if (threadIdx.x == 0) {
@@ -536,8 +603,7 @@ __global__ void __launch_bounds__(256) lbfgs_dots_logic_kernel(const float* __re
                                                                float* __restrict__ fhist, int* __restrict__ ticket,
                                                                LbCfg c) {
   extern __shared__ __attribute__((aligned(16))) double lb_lds[];
-  __shared__ double red[4 * LB_NF];
-  __shared__ int flag[6];
+  __shared__ double red[4 * LB_G * LB_NF];
   __shared__ int last;
   if (st[LB_ACTIVE] == 0.0) {  // every block sees the same value: only the last block changes it
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st[LB_BEST] = 0.0;
@@ -553,10 +619,10 @@ __global__ void __launch_bounds__(256) lbfgs_dots_logic_kernel(const float* __re
   __syncthreads();
   if (!last) return;
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  lbfgs_logic_body<true>(fg, part, st, SY, YY, coef, fhist, c, lb_lds, flag);
+  lbfgs_logic_body<true>(fg, part, st, SY, YY, coef, fhist, c, lb_lds);
 }
 
-__global__ void __launch_bounds__(256) lbfgs_dir_step_kernel(float* __restrict__ x, const float* __restrict__ fg,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) lbfgs_dir_step_kernel(float* __restrict__ x, const float* __restrict__ fg,
                                                              float* __restrict__ g_old, float* __restrict__ d,
                                                              float* __restrict__ S, float* __restrict__ Y,
                                                              float* __restrict__ best_x, float* __restrict__ x_prev,
@@ -564,6 +630,7 @@ __global__ void __launch_bounds__(256) lbfgs_dir_step_kernel(float* __restrict__
                                                              double* __restrict__ part2, int* __restrict__ ticket,
                                                              LbCfg c) {
   __shared__ double red[8];
+  __shared__ double qs[4][64];
   __shared__ int last, stop;
   const bool best = st[LB_BEST] != 0.0, active = st[LB_ACTIVE] != 0.0;
   const int n_iter = (int)st[LB_NITER], pushed = (int)st[LB_PUSHED], slot = (int)st[LB_SLOT];
@@ -573,31 +640,42 @@ __global__ void __launch_bounds__(256) lbfgs_dir_step_kernel(float* __restrict__
   const double tnext = (n_iter == 1) ? fmin(1.0, 1.0 / st[LB_G1]) : c.lr;
   const float tn = (float)tnext;
   const double cG = coef[2 * m];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // w: wave-uniform
   double acc[2] = {0.0, 0.0};
-  for (int j = blockIdx.x * 256 + threadIdx.x; j < c.p; j += gridDim.x * 256) {
-    const float xj = x[j];
-    if (best) best_x[j] = xj;
-    if (!active) continue;
-    const float g = fg[j];
-    double dn = cG * g;
-    if (n_iter > 1) {
-      const float s = tf * d[j], y = g - g_old[j];
-      if (pushed) {
-        S[(size_t)slot * c.p + j] = s;
-        Y[(size_t)slot * c.p + j] = y;
+  for (int jb = blockIdx.x * 64; jb < c.p; jb += gridDim.x * 64) {
+    const int j = jb + l;
+    const bool in = j < c.p;
+    const int jc = in ? j : c.p - 1;  // unconditional loads: all in flight before the first use
+    const float g = fg[jc], dj = d[jc], oj = g_old[jc], xj = x[jc];
+    // branch-free (k = 0 before the first push: every pair masked; rows stay in range)
+    const double qv = dir_quarter(S, Y, coef, jc, c.p, k, head, m, pushed, slot, tf, g, dj, oj, w);
+    qs[w][l] = (active && n_iter > 1) ? qv : 0.0;
+    const float s = tf * dj, y = g - oj;
+    __syncthreads();
+    if (w == 0 && in) {
+      if (best) best_x[j] = xj;
+      if (active) {
+        double dn = cG * g;
+        if (n_iter > 1) {
+          if (pushed) {
+            S[(size_t)slot * c.p + j] = s;
+            Y[(size_t)slot * c.p + j] = y;
+          }
+          dn += (qs[0][l] + qs[1][l]) + (qs[2][l] + qs[3][l]);
+        }
+        const float df = (float)dn;
+        g_old[j] = g;
+        d[j] = df;
+        // speculative step, undone below if the descent test fails.  Both x stores are
+        // write-through (sc1): a plain store would leave a dirty line in this XCD's L2 whose
+        // write-back at kernel end could land after the last block's restore of the same element.
+        __hip_atomic_store(&x_prev[j], xj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&x[j], fmaf(tn, df, xj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[0] += (double)g * df;
+        acc[1] += fabs((double)df);
       }
-      dn = dir_elem(S, Y, coef, j, c.p, k, head, m, pushed, slot, s, y, dn);
     }
-    const float df = (float)dn;
-    g_old[j] = g;
-    d[j] = df;
-    // speculative step, undone below if the descent test fails.  Both x stores are write-through
-    // (sc1): a plain store would leave a dirty line in this XCD's L2 whose write-back at kernel
-    // end could land after the last block's restore of the same element.
-    __hip_atomic_store(&x_prev[j], xj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&x[j], fmaf(tn, df, xj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    acc[0] += (double)g * df;
-    acc[1] += fabs((double)df);
+    __syncthreads();  // qs is rewritten by the next tile
   }
   if (!active) return;  // uniform: no ticket, nothing to reduce
   block_sum<2>(acc, red);
@@ -656,16 +734,15 @@ int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, fl
   if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
   LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const size_t lds = ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m + 4 * 64) * sizeof(double);
+  const size_t lds = lbfgs_logic_lds(m);
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgs_logic_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)(((LB_MAXM + 1) * LB_NF + 2 * LB_MAXM * LB_MAXM + 4 * 64) * sizeof(double)));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbfgs_logic_lds(LB_MAXM));
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL(lbfgs_dots_kernel, dim3(nchunks, m + 1), dim3(256), 0, s, fg, g_old, d, S, Y, st, part, c);
+  hipLaunchKernelGGL(lbfgs_dots_kernel, dim3(nchunks, (m + LB_G) / LB_G), dim3(256), 0, s, fg, g_old, d, S, Y, st, part, c);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(lbfgs_logic_kernel, dim3(1), dim3(256), lds, s, fg, part, st, SY, YY, coef, fhist, c);
   TDQ_CHECK_LAUNCH();
@@ -687,16 +764,15 @@ int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, fl
   if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
   LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const size_t lds = ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m + 4 * 64) * sizeof(double);
+  const size_t lds = lbfgs_logic_lds(m);
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgs_dots_logic_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)(((LB_MAXM + 1) * LB_NF + 2 * LB_MAXM * LB_MAXM + 4 * 64) * sizeof(double)));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbfgs_logic_lds(LB_MAXM));
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL(lbfgs_dots_logic_kernel, dim3(nchunks, m + 1), dim3(256), lds, s, fg, g_old, d, S, Y, st, part, SY,
+  hipLaunchKernelGGL(lbfgs_dots_logic_kernel, dim3(nchunks, (m + LB_G) / LB_G), dim3(256), lds, s, fg, g_old, d, S, Y, st, part, SY,
                      YY, coef, fhist, ticket, c);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(lbfgs_dir_step_kernel, dim3(nblk), dim3(256), 0, s, x, fg, g_old, d, S, Y, best_x, x_prev, st,

@@ -90,7 +90,7 @@ class DeviceLBFGS:
         self.YY = torch.zeros(self.m, self.m, **f64)
         self.coef = torch.zeros(2 * self.m + 1, **f64)
         self.nchunks = max(1, min(64, _ceil(p, 4096)))
-        self.nblk = max(1, min(1024, _ceil(p, 256)))
+        self.nblk = max(1, min(2048, _ceil(p, 64)))  # direction blocks: 64 elements x 4 history quarters
         self.part = torch.zeros(self.nchunks * (self.m + 1) * 5, **f64)
         self.part2 = torch.zeros(2 * self.nblk, **f64)
         self.fhist = torch.full((self.max_iter + 1,), float("nan"), **f32) if record_history else None
