@@ -24,6 +24,10 @@ force_dp               TDQ_FORCE_DP=1              DP machinery (process group, 
                                                    even at world 1 (parallel/dist.py)
 dp_graph               TDQ_DP_GRAPH=0 disables     RCCL all-reduce captured inside the step graph
 nan_check              TDQ_NAN_CHECK=0 disables    device loss-history NaN/Inf scan (fit.py)
+(split)                TDQ_SPLIT                   auto (cut at 0.45 for bf16, 0.35 for bf16x3) | off | cut
+                                                   fraction: two point ranges on concurrent graph
+                                                   branches (fit.point_ranges)
+(lbfgs_fused)          TDQ_LBFGS_FUSED=0           five-launch L-BFGS update instead of two
 (profiling)            TDQ_PROFILE                 directory: every fit() runs under torch.profiler
                                                    -> trace.json + kernels.txt (profiling.py)
 =====================  ==========================  =========================================

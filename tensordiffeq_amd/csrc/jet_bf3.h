@@ -649,13 +649,15 @@ template <int WT, int S, int NSO, bool LO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(bf3_wpe(WT, S, LO), bf3_wpe(WT, S, LO))))
 jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
                    float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r,
-                   bf16x4* __restrict__ gstage) {
+                   bf16x4* __restrict__ gstage, int wg0) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wg = blockIdx.x, nwg = gridDim.x;
+  // wg0: first workgroup of this launch (a point range of the whole set, see Bf3Args::p_lo); the
+  // saved-activation layout and J always index the whole set
+  const int wg = wg0 + (int)blockIdx.x, nwg = (N + 63) / 64;
   const int n = wg * 64 + w * 16 + p;
   const bool valid = n < N;
   const int nc = valid ? n : N - 1;  // clamped: every load is in bounds, no exec branches
@@ -885,7 +887,7 @@ __attribute__((amdgpu_waves_per_eu(bf3_wpe(WT, S, LO), bf3_wpe(WT, S, LO))))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
                    int Ptot, NetDims d, JetSpec sp, int rev, int h0r, bf16x4* __restrict__ gstage,
-                   const bf16x8* __restrict__ Fimg) {
+                   const bf16x8* __restrict__ Fimg, int wg0) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int W = 16 * WT;
   constexpr int KB = WT / 2;
@@ -944,7 +946,8 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // rev: tiles in reverse dispatch order - the forward wrote the highest tiles last, so theirs are
   // the saved activations still resident in the 256 MiB Infinity Cache when the backward starts
-  const int nwg = gridDim.x, wg = rev ? nwg - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  // (wg0: first workgroup of a point-range launch; slabs and saved activations index the whole set)
+  const int nwl = gridDim.x, wg = wg0 + (rev ? nwl - 1 - (int)blockIdx.x : (int)blockIdx.x);
   const int n = wg * PTS + w * 16 + p;
   // saved activations are laid out by the forward's 64-point workgroups: this wave's region is
   // forward workgroup wg_f, wave w_f (clamped: the padding half of a last 128-point workgroup
@@ -1372,11 +1375,16 @@ struct Bf3Args {
   int lo;            // 1: bf16x3 (operands hi + lo), 0: bf16 (operands rounded to bf16)
   bf16x4* gstage;    // wide bf16x3 plans: global fragment stage (bf3_gstage), else unused
   const bf16x8* fimg;  // bwd: the forward's weight images (TDQ_RECOMPUTE_TOP)
+  // point range [p_lo, p_hi) of this launch (p_lo a multiple of 128, p_hi one too or = N): the
+  // kernels index J / dJ, the saved activations and the slabs of the whole set N, so launches
+  // over disjoint ranges may run concurrently (separate streams) into the same buffers
+  int p_lo = 0, p_hi = -1;
 };
 
 template <int WT, int S, int NSO, bool LO>
 int launch_fwd_bf3_lo(const Bf3Args& a) {
-  const int nwg = (a.N + 63) / 64;
+  const int hi = a.p_hi < 0 ? a.N : a.p_hi, wg0 = a.p_lo / 64;
+  const int nwg = (hi + 63) / 64 - wg0;
   const size_t lds = fwd_bf3_lds(WT, S, LO);
   static bool attr = false;
   if (!attr) {
@@ -1385,7 +1393,7 @@ int launch_fwd_bf3_lo(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
-                     a.Hs, a.N, a.d, a.sp, h0_recompute(), a.gstage);
+                     a.Hs, a.N, a.d, a.sp, h0_recompute(), a.gstage, wg0);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -1398,7 +1406,8 @@ int launch_fwd_bf3(const Bf3Args& a) {
 template <int WT, int S, int NSO, bool LO>
 int launch_bwd_bf3_lo(const Bf3Args& a) {
   constexpr int NWV = bwd_waves(WT, LO, S);
-  const int nwg = (a.N + 16 * NWV - 1) / (16 * NWV);
+  const int hi = a.p_hi < 0 ? a.N : a.p_hi, wg0 = a.p_lo / (16 * NWV);
+  const int nwg = (hi + 16 * NWV - 1) / (16 * NWV) - wg0;
   const size_t lds = bwd_bf3_lds(WT, S, LO);
   static bool attr = false;
   if (!attr) {
@@ -1407,7 +1416,8 @@ int launch_bwd_bf3_lo(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(64 * NWV), lds, a.st, a.X, a.aux, a.img, a.dJ,
-                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute(), a.gstage, a.fimg);
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute(), a.gstage, a.fimg,
+                     wg0);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -393,9 +393,14 @@ static inline bf16x4* scratch_stage(float* scratch, int N, int d_in, int n_hidde
 // lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16).
 // pack = 0: the weight images in scratch are already current (written by the previous step's
 // tail_adam), so the forward skips its pack launch.
-int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch, int N, int d_in, const int* widths,
-                       int d_out, int n_hidden, int S, const int* spec, int lo, int pack, void* stream) {
+// forward over the point range [p_lo, p_hi) of the N-point set (p_lo a multiple of 128, p_hi one
+// too or = N); pack = 1 packs the weight images first
+int tdq_jet_fwd_bf3_range(const float* X, const float* P, float* J, float* scratch, int N, int p_lo, int p_hi,
+                          int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo, int pack,
+                          void* stream) {
   if (N <= 0) return 0;
+  if (p_lo < 0 || p_lo % 128 != 0 || p_hi > N || p_hi <= p_lo || (p_hi != N && p_hi % 128 != 0))
+    return (int)hipErrorInvalidValue;
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -413,8 +418,13 @@ int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch,
     if (rc) return rc;
   }
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
-            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), nullptr};
+            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), nullptr, p_lo, p_hi};
   return dispatch(true, WT, S, nso, a);
+}
+
+int tdq_jet_fwd_bf3_ex(const float* X, const float* P, float* J, float* scratch, int N, int d_in, const int* widths,
+                       int d_out, int n_hidden, int S, const int* spec, int lo, int pack, void* stream) {
+  return tdq_jet_fwd_bf3_range(X, P, J, scratch, N, 0, N, d_in, widths, d_out, n_hidden, S, spec, lo, pack, stream);
 }
 
 int tdq_jet_fwd_bf3(const float* X, const float* P, float* J, float* scratch, int N, int d_in, const int* widths,
@@ -435,11 +445,14 @@ int tdq_jet_bf3_pack(const float* P, float* scratch, int N, int d_in, const int*
                      reinterpret_cast<hipStream_t>(stream));
 }
 
-// reduce = 0: only the backward kernel (gradient slabs in work); tdq_step_tail_bf3 reduces them
-int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
-                       int N, int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo, int reduce,
-                       void* stream) {
+// backward over the point range [p_lo, p_hi) (see tdq_jet_fwd_bf3_range): the slabs of the
+// range's workgroups only; tdq_step_tail_bf3 / tdq_dp_tail_a_bf3 reduce all of them
+int tdq_jet_bwd_bf3_range(const float* X, const float* dJ, const float* Hs, float* work, int N, int p_lo, int p_hi,
+                          int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo,
+                          void* stream) {
   if (N <= 0) return 0;
+  if (p_lo < 0 || p_lo % 128 != 0 || p_hi > N || p_hi <= p_lo || (p_hi != N && p_hi % 128 != 0))
+    return (int)hipErrorInvalidValue;
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -449,21 +462,31 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   const int nso = spec_nso(S, spec);
   if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
   const int Ptot = param_count(d);
-  const int chunks = slab_chunks(nwg_b);
-  float* slab = work;
   // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
   float *img, *bimg, *aux;
   scratch_images(const_cast<float*>(Hs), N, n_hidden, S, WT, &img, &bimg, &aux);
-  (void)P;
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
-  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), slab, N,
+  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), work, N,
             slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo),
-            reinterpret_cast<const bf16x8*>(img)};
-  int rc = dispatch(false, WT, S, nso, a);
+            reinterpret_cast<const bf16x8*>(img), p_lo, p_hi};
+  return dispatch(false, WT, S, nso, a);
+}
+
+// reduce = 0: only the backward kernel (gradient slabs in work); tdq_step_tail_bf3 reduces them
+int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,
+                       int N, int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo, int reduce,
+                       void* stream) {
+  if (N <= 0) return 0;
+  (void)P;
+  int rc = tdq_jet_bwd_bf3_range(X, dJ, Hs, work, N, 0, N, d_in, widths, d_out, n_hidden, S, spec, lo, stream);
   if (rc || !reduce) return rc;
-  return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, chunks, (int)slab_half(lo != 0), stream);
+  NetDims d;
+  make_dims(d, d_in, widths, 0, d_out, n_hidden);
+  const int WT = width_tiles(d.width);
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
+  const int Ptot = param_count(d);
+  return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, slab_chunks(nwg_b), (int)slab_half(lo != 0), stream);
 }
 
 int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float* Hs, float* work, float* grad,

@@ -35,6 +35,10 @@ struct LFGroup {
   int n, block_off, out_off, n_out;
   int n_slots, seg_off[LF_MAX_SLOTS];
   unsigned loaded[LF_MAX_SLOTS];  // bit s set: stream s of that slot is read by the program
+  // instances start `phase` threads into the group's first block: single-segment groups put their
+  // block boundaries on absolute point indices that are multiples of LF_BLOCK, so point-range
+  // launches of the jet kernels (multiples of 128) cut the loss blocks cleanly
+  int phase;
 };
 
 struct LFOut {
@@ -76,12 +80,12 @@ __global__ void __launch_bounds__(LF_BLOCK) loss_fused_kernel(const int4* __rest
                                                               const LFGroup* __restrict__ groups, LFMeta meta,
                                                               const LFPtrs* __restrict__ ptrp, const float* __restrict__ J,
                                                               const float* __restrict__ X, float* __restrict__ dJ,
-                                                              float* __restrict__ partials) {
+                                                              float* __restrict__ partials, int blk0) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ float red[LF_BLOCK / 16];
   __shared__ float acc[LF_MAX_TERMS + LF_MAX_SCAL];
   const int tid = threadIdx.x;
-  const int blk = blockIdx.x;
+  const int blk = blk0 + (int)blockIdx.x;  // blk0: first block of a range launch
   int gi = 0;
   for (int q = 1; q < meta.n_groups; ++q)
     if (blk >= groups[q].block_off) gi = q;
@@ -90,8 +94,8 @@ __global__ void __launch_bounds__(LF_BLOCK) loss_fused_kernel(const int4* __rest
   // slot lookups by select (a runtime-indexed member array would be placed in scratch)
   const int so0 = G.seg_off[0], so1 = G.seg_off[1];
   auto seg_off = [&](int slot) { return slot == 0 ? so0 : so1; };
-  const int i = (blk - G.block_off) * LF_BLOCK + tid;
-  const bool active = i < G.n;
+  const int i = (blk - G.block_off) * LF_BLOCK + tid - G.phase;
+  const bool active = i >= 0 && i < G.n;
   const int ii = active ? i : 0;
   float* V = lds;                               // [n_regs][LF_BLOCK]
   float* A = lds + G.n_regs * LF_BLOCK;         // [n_regs][LF_BLOCK]
@@ -274,13 +278,15 @@ extern "C" {
 // code: int4 per instruction; outs / groups / ptrs: device buffers of LFOut / LFGroup / LFPtrs
 // do_reduce = 0: only the loss kernel (dJ, dlam, block partials); the fused step tail
 // (tdq_step_tail_bf3 / tdq_dp_tail_a_bf3) reduces the partials itself
-int tdq_loss_fused(const int* code, const float* consts, const void* outs, const void* groups,
-                   const void* ptrs, int n_groups, int n_terms, int n_scal, int S, int d_in, int N,
-                   const float* J, const float* X, float* dJ, float* partials, int n_blocks, int max_regs,
-                   float* losses, float* total, float* dscal, int with_total, int do_reduce, void* stream) {
+// blocks [blk0, blk0 + nblk) only (a range launch: dJ / dlam / partials of those blocks); the
+// reduction is left to the fused step tail
+int tdq_loss_fused_range(const int* code, const float* consts, const void* outs, const void* groups,
+                         const void* ptrs, int n_groups, int n_terms, int n_scal, int S, int d_in, int N,
+                         const float* J, const float* X, float* dJ, float* partials, int n_blocks, int blk0, int nblk,
+                         int max_regs, void* stream) {
   LFMeta meta{n_groups, n_terms, n_scal, S, d_in, N};
   if (meta.n_groups < 1 || meta.n_groups > LF_MAX_GROUPS || meta.n_terms > LF_MAX_TERMS ||
-      meta.n_scal > LF_MAX_SCAL)
+      meta.n_scal > LF_MAX_SCAL || blk0 < 0 || nblk < 1 || blk0 + nblk > n_blocks)
     return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const size_t lds = (size_t)2 * max_regs * LF_BLOCK * sizeof(float);
@@ -290,13 +296,25 @@ int tdq_loss_fused(const int* code, const float* consts, const void* outs, const
                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 120 * LF_BLOCK * (int)sizeof(float));
     attr = true;
   }
-  hipLaunchKernelGGL(loss_fused_kernel, dim3(n_blocks), dim3(LF_BLOCK), lds, st,
+  hipLaunchKernelGGL(loss_fused_kernel, dim3(nblk), dim3(LF_BLOCK), lds, st,
                      reinterpret_cast<const int4*>(code), consts, reinterpret_cast<const LFOut*>(outs),
                      reinterpret_cast<const LFGroup*>(groups), meta, reinterpret_cast<const LFPtrs*>(ptrs), J, X,
-                     dJ, partials);
+                     dJ, partials, blk0);
   TDQ_CHECK_LAUNCH();
-  if (!do_reduce) return 0;
-  return loss_reduce(partials, n_blocks, meta.n_terms, meta.n_scal, losses, total, dscal, with_total, stream);
+  return 0;
+}
+
+// code: int4 per instruction; outs / groups / ptrs: device buffers of LFOut / LFGroup / LFPtrs
+// do_reduce = 0: only the loss kernel (dJ, dlam, block partials); the fused step tail
+// (tdq_step_tail_bf3 / tdq_dp_tail_a_bf3) reduces the partials itself
+int tdq_loss_fused(const int* code, const float* consts, const void* outs, const void* groups,
+                   const void* ptrs, int n_groups, int n_terms, int n_scal, int S, int d_in, int N,
+                   const float* J, const float* X, float* dJ, float* partials, int n_blocks, int max_regs,
+                   float* losses, float* total, float* dscal, int with_total, int do_reduce, void* stream) {
+  int rc = tdq_loss_fused_range(code, consts, outs, groups, ptrs, n_groups, n_terms, n_scal, S, d_in, N, J, X, dJ,
+                                partials, n_blocks, 0, n_blocks, max_regs, stream);
+  if (rc || !do_reduce) return rc;
+  return loss_reduce(partials, n_blocks, n_terms, n_scal, losses, total, dscal, with_total, stream);
 }
 
 int tdq_loss_meta_sizes(int* out) {

@@ -263,6 +263,12 @@ class AdamEngine:
         self._tail_ok = ok
         return ok
 
+    def _point_ranges(self, fop):
+        if getattr(self, "_ranges", 0) == 0:
+            self._ranges = point_ranges(self.program, fop)
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in (self._ranges or ())]
+        return self._ranges
+
     def _tail_step(self, in_graph):
         """One Adam step ending in the fused tail.  ``in_graph``: the step is being captured, so
         the forward reuses the weight images that the previous replay's tail wrote (the engine
@@ -276,10 +282,14 @@ class AdamEngine:
         if st["best_flat"].numel() != self.flat.numel():
             raise ValueError(f"best-weights snapshot has {st['best_flat'].numel()} elements, parameters "
                              f"{self.flat.numel()}")
-        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
-                                       pack=not in_graph)
-        fop(J, with_total=False, reduce=False)
-        grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
+        if self._point_ranges(fop):  # point ranges on concurrent graph branches (see point_ranges)
+            saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams, pack=not in_graph)
+            grad = torch.empty_like(self.flat)
+        else:
+            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                           pack=not in_graph)
+            fop(J, with_total=False, reduce=False)
+            grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
         grads = self._fused_grads(fop, grad, fop.dlam, fop.dscal)
         packed = fused.group_array(self._opt_groups(grads))
         if packed is None:  # gradient tensors the single launch cannot take: reduce, then Adam
@@ -376,8 +386,12 @@ class AdamEngine:
         from .ops import jet_hip
         prog = self.program
         fop = prog.fused_op
-        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision, pack=False)
-        fop(J, with_total=False, reduce=False)
+        rng = self._point_ranges(fop)
+        if rng:
+            saved, work = run_ranges(prog, fop, self.flat, rng, self._streams, pack=False)
+        else:
+            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision, pack=False)
+            fop(J, with_total=False, reduce=False)
         n_p = self.flat.numel()
         red_idx = self.red_idx
         if not red_idx or red_idx[0] != 0:
@@ -387,7 +401,8 @@ class AdamEngine:
         n_e, n_t = sum(sizes), fop.n_terms
         buf = torch.empty(n_p + n_e + 1 + n_t, dtype=torch.float32, device=self.device)
         grad_view = buf[:n_p]
-        grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=grad_view)
+        if not rng:
+            grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=grad_view)
         jet_hip.dp_tail_a(saved, work, grad_view, fop, total=buf[n_p + n_e:n_p + n_e + 1],
                           losses=buf[n_p + n_e + 1:])
         grads = self._fused_grads(fop, grad_view, fop.dlam, fop.dscal)
@@ -474,6 +489,76 @@ class AdamEngine:
         return hi
 
 
+def point_ranges(program, fop):
+    """Point ranges whose forward -> loss -> backward chains run on separate streams (graph
+    branches), or ``None``.
+
+    One jet launch over N points is a whole number of wave rounds (bf16 at 50k points: 3184 waves
+    of 16 points over 2048 wave slots = 1.55 rounds, run as 2; bf16x3: 3.1 rounds over 1024 slots,
+    run as 4), and the loss launch between them idles the GPU.  With the points in two ranges on
+    two streams, the loss and backward of one range fill the slots the forward of the other
+    leaves idle (MI355X, AC-SA 50k: bf16 Adam step 0.211 -> 0.200 ms, bf16x3 0.446 -> 0.411 ms,
+    bf16x3 L-BFGS iteration 0.51 -> 0.48 ms; profiles/r3_l_split_sweep.jsonl).  ``TDQ_SPLIT``:
+    ``auto`` (default: cut at 0.45 for bf16, 0.35 for bf16x3, the sweep's best), ``0`` / ``off``,
+    or the cut fraction.  Cuts land on multiples of 128 points that also cut the fused loss's blocks
+    cleanly (:meth:`FusedLossOp.split_block`); results are bitwise those of single launches (every
+    workgroup / block keeps its index and buffers)."""
+    from .ops.jet_mlp import hip_config
+    spec = os.environ.get("TDQ_SPLIT", "auto").strip().lower()
+    if spec in ("0", "off", "none", "", "0.0"):
+        return None
+    try:
+        cfg = hip_config(program.net, program.plan, program.precision)
+    except ValueError:
+        return None
+    if cfg["precision"] not in ("bf16x3", "bf16"):
+        return None
+    if spec == "auto":
+        fracs = [0.35] if cfg["precision"] == "bf16x3" else [0.45]
+    else:
+        fracs = sorted(float(v) for v in spec.split(","))
+    if len(fracs) > 1:
+        # three graph branches made hipGraphLaunch segfault on the host (ROCm 7.2, MI355X,
+        # gpurun_out r3l); two are tested (tests/test_hip_kernels.py, tests/test_dist_gpu.py)
+        raise ValueError("TDQ_SPLIT: one cut (two point ranges) at most")
+    N = program.X_all.shape[0]
+    if N < 8192:
+        return None
+    cuts, blks = [0], [0]
+    for f in fracs:
+        a = int(round(f * N / 128)) * 128
+        if a <= cuts[-1] or a >= N:
+            return None
+        b = fop.split_block(a)
+        if b is None or b <= blks[-1]:
+            return None
+        cuts.append(a)
+        blks.append(b)
+    cuts.append(N)
+    blks.append(fop.n_blocks)
+    return [(cuts[i], cuts[i + 1], blks[i], blks[i + 1] - blks[i]) for i in range(len(cuts) - 1)]
+
+
+def run_ranges(program, fop, flat, ranges, streams, pack=True):
+    """Forward -> fused loss -> backward of every point range on its own stream (forked from and
+    joined back into the current one).  Returns ``(saved, work)`` for the fused step tail."""
+    from .ops import jet_hip
+    J, saved = jet_hip.alloc_forward(program.X_all, flat, program.net, program.plan, program.precision)
+    work = jet_hip.alloc_backward(saved)
+    if pack:
+        jet_hip.pack_images(saved)
+    cur = torch.cuda.current_stream(flat.device)
+    for (lo, hi, b0, nb), st in zip(ranges, streams):
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            jet_hip.forward_range(saved, J, lo, hi)
+            fop.run_range(J, b0, nb)
+            jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
+    for st in streams:
+        cur.wait_stream(st)
+    return saved, work
+
+
 class LossGradEngine:
     """``(f, g_theta)`` at a flat parameter vector (lambdas frozen, B15); DP all-reduced."""
 
@@ -509,13 +594,21 @@ class LossGradEngine:
         if fop is not None:
             from .ops import jet_hip
             prog = self.program
-            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
             if self._fused_tail():
-                fop(J, with_total=False, reduce=False)
                 fg = torch.empty(self.flat.numel() + 1, dtype=torch.float32, device=self.flat.device)
+                if getattr(self, "_ranges", 0) == 0:
+                    self._ranges = point_ranges(prog, fop)
+                    self._streams = [torch.cuda.Stream(device=self.flat.device) for _ in (self._ranges or ())]
+                if self._ranges:
+                    saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams)
+                    jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:])
+                    return fg
+                J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+                fop(J, with_total=False, reduce=False)
                 grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=fg[:-1])
                 jet_hip.dp_tail_a(saved, work, grad, fop, total=fg[-1:])
                 return fg
+            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
             total, _, dJ, _, _ = fop(J)
             g = jet_hip.backward_raw(saved, dJ)
             return torch.cat([g.reshape(-1), total.reshape(1)])

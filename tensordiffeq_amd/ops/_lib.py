@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _lock = threading.Lock()
 _lib = None
@@ -44,6 +44,8 @@ def _declare(lib):
         "tdq_jet_bwd_bf3": (I, [P, P, P, P, P, P, I, I, P, I, I, I, P, I, P]),
         "tdq_jet_fwd_bf3_ex": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, P]),
         "tdq_jet_bwd_bf3_ex": (I, [P, P, P, P, P, P, I, I, P, I, I, I, P, I, I, P]),
+        "tdq_jet_fwd_bf3_range": (I, [P, P, P, P, I, I, I, I, P, I, I, I, P, I, I, P]),
+        "tdq_jet_bwd_bf3_range": (I, [P, P, P, P, I, I, I, I, P, I, I, I, P, I, P]),
         "tdq_jet_bf3_pack": (I, [P, P, I, I, P, I, I, I, P]),
         "tdq_step_tail_bf3": (I, [P, P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P] + [P, L, P, P, P, P]
                               + [P, I, P, I, P, P]),
@@ -55,6 +57,7 @@ def _declare(lib):
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
         "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, I, I, P]),
+        "tdq_loss_fused_range": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, I, I, P]),
         "tdq_loss_meta_sizes": (I, [P]),
         "tdq_lbfgs_nst": (I, []),
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),

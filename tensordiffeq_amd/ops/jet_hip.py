@@ -118,6 +118,57 @@ def backward_raw(saved, dJ, reduce=True, grad=None):
     return grad
 
 
+def alloc_forward(X, P, net, plan, precision=None):
+    """Buffers of a split-bf16 forward over the whole point set, nothing launched: ``(J, saved)``
+    for :func:`pack_images`, :func:`forward_range` and :func:`backward_range`."""
+    cfg = hip_config(net, plan, precision)
+    if not is_split_bf16(cfg):
+        raise ValueError("point-range launches need a split-bf16 precision")
+    lib = _lib.load()
+    _, _, scratch_floats, _ = _fns(lib, cfg)
+    X = X.contiguous()
+    N = X.shape[0]
+    nscr = scratch_floats(N)
+    if nscr < 0:
+        raise ValueError(f"jet kernels cannot serve {cfg}")
+    J = torch.empty((plan.S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
+    scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
+    return J, (X, P, scratch, cfg, stream_spec(plan), plan.S)
+
+
+def forward_range(saved, J, lo, hi):
+    """Forward of the points ``[lo, hi)`` (``lo`` a multiple of 128, ``hi`` too or ``N``) into
+    the whole-set ``J`` / saved activations, on the current stream; the weight images must be
+    packed (:func:`pack_images`)."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    spec_c = (ctypes.c_int * len(spec))(*spec)
+    rc = lib.tdq_jet_fwd_bf3_range(_lib.ptr(X), _lib.ptr(P), _lib.ptr(J), _lib.ptr(scratch), X.shape[0], int(lo),
+                                   int(hi), cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], S, spec_c,
+                                   *_lo_args(cfg), 0, _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_jet_fwd_bf3_range")
+
+
+def alloc_backward(saved):
+    """Gradient-slab buffer of the whole point set (see :func:`backward_range`)."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    _, _, _, slab_floats = _fns(lib, cfg)
+    return torch.empty(max(int(slab_floats(X.shape[0])), 1), dtype=torch.float32, device=X.device)
+
+
+def backward_range(saved, dJ, work, lo, hi):
+    """Backward of the points ``[lo, hi)``: the gradient slabs of their workgroups in ``work``
+    (reduced with the others by :func:`step_tail` / :func:`dp_tail_a`), on the current stream."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    spec_c = (ctypes.c_int * len(spec))(*spec)
+    rc = lib.tdq_jet_bwd_bf3_range(_lib.ptr(X), _lib.ptr(dJ), _lib.ptr(scratch), _lib.ptr(work), X.shape[0],
+                                   int(lo), int(hi), cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], S,
+                                   spec_c, *_lo_args(cfg), _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_jet_bwd_bf3_range")
+
+
 def is_split_bf16(cfg):
     return cfg["precision"] in ("bf16x3", "bf16")
 

@@ -28,6 +28,7 @@ class FusedLossOp:
             raise ValueError("fused loss program exceeds kernel table limits")
         self.fl, self.prog = fl, prog
         code, consts, outs, groups = [], [], [], []
+        spans = []
         block_off = 0
         self.max_regs = 1
         for gr in fl.groups:
@@ -37,15 +38,26 @@ class FusedLossOp:
             loaded = [0] * MAX_SLOTS
             for (slot, s) in P.stream_regs:
                 loaded[slot] |= 1 << s
-            seg_off = [prog.segments[s].offset for s in gr.segs] + [0] * (MAX_SLOTS - len(gr.segs))
+            offs = [prog.segments[s].offset for s in gr.segs]
+            seg_off = offs + [0] * (MAX_SLOTS - len(gr.segs))
+            # single-segment groups: block boundaries on absolute multiples of LF_BLOCK (LFGroup.phase)
+            phase = offs[0] % LF_BLOCK if len(offs) == 1 else 0
             groups.append([len(code), len(P.code), len(consts), P.n_regs, gr.n, block_off, len(outs),
-                           len(P.outputs), len(gr.segs)] + seg_off + loaded)
+                           len(P.outputs), len(gr.segs)] + seg_off + loaded + [phase])
             code += P.code
             consts += P.consts
             outs += P.outputs
-            block_off += max(1, math.ceil(gr.n / LF_BLOCK))
+            nb = max(1, math.ceil((gr.n + phase) / LF_BLOCK))
+            for k in range(nb):  # the point span every block reads / writes (range launches)
+                a, b = max(0, k * LF_BLOCK - phase), min(gr.n, (k + 1) * LF_BLOCK - phase) - 1
+                if b < a:
+                    spans.append((math.inf, -math.inf))
+                else:
+                    spans.append((min(o + a for o in offs), max(o + b for o in offs)))
+            block_off += nb
             self.max_regs = max(self.max_regs, P.n_regs)
         self.n_blocks = block_off
+        self.block_spans = spans
         self.n_groups = len(groups)
         self.n_terms = len(fl.term_names)
         self.n_scal = len(fl.scal_slots)
@@ -55,7 +67,13 @@ class FusedLossOp:
         for k, (f, w, t, c) in enumerate(outs):
             ob[k] = (f, w, t, c)
         self.outs = torch.from_numpy(ob.view(np.uint8).copy()).to(dev)
-        self.groups = torch.tensor(np.asarray(groups, dtype=np.int32), device=dev)
+        ga = np.asarray(groups, dtype=np.int32)
+        if dev.type == "cuda":
+            sizes = (ctypes.c_int * 4)()
+            _lib.load().tdq_loss_meta_sizes(sizes)
+            if sizes[3] != 4 * ga.shape[1]:
+                raise RuntimeError(f"LFGroup is {sizes[3]} bytes in libtdq_hip.so, {4 * ga.shape[1]} here; rebuild")
+        self.groups = torch.tensor(ga, device=dev)
         # persistent inputs / outputs
         self.vals = [v.to(dev).contiguous() for v in fl.val_arrays]
         lam_offsets = lam_offsets or {}
@@ -101,4 +119,29 @@ class FusedLossOp:
                                 _lib.stream_ptr(J.device))
         _lib.check(rc, "tdq_loss_fused")
         return self.total, self.losses, self.dJ, self.dlam, self.dscal
+
+    def split_block(self, a):
+        """Block index ``b`` such that blocks ``[0, b)`` touch only points ``< a`` and blocks
+        ``[b, n_blocks)`` only points ``>= a`` (so the two ranges can run as separate launches
+        next to the jet kernels of their point ranges), or ``None``."""
+        b = 0
+        while b < self.n_blocks and self.block_spans[b][1] < a:
+            b += 1
+        if b == 0 or b == self.n_blocks:
+            return None
+        if any(lo < a for lo, _ in self.block_spans[b:]):
+            return None
+        return b
+
+    def run_range(self, J, blk0, nblk):
+        """Blocks ``[blk0, blk0 + nblk)`` only (dJ / dlam / block partials of their points; the
+        fused step tail reduces the partials), on the current stream."""
+        lib = _lib.load()
+        rc = lib.tdq_loss_fused_range(_lib.ptr(self.code), _lib.ptr(self.consts), _lib.ptr(self.outs),
+                                      _lib.ptr(self.groups), _lib.ptr(self.ptrs), self.n_groups, self.n_terms,
+                                      self.n_scal, self.fl.n_streams, self.prog.d_in, self.N, _lib.ptr(J),
+                                      _lib.ptr(self.prog.X_all), _lib.ptr(self.dJ), _lib.ptr(self.partials),
+                                      self.n_blocks, int(blk0), int(nblk), self.max_regs,
+                                      _lib.stream_ptr(J.device))
+        _lib.check(rc, "tdq_loss_fused_range")
 

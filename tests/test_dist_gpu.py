@@ -26,9 +26,9 @@ def _free_port():
     return port
 
 
-def _build(dist, world=1, precision=None):
+def _build(dist, world=1, precision=None, n_f=N_F):
     import bench
-    return bench.build_problem(N_F, world, "hip", torch.device("cuda", 0), dist, precision)
+    return bench.build_problem(n_f, world, "hip", torch.device("cuda", 0), dist, precision)
 
 
 def _worker(rank, world, port, q, precision):
@@ -42,10 +42,12 @@ def _worker(rank, world, port, q, precision):
     eng = m._get_engine(None, 10)
     loss, grads, terms = eng._phase_a()
     loss, grads, terms = eng._reduce(loss, grads, terms)
-    res = {"loss": float(loss), "gflat": grads[0].detach().cpu().clone()}
+    # numpy over the queue: a torch tensor travels as a shared-memory handle that is gone once
+    # this process exits
+    res = {"loss": float(loss), "gflat": grads[0].detach().cpu().numpy().copy()}
     m.fit(tf_iter=8)                       # graph-captured (split around the all-reduce)
     res["hist"] = [h["Total Loss"] for h in m.losses]
-    res["flat_after"] = m.u_model.flat.detach().cpu().clone()
+    res["flat_after"] = m.u_model.flat.detach().cpu().numpy().copy()
     m.fit(newton_iter=3)
     res["lbfgs_loss"] = float(m.min_loss["l-bfgs"])
     if rank == 0:
@@ -78,26 +80,28 @@ def test_dp_two_ranks_on_gpu_match_single_process(precision):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert res["loss"] == pytest.approx(loss, rel=1e-4)
-    assert ((res["gflat"] - g_ref).norm() / g_ref.norm()).item() < 1e-3
+    gflat, flat_after = torch.from_numpy(res["gflat"]), torch.from_numpy(res["flat_after"])
+    assert ((gflat - g_ref).norm() / g_ref.norm()).item() < 1e-3
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-3)
-    assert ((res["flat_after"] - ref_flat).norm() / ref_flat.norm()).item() < 1e-3
+    assert ((flat_after - ref_flat).norm() / ref_flat.norm()).item() < 1e-3
     assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=5e-2)
 
 
-def _forced_worker(q, precision, dp_graph):
-    os.environ.update(TDQ_FORCE_DP="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TDQ_DP_GRAPH=dp_graph)
+def _forced_worker(q, precision, dp_graph, n_f=N_F, split="auto"):
+    os.environ.update(TDQ_FORCE_DP="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TDQ_DP_GRAPH=dp_graph,
+                      TDQ_SPLIT=split)
     os.environ.pop("MASTER_PORT", None)
     from tensordiffeq_amd.parallel import dist as pdist
     pdist.reset_context()
     ctx = pdist.init_distributed(device="cuda:0")       # backend nccl = RCCL
     assert ctx.backend == "nccl" and ctx.is_distributed and ctx.forced
     assert ctx.graph_collectives == (dp_graph == "1")
-    m = _build(True, 1, precision)
+    m = _build(True, 1, precision, n_f)
     assert m.active_backend == "hip"
     m.fit(tf_iter=8)
     eng = m._get_engine(None, 1)
     res = {"hist": [h["Total Loss"] for h in m.losses], "flat": m.u_model.flat.detach().cpu().numpy().copy(),
-           "one_graph": eng.graph_b is None}
+           "one_graph": eng.graph_b is None, "ranges": getattr(eng, "_ranges", None)}
     m.fit(newton_iter=3)
     res["lbfgs_loss"] = float(m.min_loss["l-bfgs"])
     q.put(res)
@@ -124,6 +128,31 @@ def test_forced_dp_rccl_world1_matches_single_process(dp_graph):
     p.join(timeout=120)
     assert p.exitcode == 0
     assert res["one_graph"] == (dp_graph == "1")
+    assert res["hist"] == pytest.approx(ref_hist, rel=1e-6)
+    assert torch.allclose(torch.from_numpy(res["flat"]), ref_flat, rtol=1e-6, atol=1e-7)
+    assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=1e-6)
+
+
+@pytest.mark.timeout(600)
+def test_forced_dp_rccl_point_ranges(monkeypatch):
+    """The DP step with its points in two ranges on concurrent graph branches (TDQ_SPLIT, the
+    in-place bucket tail after them, RCCL all-reduce in the graph) against the single-process run
+    with single launches."""
+    precision, n_f = "bf16", 20000
+    monkeypatch.setenv("TDQ_SPLIT", "0")
+    ref = _build(False, 1, precision, n_f)
+    ref.fit(tf_iter=8)
+    ref_hist = [h["Total Loss"] for h in ref.losses]
+    ref_flat = ref.u_model.flat.detach().cpu().clone()
+    ref.fit(newton_iter=3)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(q, precision, "1", n_f, "0.5"))
+    p.start()
+    res = q.get(timeout=500)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert res["ranges"] is not None and len(res["ranges"]) == 2
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-6)
     assert torch.allclose(torch.from_numpy(res["flat"]), ref_flat, rtol=1e-6, atol=1e-7)
     assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=1e-6)

@@ -529,3 +529,32 @@ def test_solver_unequal_widths_hip_matches_jet(prec):
         assert ((x - y).norm() / y.norm().clamp_min(1e-12)).item() < 10 * tol
     a.fit(tf_iter=10)
     assert all(np_isfinite(r["Total Loss"]) for r in a.losses)
+
+
+@pytest.mark.parametrize("prec,cuts", [("bf16x3", "0.4"), ("bf16", "0.5"), ("bf16", "0.3")])
+def test_point_ranges_match_single_launch(prec, cuts, monkeypatch):
+    """Point ranges on concurrent graph branches (fit.point_ranges: forward -> fused loss ->
+    backward per range, one stream each) keep every workgroup's index and buffers, so the Adam
+    trajectory, the L-BFGS objective and the L-BFGS trajectory are bitwise those of single
+    launches."""
+    res = []
+    for split in ("0", cuts):
+        monkeypatch.setenv("TDQ_SPLIT", split)
+        m = _ac_sa_model(prec, n_f=20000)
+        m.fit(tf_iter=40)
+        eng = m._get_engine(None, 1)
+        assert (eng._ranges is None) == (split == "0")
+        hist = [h["Total Loss"] for h in m.losses]
+        flat = m.u_model.flat.detach().clone()
+        lam = m.lambdas[0].detach().clone()
+        from tensordiffeq_amd.fit import LossGradEngine
+        le = LossGradEngine(m, m.program(precision=prec), m.lambdas)
+        f0, g0 = le(m.u_model.flat.detach().clone())
+        assert (le._ranges is None) == (split == "0")
+        m.fit(newton_iter=30)
+        res.append((hist, flat, lam, float(f0), g0.clone(), m.u_model.flat.detach().clone()))
+    a, b = res
+    assert a[0] == b[0]
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3] == b[3] and torch.equal(a[4], b[4])
+    assert torch.equal(a[5], b[5])
