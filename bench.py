@@ -126,10 +126,12 @@ def time_steps(eng, ctx, device, steps, warmup, min_warmup_s):
         n_warm += max(10, warmup)
         sync()
     # room in the device loss history for the timed steps: a re-allocation would re-capture the
-    # step graph inside the timed region; one more (untimed) step replays the final graph
-    eng._ensure_hist(steps + 2)
-    eng.run(1)
-    n_warm += 1
+    # step graphs inside the timed region; K + 1 more (untimed) steps capture / replay the final
+    # 1-step and K-step graphs (fit.AdamEngine._unroll)
+    K = eng._unroll()
+    eng._ensure_hist(steps + K + 3)
+    eng.run(K + 1)
+    n_warm += K + 1
     sync()
     warm_s = time.perf_counter() - t_w
     ctx.barrier()

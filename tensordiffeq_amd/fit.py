@@ -117,6 +117,7 @@ class AdamEngine:
                 new[: st["hist"].shape[0]] = st["hist"]
             st["hist"] = new
             self.graph_a = self.graph_b = None  # history pointer changed
+            self.graph_k = None
 
     # ---------------------------------------------------------------- step pieces -------
     def _fused_map(self, fop):
@@ -263,6 +264,16 @@ class AdamEngine:
         self._tail_ok = ok
         return ok
 
+    def _step_buffers(self):
+        """Jets, forward scratch (saved activations + weight images), gradient slabs and the
+        theta gradient of the fused-tail step, allocated once per engine."""
+        if getattr(self, "_bufs", None) is None:
+            from .ops import jet_hip
+            prog = self.program
+            J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+            self._bufs = (J, saved, jet_hip.alloc_backward(saved), torch.empty_like(self.flat))
+        return self._bufs
+
     def _point_ranges(self, fop):
         if getattr(self, "_ranges", 0) == 0:
             self._ranges = point_ranges(self.program, fop)
@@ -282,14 +293,11 @@ class AdamEngine:
         if st["best_flat"].numel() != self.flat.numel():
             raise ValueError(f"best-weights snapshot has {st['best_flat'].numel()} elements, parameters "
                              f"{self.flat.numel()}")
-        if self._point_ranges(fop):  # point ranges on concurrent graph branches (see point_ranges)
-            saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams, pack=not in_graph)
-            grad = torch.empty_like(self.flat)
-        else:
-            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
-                                           pack=not in_graph)
-            fop(J, with_total=False, reduce=False)
-            grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False)
+        # persistent buffers: every captured step (the 1-step and the K-step graph) reads the weight
+        # images the previous step's tail wrote into this one scratch
+        J, saved, work, grad = self._step_buffers()
+        rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
+        run_ranges(prog, fop, self.flat, rng, self._streams, pack=not in_graph, bufs=(J, saved, work))
         grads = self._fused_grads(fop, grad, fop.dlam, fop.dscal)
         packed = fused.group_array(self._opt_groups(grads))
         if packed is None:  # gradient tensors the single launch cannot take: reduce, then Adam
@@ -423,6 +431,18 @@ class AdamEngine:
             grads[i] = gg.view_as(grads[i])
         self.static_loss = (self._dp_tail_phase_b if tail else self._phase_b)(scal[0], grads, scal[1:])
 
+    def _capture_k(self, k):
+        """K fused-tail steps in ONE graph (single process): replays of a 1-step graph leave the
+        GPU idle ~9 us between graphs (rocprofv3 kernel trace, tools/timeline.py); inside a
+        graph the steps follow back to back.  Every step's state lives on the device (epoch,
+        history row, counters, best tracking), so K captured copies are K real steps."""
+        pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with capture_graph(g, pool=pool):
+            for _ in range(k):
+                loss = self._tail_step(in_graph=True)
+        self.graph_k, self.static_loss_k, self._k = g, loss, k
+
     def _replay(self):
         self.graph_a.replay()
         if self.graph_b is not None:
@@ -440,6 +460,7 @@ class AdamEngine:
         if any(a is not b for a, b in zip(opts, self.opts)) or sig != getattr(self, "_sig", sig):
             self._bind_opts()
             self.graph_a = self.graph_b = None
+            self.graph_k = None
         self._sig = sig
         self._ensure_hist(n_steps)
         use_graph = _use_graphs(self.device) if use_graph is None else use_graph
@@ -458,15 +479,35 @@ class AdamEngine:
             from .ops import jet_hip
             jet_hip.pack_images(self._graph_saved)
         checked = int(st["epoch_host"]) - done
+        K = self._unroll()
+        if use_graph and self.graph_a is not None and K > 1 and n_steps - done >= K \
+                and getattr(self, "graph_k", None) is None:
+            self._capture_k(K)
         while done < n_steps:
-            loss = self._replay() if (use_graph and self.graph_a is not None) else self._eager_step()
-            done += 1
-            st["epoch_host"] += 1
+            # K steps at once unless that would jump over a progress / NaN-check point
+            next_log = (done // log_every + 1) * log_every if progress is not None else n_steps
+            if use_graph and K > 1 and getattr(self, "graph_k", None) is not None and n_steps - done >= K \
+                    and done + K <= next_log:
+                self.graph_k.replay()
+                loss = self.static_loss_k
+                done += K
+                st["epoch_host"] += K
+            else:
+                loss = self._replay() if (use_graph and self.graph_a is not None) else self._eager_step()
+                done += 1
+                st["epoch_host"] += 1
             if progress is not None and (done % log_every == 0 or done == n_steps):
                 checked = self._check_finite(checked)
                 progress(done, float(loss))
         self._check_finite(checked)
         return loss
+
+    def _unroll(self):
+        """Steps per multi-step graph (``TDQ_STEP_UNROLL``, default 8): single-process fused-tail
+        steps only; 1 = one graph per step."""
+        if self.dist.is_distributed or not self._tail_eligible():
+            return 1
+        return max(1, int(os.environ.get("TDQ_STEP_UNROLL", "8")))
 
     def _check_finite(self, lo):
         """Failure detection: the loss-history rows ``[lo, epoch)`` written on the
@@ -539,22 +580,36 @@ def point_ranges(program, fop):
     return [(cuts[i], cuts[i + 1], blks[i], blks[i + 1] - blks[i]) for i in range(len(cuts) - 1)]
 
 
-def run_ranges(program, fop, flat, ranges, streams, pack=True):
-    """Forward -> fused loss -> backward of every point range on its own stream (forked from and
-    joined back into the current one).  Returns ``(saved, work)`` for the fused step tail."""
+def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None):
+    """Forward -> fused loss -> backward of every point range, each range on its own stream
+    (forked from and joined back into the current one; one range runs on the current stream).
+    ``bufs``: ``(J, saved, work)`` to reuse (persistent step buffers), else allocated here.
+    Returns ``(saved, work)`` for the fused step tail."""
     from .ops import jet_hip
-    J, saved = jet_hip.alloc_forward(program.X_all, flat, program.net, program.plan, program.precision)
-    work = jet_hip.alloc_backward(saved)
+    if bufs is None:
+        J, saved = jet_hip.alloc_forward(program.X_all, flat, program.net, program.plan, program.precision)
+        work = jet_hip.alloc_backward(saved)
+    else:
+        J, saved, work = bufs
     if pack:
         jet_hip.pack_images(saved)
+    if len(ranges) == 1:
+        lo, hi, b0, nb = ranges[0]
+        jet_hip.forward_range(saved, J, lo, hi)
+        fop.run_range(J, b0, nb)
+        jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
+        return saved, work
+    # (keeping one range on the current stream measured the same: the graph runtime picks the
+    # hardware queues of its branches itself, and the join still waits ~9 us across queues)
     cur = torch.cuda.current_stream(flat.device)
-    for (lo, hi, b0, nb), st in zip(ranges, streams):
+    for st in streams[:len(ranges)]:
         st.wait_stream(cur)
+    for (lo, hi, b0, nb), st in zip(ranges, streams):
         with torch.cuda.stream(st):
             jet_hip.forward_range(saved, J, lo, hi)
             fop.run_range(J, b0, nb)
             jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
-    for st in streams:
+    for st in streams[:len(ranges)]:
         cur.wait_stream(st)
     return saved, work
 

@@ -341,30 +341,36 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
         one()
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize(dev)
+    # iterations per graph (TDQ_LBFGS_UNROLL, default 8): back-to-back replays of a one-iteration
+    # graph leave the GPU idle ~9 us between graphs (tools/timeline.py); past a stopping test the
+    # extra captured iterations are no-ops, so a replay may run over the end by up to K - 1
+    import os
+    K = 1 if split else max(1, int(os.environ.get("TDQ_LBFGS_UNROLL", "8")))
     if opt.active():
         pool = torch.cuda.graph_pool_handle()
         ga = torch.cuda.CUDAGraph()
         with capture_graph(ga, pool=pool):
-            opt.axpy()
-            fg_static = evaluate()
-            if all_reduce is not None and not split:
-                all_reduce(fg_static)
-            if not split:
-                opt.update(fg_static)
+            for _ in range(K):
+                opt.axpy()
+                fg_static = evaluate()
+                if all_reduce is not None and not split:
+                    all_reduce(fg_static)
+                if not split:
+                    opt.update(fg_static)
         gb = None
         if split:
             gb = torch.cuda.CUDAGraph()
             with capture_graph(gb, pool=pool):
                 opt.update(fg_static)
         launched = 1
-        while opt.active() and launched <= 2 * max_iter + 8:  # the maxIter test always fires first
+        while opt.active() and launched <= 2 * max_iter + 8 * K:  # the maxIter test always fires first
             n = max(1, min(poll_every, max_iter - opt.n_iter + 1))
-            for _ in range(n):
+            for _ in range((n + K - 1) // K):
                 ga.replay()
                 if gb is not None:
                     all_reduce(fg_static)
                     gb.replay()
-            launched += n
+            launched += (n + K - 1) // K * K
             if on_poll is not None:
                 on_poll(opt)
     if on_poll is not None:
