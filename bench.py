@@ -226,6 +226,7 @@ def main(argv=None):
     eng = model._get_engine(None, args.warmup + args.steps + 2)
     backend = model.active_backend
     elapsed, n_warm, warm_s = time_steps(eng, ctx, device, args.steps, args.warmup, args.min_warmup_s)
+    steps_per_graph = eng._unroll()
     loss = float(model._state["hist"][int(model._state["epoch_host"]) - 1, 0])
     total_steps = int(model._state["epoch_host"])
     pts_per_s = n_glob * args.steps / elapsed
@@ -283,6 +284,11 @@ def main(argv=None):
         elif acc_err is not None:
             rec["l2_full_schedule"] = None
             rec["accuracy_error"] = acc_err
+        rec["steps_per_graph"] = steps_per_graph
+        if dist:
+            # which all-reduce the DP step captured: RCCL, or the one-shot peer kernel (csrc/peer.hip)
+            # when its start-up self-test passed and it timed faster on this node
+            rec["allreduce"] = dict(ctx.allreduce_info)
         if dp is not None:
             rec["forced_dp"] = dp
         print(json.dumps(rec), flush=True)

@@ -394,12 +394,11 @@ class AdamEngine:
         from .ops import jet_hip
         prog = self.program
         fop = prog.fused_op
-        rng = self._point_ranges(fop)
-        if rng:
-            saved, work = run_ranges(prog, fop, self.flat, rng, self._streams, pack=False)
-        else:
-            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision, pack=False)
-            fop(J, with_total=False, reduce=False)
+        # persistent step buffers (as in _tail_step): the 1-step and the K-step graph read the
+        # weight images that the previous step's dp_tail_b wrote into this one scratch
+        J, saved, work, _ = self._step_buffers()
+        rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
+        run_ranges(prog, fop, self.flat, rng, self._streams, pack=False, bufs=(J, saved, work))
         n_p = self.flat.numel()
         red_idx = self.red_idx
         if not red_idx or red_idx[0] != 0:
@@ -407,10 +406,10 @@ class AdamEngine:
         others = [i for i in red_idx[1:]]
         sizes = [self.wrt[i].numel() for i in others]
         n_e, n_t = sum(sizes), fop.n_terms
-        buf = torch.empty(n_p + n_e + 1 + n_t, dtype=torch.float32, device=self.device)
+        buf = getattr(self, "_dp_buf", None)
+        if buf is None or buf.numel() != n_p + n_e + 1 + n_t:
+            buf = self._dp_buf = torch.empty(n_p + n_e + 1 + n_t, dtype=torch.float32, device=self.device)
         grad_view = buf[:n_p]
-        if not rng:
-            grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=grad_view)
         jet_hip.dp_tail_a(saved, work, grad_view, fop, total=buf[n_p + n_e:n_p + n_e + 1],
                           losses=buf[n_p + n_e + 1:])
         grads = self._fused_grads(fop, grad_view, fop.dlam, fop.dscal)
@@ -440,7 +439,13 @@ class AdamEngine:
         g = torch.cuda.CUDAGraph()
         with capture_graph(g, pool=pool):
             for _ in range(k):
-                loss = self._tail_step(in_graph=True)
+                if self.dist.is_distributed:   # graph_collectives: the all-reduce is a graph node
+                    self._dp_half_a(True)
+                    self.dist.all_reduce_(self._bucket_buf)
+                    self._dp_half_b(True)
+                    loss = self.static_loss
+                else:
+                    loss = self._tail_step(in_graph=True)
         self.graph_k, self.static_loss_k, self._k = g, loss, k
 
     def _replay(self):
@@ -503,9 +508,10 @@ class AdamEngine:
         return loss
 
     def _unroll(self):
-        """Steps per multi-step graph (``TDQ_STEP_UNROLL``, default 8): single-process fused-tail
-        steps only; 1 = one graph per step."""
-        if self.dist.is_distributed or not self._tail_eligible():
+        """Steps per multi-step graph (``TDQ_STEP_UNROLL``, default 8): fused-tail steps, single
+        process or DP with the all-reduce captured in the graph (RCCL / peer); 1 = one graph per
+        step."""
+        if not self._tail_eligible() or (self.dist.is_distributed and not self.dist.graph_collectives):
             return 1
         return max(1, int(os.environ.get("TDQ_STEP_UNROLL", "8")))
 
@@ -518,6 +524,7 @@ class AdamEngine:
         disables the check.  Returns the new low-water mark."""
         st = self.state
         hi = int(st["epoch_host"])
+        self.dist.check_health()
         if hi <= lo or os.environ.get("TDQ_NAN_CHECK", "1") == "0":
             return hi
         col = st["hist"][lo:hi, 0]

@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _lock = threading.Lock()
 _lib = None
@@ -63,6 +63,15 @@ def _declare(lib):
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
         "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P]),
+        # one-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py)
+        "tdq_peer_maxw": (I, []),
+        "tdq_peer_chunk": (I, []),
+        "tdq_peer_alloc": (I, [L, I, P]),
+        "tdq_peer_free": (I, [P]),
+        "tdq_peer_ipc_handle": (I, [P, P]),
+        "tdq_peer_ipc_open": (I, [P, P]),
+        "tdq_peer_ipc_close": (I, [P]),
+        "tdq_peer_allreduce": (I, [P, I, I, I, L, I, P, P, P, P, L, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

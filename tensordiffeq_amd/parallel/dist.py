@@ -19,9 +19,12 @@ Design here:
   world 1, so the DP machinery - split or single HIP graph around the collective, bucket packing,
   RCCL itself - runs (and is tested / timed) on a one-GPU box; at world 1 it must reproduce the
   single-process trajectory.
-* ``graph_collectives``: with RCCL the bucket all-reduce is captured INSIDE the step's HIP graph
-  (one replay per step, no host-launched collective); gloo, or ``TDQ_DP_GRAPH=0``, keeps the
-  two-graph split with the collective launched from the host in between.
+* ``graph_collectives``: with RCCL (or the peer all-reduce) the bucket all-reduce is captured
+  INSIDE the step's HIP graph (one replay per step, no host-launched collective); plain gloo, or
+  ``TDQ_DP_GRAPH=0``, keeps the two-graph split with the collective launched from the host.
+* Peer all-reduce (``parallel/peer.py``, ``csrc/peer.hip``): GPU ranks on one host may replace
+  ``dist.all_reduce`` of the fp32 bucket with a one-shot push over xGMI (self-tested and, in
+  ``auto`` mode, timed against RCCL at start-up; ``ctx.allreduce_info`` records the choice).
 """
 from __future__ import annotations
 
@@ -42,6 +45,8 @@ class DistContext:
         self.backend = backend
         self.initialized = initialized
         self.forced = forced
+        self.peer = None            # parallel.peer.PeerComm when the one-shot all-reduce is on
+        self.allreduce_info = {"impl": "torch.distributed"}
 
     @property
     def is_distributed(self):
@@ -50,8 +55,8 @@ class DistContext:
     @property
     def graph_collectives(self):
         """Capture the per-step all-reduce inside the step's HIP graph (RCCL only)."""
-        return (self.is_distributed and self.backend == "nccl" and self.device.type == "cuda"
-                and os.environ.get("TDQ_DP_GRAPH", "1") != "0")
+        return (self.is_distributed and (self.backend == "nccl" or self.peer is not None)
+                and self.device.type == "cuda" and os.environ.get("TDQ_DP_GRAPH", "1") != "0")
 
     def barrier(self):
         if self.is_distributed:
@@ -62,8 +67,17 @@ class DistContext:
 
     def all_reduce_(self, buf):
         if self.is_distributed:
-            dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+            if self.peer is not None and self.peer.accepts(buf):
+                self.peer.all_reduce_(buf)
+            else:
+                dist.all_reduce(buf, op=dist.ReduceOp.SUM)
         return buf
+
+    def check_health(self):
+        """Raise if the peer all-reduce ever timed out waiting for a rank (read at the
+        progress / NaN-check cadence, never inside a step)."""
+        if self.peer is not None:
+            self.peer.check()
 
     def broadcast_(self, buf, src=0):
         if self.is_distributed:
@@ -134,6 +148,9 @@ def init_distributed(backend=None, device=None, timeout_s=600, force=None):
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         initialized = True
     _CTX = DistContext(rank, world, local_rank, device, backend, initialized, forced=force and world == 1)
+    if initialized and world > 1 and device.type == "cuda":
+        from . import peer
+        _CTX.peer = peer.setup(_CTX)
     return _CTX
 
 
@@ -165,6 +182,9 @@ def shard(t, rank, world):
 
 def destroy():
     global _CTX
+    if _CTX is not None and _CTX.peer is not None:
+        _CTX.peer.close()
+        _CTX.peer = None
     if dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

@@ -1,0 +1,218 @@
+"""One-shot peer-memory all-reduce over xGMI (``csrc/peer.hip``) for the per-step DP bucket.
+
+The reference all-reduces gradients with NCCL inside ``MirroredStrategy.apply_gradients``
+(``tensordiffeq/fit.py:150-224``).  Here the message is one ~196 KiB fp32 bucket per ~0.2 ms step:
+latency, not bandwidth, decides.  RCCL's ring pays 2 (world - 1) hops; MI355X nodes wire every GPU
+pair with its own xGMI link, so :class:`PeerComm` lets each rank write its bucket straight into a
+receive slot of every peer (one hop, all links at once) and sum the world copies in rank order
+(bitwise identical on every rank).  The receive slots and flags live in one uncached device
+allocation per rank, shared with ``hipIpcGetMemHandle`` / ``hipIpcOpenMemHandle``; the handle
+exchange rides on the torch.distributed process group (RCCL or gloo).
+
+:func:`setup` runs collectively from :func:`..parallel.dist.init_distributed` on GPU ranks of one
+host: it builds the communicator, self-tests it (three calls, both receive parities, exact integer
+data checked on every rank) and - in ``auto`` mode - times it against ``dist.all_reduce`` on a
+bucket-sized buffer, keeping whichever is faster (decided on the max over ranks, so every rank
+agrees).  Any failure on any rank disables it on all ranks (``dist.all_reduce`` stays).
+``TDQ_PEER_ALLREDUCE``: ``auto`` (default), ``1`` (use it whenever the self-test passes), ``0``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import socket
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+_KINDS = {0: "uncached", 1: "fine-grained", 2: "coarse"}
+
+
+def mode():
+    m = os.environ.get("TDQ_PEER_ALLREDUCE", "auto").strip().lower()
+    return m if m in ("auto", "0", "1") else "auto"
+
+
+class PeerComm:
+    """Peer receive slots + flags of every rank mapped into this process; :meth:`all_reduce_` sums
+    a contiguous fp32 CUDA tensor over ranks in place (one kernel on the current stream).
+
+    Construct on every rank at the same time (the IPC handles are all-gathered)."""
+
+    def __init__(self, rank, world, device, cap_floats=None, kind=None, timeout_s=None):
+        lib = _lib.load(required=True)
+        self.lib, self.rank, self.world, self.device = lib, rank, world, torch.device(device)
+        self.maxw, self.chunk = lib.tdq_peer_maxw(), lib.tdq_peer_chunk()
+        if not 1 <= world <= self.maxw:
+            raise ValueError(f"peer all-reduce supports 1..{self.maxw} ranks, got {world}")
+        cap = int(cap_floats or os.environ.get("TDQ_PEER_CAP", 1 << 20))
+        self.cap = (cap + self.chunk - 1) // self.chunk * self.chunk
+        self.max_blocks = self.cap // self.chunk
+        self.recv_bytes = 2 * self.maxw * self.cap * 4
+        flag_bytes = self.maxw * self.max_blocks * 4
+        self.timeout_ticks = int(float(timeout_s or os.environ.get("TDQ_PEER_TIMEOUT_S", 30)) * 1e8)
+        self._base = ctypes.c_void_p(0)
+        self._opened = []
+        kinds = [kind] if kind is not None else [0, 1, 2]
+        rc = -1
+        for k in kinds:
+            rc = lib.tdq_peer_alloc(self.recv_bytes + flag_bytes, k, ctypes.byref(self._base))
+            if rc == 0:
+                self.kind = k
+                break
+        _lib.check(rc, "tdq_peer_alloc")
+        self.seqs = torch.zeros(self.max_blocks, dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._recv = (ctypes.c_void_p * world)()
+        self._flag = (ctypes.c_void_p * world)()
+
+    # -- collective setup ------------------------------------------------------------------
+    def handle(self):
+        h = ctypes.create_string_buffer(64)
+        _lib.check(self.lib.tdq_peer_ipc_handle(self._base, h), "hipIpcGetMemHandle")
+        return bytes(h.raw)
+
+    def open_peers(self, handles):
+        """Map every peer's region (``handles[q]``: rank q's 64-byte IPC handle)."""
+        for q in range(self.world):
+            if q == self.rank:
+                base = self._base.value
+            else:
+                p = ctypes.c_void_p(0)
+                _lib.check(self.lib.tdq_peer_ipc_open(ctypes.create_string_buffer(handles[q], 64), ctypes.byref(p)),
+                           f"hipIpcOpenMemHandle(rank {q})")
+                self._opened.append(p)
+                base = p.value
+            self._recv[q] = base
+            self._flag[q] = base + self.recv_bytes
+
+    # -- data path -------------------------------------------------------------------------
+    def accepts(self, buf):
+        return (buf.is_cuda and buf.dtype == torch.float32 and buf.is_contiguous() and buf.numel() <= self.cap
+                and buf.data_ptr() % 16 == 0 and buf.device == self.device)
+
+    def all_reduce_(self, buf):
+        rc = self.lib.tdq_peer_allreduce(_lib.ptr(buf), buf.numel(), self.rank, self.world, self.cap,
+                                         self.max_blocks, self._recv, self._flag, _lib.ptr(self.seqs),
+                                         _lib.ptr(self.err), self.timeout_ticks, _lib.stream_ptr(self.device))
+        _lib.check(rc, "tdq_peer_allreduce")
+        return buf
+
+    def check(self):
+        """Raise if a wait ever timed out (a peer did not arrive within TDQ_PEER_TIMEOUT_S)."""
+        if int(self.err.item()) != 0:
+            raise RuntimeError(f"peer all-reduce: rank {self.rank} timed out waiting for a peer "
+                               f"(TDQ_PEER_TIMEOUT_S); results of the steps since the last check are invalid")
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            self.lib.tdq_peer_ipc_close(p)
+        self._opened = []
+        if self._base.value:
+            self.lib.tdq_peer_free(self._base)
+            self._base = ctypes.c_void_p(0)
+
+
+def _gather(obj, world):
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def _self_test(comm, n):
+    """Three calls (both receive parities, then the first again) on exact small integers."""
+    ok = True
+    idx = torch.arange(n, device=comm.device, dtype=torch.float32)
+    for it in range(3):
+        buf = (idx.remainder(97) + 1.0) * (comm.rank + 1 + it)
+        comm.all_reduce_(buf)
+        tot = sum(q + 1 + it for q in range(comm.world))
+        want = (idx.remainder(97) + 1.0) * tot
+        ok = ok and bool(torch.equal(buf, want))
+    torch.cuda.synchronize(comm.device)
+    return ok and int(comm.err.item()) == 0
+
+
+def _time_us(fn, buf, reps=30):
+    for _ in range(3):
+        fn(buf)
+    torch.cuda.synchronize(buf.device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn(buf)
+    torch.cuda.synchronize(buf.device)
+    return (time.perf_counter() - t0) / reps * 1e6
+
+
+def setup(ctx, bench_floats=49_408):
+    """Collectively build, self-test and (``auto``) time the peer all-reduce; returns the
+    :class:`PeerComm` to use, or ``None``.  Records what happened in ``ctx.allreduce_info``."""
+    m = mode()
+    info = {"impl": "torch.distributed", "peer_mode": m}
+    ctx.allreduce_info = info
+    if m == "0" or ctx.device.type != "cuda" or ctx.world < 2 or not _lib.available():
+        return None
+    W = ctx.world
+    hosts = _gather(socket.gethostname(), W)
+    if len(set(hosts)) != 1:
+        info["peer"] = "off: ranks on more than one host"
+        return None
+    comm, err = None, None
+    try:
+        comm = PeerComm(ctx.rank, W, ctx.device)
+        h = comm.handle()
+    except Exception as e:  # noqa: BLE001 - reported, every rank falls back together
+        h, err = None, f"{type(e).__name__}: {e}"
+    handles = _gather(h, W)
+    if any(x is None for x in handles):
+        info["peer"] = f"off: setup failed ({err or 'on another rank'})"
+        if comm is not None:
+            comm.close()
+        return None
+    try:
+        comm.open_peers(handles)
+        ok = True
+    except Exception as e:  # noqa: BLE001
+        ok, err = False, f"{type(e).__name__}: {e}"
+    oks = _gather(ok, W)
+    if not all(oks):
+        info["peer"] = f"off: IPC open failed ({err or 'on another rank'})"
+        comm.close()
+        return None
+    try:
+        ok = _self_test(comm, min(comm.cap, bench_floats + 777))
+    except Exception as e:  # noqa: BLE001
+        ok, err = False, f"{type(e).__name__}: {e}"
+    oks = _gather(ok, W)
+    info["memory"] = _KINDS.get(comm.kind, "?")
+    if not all(oks):
+        info["peer"] = f"off: self-test failed ({err or 'wrong sums or a timeout'})"
+        comm.close()
+        return None
+    buf = torch.randn(bench_floats, device=ctx.device)
+    t_peer = _time_us(comm.all_reduce_, buf)
+    if m == "auto":
+        t_ref = _time_us(lambda b: dist.all_reduce(b, op=dist.ReduceOp.SUM), buf)
+    else:
+        t_ref = float("nan")
+    ts = _gather([t_peer, t_ref], W)
+    t_peer = max(x[0] for x in ts)
+    t_ref = max(x[1] for x in ts)
+    info.update(peer_us=round(t_peer, 2), torch_us=None if t_ref != t_ref else round(t_ref, 2),
+                bench_floats=bench_floats)
+    use = m == "1" or not (t_ref <= t_peer)
+    if comm.err.item() != 0:  # a late timeout during the timing
+        use = False
+    uses = _gather(use, W)
+    if not all(uses):
+        info["peer"] = "off: slower than torch.distributed" if all(not u for u in uses) else "off: disagreement"
+        comm.close()
+        return None
+    info["impl"] = "peer one-shot"
+    info["peer"] = "on"
+    return comm

@@ -31,9 +31,9 @@ def _build(dist, world=1, precision=None, n_f=N_F):
     return bench.build_problem(n_f, world, "hip", torch.device("cuda", 0), dist, precision)
 
 
-def _worker(rank, world, port, q, precision):
+def _worker(rank, world, port, q, precision, peer="0"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE=peer)
     from tensordiffeq_amd.parallel import dist as pdist
     pdist.reset_context()
     ctx = pdist.init_distributed(backend="gloo", device="cuda:0")
@@ -47,6 +47,8 @@ def _worker(rank, world, port, q, precision):
     res = {"loss": float(loss), "gflat": grads[0].detach().cpu().numpy().copy()}
     m.fit(tf_iter=8)                       # graph-captured (split around the all-reduce)
     res["hist"] = [h["Total Loss"] for h in m.losses]
+    res["peer"] = ctx.peer is not None
+    res["one_graph"] = m._get_engine(None, 1).graph_b is None
     res["flat_after"] = m.u_model.flat.detach().cpu().numpy().copy()
     m.fit(newton_iter=3)
     res["lbfgs_loss"] = float(m.min_loss["l-bfgs"])
@@ -57,8 +59,10 @@ def _worker(rank, world, port, q, precision):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
-def test_dp_two_ranks_on_gpu_match_single_process(precision):
+@pytest.mark.parametrize("precision,peer", [("bf16x3", "0"), ("bf16", "0"), ("bf16", "1")])
+def test_dp_two_ranks_on_gpu_match_single_process(precision, peer):
+    """peer "1": the bucket all-reduce is the one-shot peer kernel (csrc/peer.hip), captured in the
+    step graph (one replay per step); "0": gloo between two graphs."""
     ref = _build(False, 1, precision)
     eng = ref._get_engine(None, 10)
     loss, grads, terms = eng._phase_a()
@@ -72,13 +76,14 @@ def test_dp_two_ranks_on_gpu_match_single_process(precision):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, precision)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, precision, peer)) for r in range(2)]
     for p in procs:
         p.start()
     res = q.get(timeout=500)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    assert res["peer"] == (peer == "1") and res["one_graph"] == (peer == "1")
     assert res["loss"] == pytest.approx(loss, rel=1e-4)
     gflat, flat_after = torch.from_numpy(res["gflat"]), torch.from_numpy(res["flat_after"])
     assert ((gflat - g_ref).norm() / g_ref.norm()).item() < 1e-3
@@ -87,9 +92,9 @@ def test_dp_two_ranks_on_gpu_match_single_process(precision):
     assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=5e-2)
 
 
-def _forced_worker(q, precision, dp_graph, n_f=N_F, split="auto"):
+def _forced_worker(q, precision, dp_graph, n_f=N_F, split="auto", iters=8, unroll="8"):
     os.environ.update(TDQ_FORCE_DP="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TDQ_DP_GRAPH=dp_graph,
-                      TDQ_SPLIT=split)
+                      TDQ_SPLIT=split, TDQ_STEP_UNROLL=unroll)
     os.environ.pop("MASTER_PORT", None)
     from tensordiffeq_amd.parallel import dist as pdist
     pdist.reset_context()
@@ -98,10 +103,11 @@ def _forced_worker(q, precision, dp_graph, n_f=N_F, split="auto"):
     assert ctx.graph_collectives == (dp_graph == "1")
     m = _build(True, 1, precision, n_f)
     assert m.active_backend == "hip"
-    m.fit(tf_iter=8)
+    m.fit(tf_iter=iters)
     eng = m._get_engine(None, 1)
     res = {"hist": [h["Total Loss"] for h in m.losses], "flat": m.u_model.flat.detach().cpu().numpy().copy(),
-           "one_graph": eng.graph_b is None, "ranges": getattr(eng, "_ranges", None)}
+           "one_graph": eng.graph_b is None, "ranges": getattr(eng, "_ranges", None),
+           "k_graph": getattr(eng, "graph_k", None) is not None}
     m.fit(newton_iter=3)
     res["lbfgs_loss"] = float(m.min_loss["l-bfgs"])
     q.put(res)
@@ -156,3 +162,24 @@ def test_forced_dp_rccl_point_ranges(monkeypatch):
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-6)
     assert torch.allclose(torch.from_numpy(res["flat"]), ref_flat, rtol=1e-6, atol=1e-7)
     assert res["lbfgs_loss"] == pytest.approx(float(ref.min_loss["l-bfgs"]), rel=1e-6)
+
+
+@pytest.mark.timeout(600)
+def test_forced_dp_rccl_multistep_graph():
+    """DP with the all-reduce in the graph also runs K steps per graph (TDQ_STEP_UNROLL): 4-step
+    graphs over persistent step buffers, RCCL all-reduce inside, against the single process."""
+    precision, iters = "bf16", 21
+    ref = _build(False, 1, precision)
+    ref.fit(tf_iter=iters)
+    ref_hist = [h["Total Loss"] for h in ref.losses]
+    ref_flat = ref.u_model.flat.detach().cpu().clone()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(q, precision, "1", N_F, "auto", iters, "4"))
+    p.start()
+    res = q.get(timeout=500)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert res["one_graph"] and res["k_graph"]
+    assert res["hist"] == pytest.approx(ref_hist, rel=1e-6)
+    assert torch.allclose(torch.from_numpy(res["flat"]), ref_flat, rtol=1e-6, atol=1e-7)

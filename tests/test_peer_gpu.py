@@ -1,0 +1,95 @@
+"""One-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py) with 2 ranks sharing cuda:0.
+
+Two processes on one GPU exercise everything the 8-GPU xGMI path runs except the fabric: the
+uncached IPC-shared receive slots and flags, the push / flag / bounded wait / rank-order sum
+kernel, the self-test and selection at start-up, graph capture of the kernel, and both receive
+parities.  The control plane (IPC handle exchange) rides on a gloo group.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 3, 1000, 1024, 1025, 4097, 49_408, 200_001]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE="1", TDQ_PEER_TIMEOUT_S="20")
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(backend="gloo", device="cuda:0")
+    res = {"info": dict(ctx.allreduce_info), "on": ctx.peer is not None}
+    if ctx.peer is not None:
+        dev = ctx.device
+        outs = {}
+        for n in SIZES:
+            g = torch.Generator().manual_seed(1000 * n + rank)
+            x = torch.randn(n, generator=g)
+            buf = x.to(dev)
+            ctx.all_reduce_(buf)
+            outs[n] = buf.cpu().numpy().copy()
+        # captured: 4 all-reduces in one graph, replayed 3 times (the call counters advance on the
+        # device, so every replay is a new pair of calls)
+        n = 49_408
+        static = torch.zeros(n, device=dev)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(4):
+                    static.mul_(0.5)
+                    ctx.all_reduce_(static)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph_out = []
+        for rep in range(3):
+            static.copy_(torch.full((n,), float(rank + 1 + rep), device=dev))
+            g.replay()
+            torch.cuda.synchronize(dev)
+            graph_out.append(static.cpu().numpy().copy())
+        ctx.check_health()
+        res.update(outs=outs, graph=graph_out, err=int(ctx.peer.err.item()))
+    q.put((rank, res))
+    ctx.barrier()
+    pdist.destroy()
+
+
+@pytest.mark.timeout(300)
+def test_peer_allreduce_two_ranks_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=250) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    print("PEER", got[0]["info"])
+    assert got[0]["on"] and got[1]["on"], got[0]["info"]
+    assert got[0]["err"] == 0 and got[1]["err"] == 0
+    for n in SIZES:
+        a = torch.randn(n, generator=torch.Generator().manual_seed(1000 * n + 0))
+        b = torch.randn(n, generator=torch.Generator().manual_seed(1000 * n + 1))
+        want = ((torch.zeros(n) + a) + b).numpy()        # the kernel's order: rank 0, then rank 1
+        assert np.array_equal(got[0]["outs"][n], want), n
+        assert np.array_equal(got[1]["outs"][n], got[0]["outs"][n]), n
+    for rep in range(3):
+        # halves of the two start values summed, then each later call halves and re-sums S
+        v = 0.5 * (float(1 + rep) + float(2 + rep))
+        assert np.all(got[0]["graph"][rep] == v) and np.all(got[1]["graph"][rep] == v), rep
