@@ -56,7 +56,7 @@ PRECISION_NOTES = {
 
 
 def build_problem(n_glob, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
-                  lbfgs_stop=None):
+                  lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1)):
     """The AC-SA problem of BASELINE.json with ``n_glob`` collocation points in total (sharded over
     ``world`` ranks when ``dist``)."""
     import tensordiffeq_amd as tdq
@@ -89,7 +89,7 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
     init_weights = {"residual": [torch.rand(n_glob, 1, generator=g)],
                     "BCs": [100 * torch.rand(512, 1, generator=g), None]}
     model = tdq.CollocationSolverND(verbose=False)
-    model.compile([2, 128, 128, 128, 128, 1], f_model, D, [init, x_periodic],
+    model.compile(list(layers), f_model, D, [init, x_periodic],
                   Adaptive_type="self-adaptive",
                   dict_adaptive={"residual": [True], "BCs": [True, False]},
                   init_weights=init_weights, backend=backend, device=device, dist=dist,

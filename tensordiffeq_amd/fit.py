@@ -559,7 +559,7 @@ def point_ranges(program, fop):
         cfg = hip_config(program.net, program.plan, program.precision)
     except ValueError:
         return None
-    if cfg["precision"] not in ("bf16x3", "bf16"):
+    if cfg["precision"] not in ("bf16x3", "bf16") or cfg.get("engine") == "layered":
         return None
     if spec == "auto":
         fracs = [0.35] if cfg["precision"] == "bf16x3" else [0.45]

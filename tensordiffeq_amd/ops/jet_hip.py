@@ -67,6 +67,9 @@ def forward_raw(X, P, net, plan, precision=None, pack=True):
     (a captured Adam step whose fused tail rewrote them, see :func:`step_tail`)."""
     lib = _lib.load()
     cfg = hip_config(net, plan, precision)
+    if is_layered(cfg):
+        from . import jet_layered
+        return jet_layered.forward_raw(X.contiguous(), P, net, plan)
     fwd, _, scratch_floats, _ = _fns(lib, cfg)
     X = X.contiguous()
     N = X.shape[0]
@@ -93,6 +96,11 @@ def backward_raw(saved, dJ, reduce=True, grad=None):
     """Flat parameter gradient for the adjoint ``dJ`` of the jet.  ``reduce=False`` (split-bf16
     only): launch only the backward kernel and return ``(grad, work)`` - the per-workgroup
     gradient slabs in ``work`` are reduced into ``grad`` later by :func:`step_tail`."""
+    if saved[0] == "layered":
+        if not reduce:
+            raise ValueError("backward_raw(reduce=False) needs the fused split-bf16 kernels")
+        from . import jet_layered
+        return jet_layered.backward_raw(saved, dJ, grad=grad)
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     _, bwd, _, slab_floats = _fns(lib, cfg)
@@ -170,7 +178,13 @@ def backward_range(saved, dJ, work, lo, hi):
 
 
 def is_split_bf16(cfg):
-    return cfg["precision"] in ("bf16x3", "bf16")
+    """The fused split-bf16 kernels (csrc/jet_bf3.h) serve this configuration."""
+    return cfg["precision"] in ("bf16x3", "bf16") and not is_layered(cfg)
+
+
+def is_layered(cfg):
+    """Hidden width beyond the fused kernels: the layer-wise engine (ops/jet_layered.py)."""
+    return cfg.get("engine") == "layered"
 
 
 def pack_images(saved):
@@ -208,12 +222,21 @@ class JetMLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, params, net, plan, precision=None):
         J, saved = forward_raw(X, params.contiguous(), net, plan, precision)
+        if saved[0] == "layered":
+            ctx.layered = saved
+            return J
+        ctx.layered = None
         ctx.save_for_backward(saved[0], saved[1], saved[2])
         ctx.meta = saved[3:]
         return J
 
     @staticmethod
     def backward(ctx, dJ):
+        if ctx.layered is not None:
+            saved = ctx.layered
+            if dJ is None:
+                dJ = torch.zeros((len(saved[5]), saved[1].shape[0], saved[3].layer_sizes[-1]), device=saved[1].device)
+            return None, backward_raw(saved, dJ), None, None, None
         X, P, scratch = ctx.saved_tensors
         cfg, spec, S = ctx.meta
         if dJ is None:

@@ -1,0 +1,137 @@
+"""Layer-wise jet engine for hidden widths beyond the fused kernels (``csrc/jet_layered.hip``).
+
+The fused jet kernels keep all derivative streams of a 16-point tile in registers through the
+whole layer stack, which bounds the hidden width at 128.  The reference accepts any layer list
+(``tensordiffeq/networks.py:10-20``), so wider networks run one layer at a time:
+
+* the S derivative streams of a layer are stacked into one ``[S*N, W]`` matrix, so every weight
+  multiplication of a layer - forward ``Z = H K``, backward ``HB = ZB K^T`` and the weight gradient
+  ``dK = H^T ZB`` (reduction over all streams and points at once) - is ONE plain library GEMM
+  (hipBLASLt via ``torch.mm``, fp32);
+* the bias, the tanh jet (value, first-, second-order streams) and its adjoint run as one fused,
+  memory-bound HIP pass per layer (``tdq_layered_epi``), the adjoint from the saved
+  post-activations only (no tanh recompute).
+
+Orders <= 2 (like the fused kernels).  On CPU the same engine runs with torch epilogues (the
+numerics oracle of the HIP pass, tests/test_layered_jet.py).  Same contract as
+:func:`.jet_hip.forward_raw` / :func:`.jet_hip.backward_raw`: ``J`` is ``(S, N, d_out)``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _spec(plan):
+    from .jet_hip import stream_spec
+    return stream_spec(plan)
+
+
+def _epi_fwd_torch(Z, bias, spec):
+    """In place Z -> H (torch mirror of ``layered_fwd_kernel``)."""
+    S = Z.shape[0]
+    z = Z.clone()
+    h = torch.tanh(z[0] + bias)
+    s1 = 1 - h * h
+    Z[0] = h
+    for s in range(1, S):
+        ty, a, b = spec[3 * s:3 * s + 3]
+        Z[s] = s1 * z[s] if ty == 1 else s1 * (z[s] - 2 * h * z[a] * z[b])
+    return Z
+
+
+def _epi_bwd_torch(HB, H, spec):
+    """In place HB -> ZB (torch mirror of ``layered_bwd_kernel``)."""
+    S = HB.shape[0]
+    hb = HB.clone()
+    h0 = H[0]
+    s1 = 1 - h0 * h0
+    acc0 = s1 * hb[0]
+    zb = [None] + [s1 * hb[s] for s in range(1, S)]
+    for s in range(1, S):
+        acc0 = acc0 - 2 * h0 * H[s] * hb[s]
+    for s in range(1, S):
+        ty, a, b = spec[3 * s:3 * s + 3]
+        if ty != 2:
+            continue
+        acc0 = acc0 - 2 * H[a] * H[b] * hb[s]
+        zb[a] = zb[a] - 2 * h0 * H[b] * hb[s]
+        zb[b] = zb[b] - 2 * h0 * H[a] * hb[s]
+    HB[0] = acc0
+    for s in range(1, S):
+        HB[s] = zb[s]
+    return HB
+
+
+def _epi(fwd, A, B, bias, spec):
+    S, N, W = A.shape
+    if A.is_cuda:
+        lib = _lib.load(required=True)
+        c = (ctypes.c_int * len(spec))(*spec)
+        rc = lib.tdq_layered_epi(1 if fwd else 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(bias), N, W, S, c,
+                                 _lib.stream_ptr(A.device))
+        _lib.check(rc, "tdq_layered_epi")
+        return A
+    return _epi_fwd_torch(A, bias, spec) if fwd else _epi_bwd_torch(A, B, spec)
+
+
+@torch.no_grad()
+def forward_raw(X, P, net, plan):
+    """``(J, saved)``; ``saved`` feeds :func:`backward_raw`."""
+    spec = _spec(plan)
+    ws = net.weights(P)
+    S, N = plan.S, X.shape[0]
+    K0, b0 = ws[0]
+    W0 = K0.shape[1]
+    Z = torch.zeros((S, N, W0), dtype=P.dtype, device=X.device)
+    torch.mm(X, K0, out=Z[0])                       # layer 0: the input is exact (no GEMM on streams)
+    for s in range(1, S):
+        if spec[3 * s] == 1:
+            Z[s].copy_(K0[spec[3 * s + 1]].expand(N, W0))
+    Hs = [_epi(True, Z, None, b0, spec)]
+    for K, b in ws[1:-1]:
+        Hp = Hs[-1]
+        Z = torch.mm(Hp.view(S * N, Hp.shape[2]), K).view(S, N, K.shape[1])
+        Hs.append(_epi(True, Z, None, b, spec))
+    Ko, bo = ws[-1]
+    Hl = Hs[-1]
+    J = torch.mm(Hl.view(S * N, Hl.shape[2]), Ko).view(S, N, Ko.shape[1])
+    J[0] += bo
+    return J, ("layered", X, P, net, spec, Hs)
+
+
+@torch.no_grad()
+def backward_raw(saved, dJ, grad=None):
+    """Flat parameter gradient of ``<dJ, J>`` (Keras layer order, like the fused kernels)."""
+    _, X, P, net, spec, Hs = saved
+    if grad is None:
+        grad = torch.empty_like(P)
+    gw = net.weights(grad)
+    ws = net.weights(P)
+    S, N = dJ.shape[0], dJ.shape[1]
+    dJ = dJ.contiguous()
+    Ko, _ = ws[-1]
+    Hl = Hs[-1]
+    dJf = dJ.view(S * N, dJ.shape[2])
+    torch.mm(Hl.view(S * N, Hl.shape[2]).t(), dJf, out=gw[-1][0])
+    torch.sum(dJ[0], dim=0, out=gw[-1][1])
+    HB = torch.mm(dJf, Ko.t()).view(S, N, Ko.shape[0])
+    for i in range(len(ws) - 2, 0, -1):
+        K, _ = ws[i]
+        ZB = _epi(False, HB, Hs[i], None, spec)
+        Hp = Hs[i - 1]
+        ZBf = ZB.view(S * N, ZB.shape[2])
+        torch.mm(Hp.view(S * N, Hp.shape[2]).t(), ZBf, out=gw[i][0])
+        torch.sum(ZB[0], dim=0, out=gw[i][1])
+        HB = torch.mm(ZBf, K.t()).view(S, N, K.shape[0])
+    ZB0 = _epi(False, HB, Hs[0], None, spec)
+    dK0, db0 = gw[0]
+    torch.mm(X.t(), ZB0[0], out=dK0)
+    for s in range(1, S):
+        if spec[3 * s] == 1:
+            dK0[spec[3 * s + 1]] += ZB0[s].sum(dim=0)
+    torch.sum(ZB0[0], dim=0, out=db0)
+    return grad

@@ -72,18 +72,18 @@ def hip_config(net, plan, precision=None):
     uniform = len(set(hidden)) == 1
     wpad = _pad16(max(hidden))
     WT = wpad // 16
-    if WT not in (1, 2, 4, 8):
-        if WT == 3:
-            WT = 4
-        elif WT in (5, 6, 7):
-            WT = 8
-        else:
-            raise ValueError("hidden width > 128")
-    if d_in > 8 or d_out > 4:
-        raise ValueError("input width > 8 or output width > 4")
     precision = precision or _precision
     if precision not in PRECISIONS:
         raise ValueError(f"precision {precision!r} not in {PRECISIONS}")
+    if WT > 8:
+        # beyond the fused kernels' register envelope: the layer-wise engine (library GEMMs on the
+        # stacked streams + fused HIP tanh-jet epilogues, ops/jet_layered.py), fp32 throughout
+        return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
+                "n_hidden": len(hidden), "precision": "fp32", "engine": "layered"}
+    if WT not in (1, 2, 4, 8):
+        WT = 4 if WT == 3 else 8
+    if d_in > 8 or d_out > 4:
+        raise ValueError("input width > 8 or output width > 4")
     if precision in ("bf16x3", "bf16") and WT < 2:
         precision = "fp32"
     # split-bf16 kernels: any S <= 8 at every width class (S x WT > 32: the one-wave-per-SIMD
