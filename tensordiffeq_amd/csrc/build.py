@@ -114,7 +114,8 @@ def build(force=False, jobs=None, verbose=True, variant=None, defines=()):
     if rebuilt or force or not os.path.exists(out) or any(
             os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         tmp = out + ".tmp"
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        # hipRTC: the specialized fused-loss kernels are compiled at run time (csrc/loss_jit.hip)
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lhiprtc"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

@@ -317,6 +317,14 @@ int tdq_loss_fused(const int* code, const float* consts, const void* outs, const
   return loss_reduce(partials, n_blocks, n_terms, n_scal, losses, total, dscal, with_total, stream);
 }
 
+// the per-term / scalar-gradient reduction alone (after a specialized loss kernel, ops/loss_jit.py)
+int tdq_loss_reduce_partials(const float* partials, int n_blocks, int n_terms, int n_scal, float* losses,
+                             float* total, float* dscal, int with_total, void* stream) {
+  if (n_blocks < 1 || n_terms < 0 || n_terms > LF_MAX_TERMS || n_scal < 0 || n_scal > LF_MAX_SCAL)
+    return (int)hipErrorInvalidValue;
+  return loss_reduce(partials, n_blocks, n_terms, n_scal, losses, total, dscal, with_total, stream);
+}
+
 int tdq_loss_meta_sizes(int* out) {
   out[0] = (int)sizeof(LFMeta);
   out[1] = (int)sizeof(LFPtrs);

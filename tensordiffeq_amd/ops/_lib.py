@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lock = threading.Lock()
 _lib = None
@@ -59,6 +59,7 @@ def _declare(lib):
         "tdq_loss_fused": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P, P, I, I, P]),
         "tdq_loss_fused_range": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, I, I, P]),
         "tdq_loss_meta_sizes": (I, [P]),
+        "tdq_loss_reduce_partials": (I, [P, I, I, I, P, P, P, I, P]),
         "tdq_lbfgs_nst": (I, []),
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
@@ -72,6 +73,12 @@ def _declare(lib):
         "tdq_peer_ipc_open": (I, [P, P]),
         "tdq_peer_ipc_close": (I, [P]),
         "tdq_peer_allreduce": (I, [P, I, I, I, L, I, P, P, P, P, L, P]),
+        # run-time specialized fused-loss kernels (csrc/loss_jit.hip, ops/loss_jit.py)
+        "tdq_rtc_compile": (I, [c.c_char_p, c.c_char_p, c.c_char_p, P, P, c.c_char_p, I]),
+        "tdq_rtc_free": (None, [P]),
+        "tdq_rtc_load": (I, [P, c.c_char_p, P, P]),
+        "tdq_rtc_unload": (I, [P]),
+        "tdq_loss_jit_range": (I, [P, P, P, P, P, P, I, I, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

@@ -28,6 +28,7 @@ class FusedLossOp:
             raise ValueError("fused loss program exceeds kernel table limits")
         self.fl, self.prog = fl, prog
         code, consts, outs, groups = [], [], [], []
+        self.group_meta = []   # (block_off, phase, n, seg_off, n_slots, loaded) per group (ops/loss_jit.py)
         spans = []
         block_off = 0
         self.max_regs = 1
@@ -44,6 +45,7 @@ class FusedLossOp:
             phase = offs[0] % LF_BLOCK if len(offs) == 1 else 0
             groups.append([len(code), len(P.code), len(consts), P.n_regs, gr.n, block_off, len(outs),
                            len(P.outputs), len(gr.segs)] + seg_off + loaded + [phase])
+            self.group_meta.append((block_off, phase, gr.n, list(seg_off), len(gr.segs), list(loaded)))
             code += P.code
             consts += P.consts
             outs += P.outputs
@@ -102,6 +104,13 @@ class FusedLossOp:
         self.losses = torch.zeros(self.n_terms, device=dev)
         self.total = torch.zeros((), device=dev)
         self.dscal = torch.zeros(max(1, self.n_scal), device=dev)
+        # the program compiled to a specialized kernel (hipRTC), or None: the interpreter
+        from . import loss_jit
+        self.jit = loss_jit.compile_for(self)
+
+    @property
+    def engine(self):
+        return "jit" if self.jit is not None else "interpreter"
 
     def __call__(self, J, with_total=True, reduce=True):
         """Run the program on jets ``J``.  ``with_total=False`` skips the total-loss launch (the Adam
@@ -110,6 +119,15 @@ class FusedLossOp:
         per-term losses and scalar gradients are reduced by the fused step tail
         (``jet_hip.step_tail`` / ``jet_hip.dp_tail_a``)."""
         lib = _lib.load()
+        if self.jit is not None:
+            st = _lib.stream_ptr(J.device)
+            self.jit.launch(J, self.prog.X_all, self.dJ, self.partials, self.ptrs, 0, self.n_blocks, st)
+            if reduce:
+                rc = lib.tdq_loss_reduce_partials(_lib.ptr(self.partials), self.n_blocks, self.n_terms, self.n_scal,
+                                                  _lib.ptr(self.losses), _lib.ptr(self.total), _lib.ptr(self.dscal),
+                                                  int(bool(with_total)), st)
+                _lib.check(rc, "tdq_loss_reduce_partials")
+            return self.total, self.losses, self.dJ, self.dlam, self.dscal
         rc = lib.tdq_loss_fused(_lib.ptr(self.code), _lib.ptr(self.consts), _lib.ptr(self.outs),
                                 _lib.ptr(self.groups), _lib.ptr(self.ptrs), self.n_groups, self.n_terms,
                                 self.n_scal, self.fl.n_streams, self.prog.d_in, self.N, _lib.ptr(J),
@@ -137,6 +155,10 @@ class FusedLossOp:
         """Blocks ``[blk0, blk0 + nblk)`` only (dJ / dlam / block partials of their points; the
         fused step tail reduces the partials), on the current stream."""
         lib = _lib.load()
+        if self.jit is not None:
+            self.jit.launch(J, self.prog.X_all, self.dJ, self.partials, self.ptrs, blk0, nblk,
+                            _lib.stream_ptr(J.device))
+            return
         rc = lib.tdq_loss_fused_range(_lib.ptr(self.code), _lib.ptr(self.consts), _lib.ptr(self.outs),
                                       _lib.ptr(self.groups), _lib.ptr(self.ptrs), self.n_groups, self.n_terms,
                                       self.n_scal, self.fl.n_streams, self.prog.d_in, self.N, _lib.ptr(J),
