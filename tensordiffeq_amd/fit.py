@@ -547,7 +547,7 @@ def point_ranges(program, fop):
     two streams, the loss and backward of one range fill the slots the forward of the other
     leaves idle (MI355X, AC-SA 50k: bf16 Adam step 0.211 -> 0.200 ms, bf16x3 0.446 -> 0.411 ms,
     bf16x3 L-BFGS iteration 0.51 -> 0.48 ms; profiles/r3_l_split_sweep.jsonl).  ``TDQ_SPLIT``:
-    ``auto`` (default: cut at 0.45 for bf16, 0.35 for bf16x3, the sweep's best), ``0`` / ``off``,
+    ``auto`` (default: cut at 0.38 for bf16, 0.35 for bf16x3, the sweeps' best), ``0`` / ``off``,
     or the cut fraction.  Cuts land on multiples of 128 points that also cut the fused loss's blocks
     cleanly (:meth:`FusedLossOp.split_block`); results are bitwise those of single launches (every
     workgroup / block keeps its index and buffers)."""
@@ -562,7 +562,9 @@ def point_ranges(program, fop):
     if cfg["precision"] not in ("bf16x3", "bf16") or cfg.get("engine") == "layered":
         return None
     if spec == "auto":
-        fracs = [0.35] if cfg["precision"] == "bf16x3" else [0.45]
+        # sweeps on MI355X with the specialized loss kernel: bf16 0.38 (0.2018 ms vs 0.2035 at 0.45,
+        # 3 passes, profiles/r3_yz_split_sweep_jit.jsonl), bf16x3 0.30-0.40 equal within noise
+        fracs = [0.35] if cfg["precision"] == "bf16x3" else [0.38]
     else:
         fracs = sorted(float(v) for v in spec.split(","))
     if len(fracs) > 1:
