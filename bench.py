@@ -193,6 +193,9 @@ def main(argv=None):
     ap.add_argument("--global-npts", type=int, default=None,
                     help="total collocation points, split over the GPUs (strong scaling)")
     ap.add_argument("--backend", default="auto")
+    ap.add_argument("--layers", default="2,128,128,128,128,1",
+                    help="network layer sizes (default: the AC-SA net of BASELINE.json; widths > 128 run the "
+                         "layer-wise engine)")
     ap.add_argument("--no-l2", action="store_true", help="skip the accuracy runs")
     ap.add_argument("--acc-seeds", type=int, nargs="*", default=[0, 1, 2],
                     help="seeds of the full-schedule accuracy runs (single GPU only)")
@@ -222,7 +225,8 @@ def main(argv=None):
 
     strong = args.global_npts is not None
     n_glob = args.global_npts if strong else args.npts * world
-    model = build_problem(n_glob, world, args.backend, device, dist, args.precision)
+    layers = tuple(int(v) for v in args.layers.split(","))
+    model = build_problem(n_glob, world, args.backend, device, dist, args.precision, layers=layers)
     eng = model._get_engine(None, args.warmup + args.steps + 2)
     backend = model.active_backend
     elapsed, n_warm, warm_s = time_steps(eng, ctx, device, args.steps, args.warmup, args.min_warmup_s)
@@ -261,7 +265,7 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16" if (backend == "hip" and args.precision != "fp32") else "fp32",
             "data": "synthetic (LHS collocation points, random Keras-init weights); L2 on data/AC.mat",
-            "config": {"model": "Allen-Cahn SA-PINN tanh MLP [2,128,128,128,128,1]",
+            "config": {"model": f"Allen-Cahn SA-PINN tanh MLP [{','.join(map(str, layers))}]",
                        "global_batch": n_glob, "seq_len": None, "parallelism": f"dp{world}",
                        "points_per_gpu": n_glob // world, "backend": backend,
                        "precision": PRECISION_NOTES[args.precision] if backend == "hip" else "fp32",

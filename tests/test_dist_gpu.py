@@ -33,7 +33,8 @@ def _build(dist, world=1, precision=None, n_f=N_F):
 
 def _worker(rank, world, port, q, precision, peer="0"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE=peer)
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE=peer,
+                      TDQ_STEP_UNROLL="4")
     from tensordiffeq_amd.parallel import dist as pdist
     pdist.reset_context()
     ctx = pdist.init_distributed(backend="gloo", device="cuda:0")
@@ -49,6 +50,7 @@ def _worker(rank, world, port, q, precision, peer="0"):
     res["hist"] = [h["Total Loss"] for h in m.losses]
     res["peer"] = ctx.peer is not None
     res["one_graph"] = m._get_engine(None, 1).graph_b is None
+    res["k_graph"] = getattr(m._get_engine(None, 1), "graph_k", None) is not None
     res["flat_after"] = m.u_model.flat.detach().cpu().numpy().copy()
     m.fit(newton_iter=3)
     res["lbfgs_loss"] = float(m.min_loss["l-bfgs"])
@@ -83,7 +85,8 @@ def test_dp_two_ranks_on_gpu_match_single_process(precision, peer):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert res["peer"] == (peer == "1") and res["one_graph"] == (peer == "1")
+    # peer: the all-reduce is a graph node, so 4-step graphs run too (TDQ_STEP_UNROLL=4, 8 steps)
+    assert res["peer"] == (peer == "1") and res["one_graph"] == (peer == "1") and res["k_graph"] == (peer == "1")
     assert res["loss"] == pytest.approx(loss, rel=1e-4)
     gflat, flat_after = torch.from_numpy(res["gflat"]), torch.from_numpy(res["flat_after"])
     assert ((gflat - g_ref).norm() / g_ref.norm()).item() < 1e-3
