@@ -105,9 +105,10 @@ __global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restri
                                                            int nwg, int Pst, int chunks, int nqb, int half, TailBook tb) {
   if ((int)blockIdx.x < nqb) {
     const int q = blockIdx.x * 256 + threadIdx.x;
-    if (4 * q < Pst) {
-      if (half) slab_reduce1_body<true>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
-      else slab_reduce1_body<false>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+    if (half) {  // bf16 slabs: 8 columns per thread, 16-byte loads (nqb counts 8-column groups)
+      if (8 * q < Pst) slab_reduce1_body8(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+    } else if (4 * q < Pst) {
+      slab_reduce1_body<false>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
     }
     return;
   }
@@ -536,9 +537,10 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   tb.improved = improved;
   tb.cnt.n = ncnt;
   for (int i = 0; i < TDQ_MAX_COUNTERS; ++i) tb.cnt.c[i] = i < ncnt ? counters[i] : nullptr;
-  const int nqb = (Pst / 4 + 255) / 256;
+  const int half = (int)slab_half(lo != 0);
+  const int nqb = (Pst / (half ? 8 : 4) + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
-                     nqb, (int)slab_half(lo != 0), tb);
+                     nqb, half, tb);
   TDQ_CHECK_LAUNCH();
   TailImg ti{nullptr, nullptr, nullptr, d, WT};
   if (scratch != nullptr) {
@@ -582,11 +584,12 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
   tb.losses = losses;
   tb.dscal = dscal;
   tb.total = total;
-  const int nqb = (Pst / 4 + 255) / 256;
+  const int half = (int)slab_half(lo != 0);
+  const int nqb = (Pst / (half ? 8 : 4) + 255) / 256, nq2 = (Pst / 4 + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
-                     nqb, (int)slab_half(lo != 0), tb);
+                     nqb, half, tb);
   TDQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nqb), dim3(256), 0, st, part, grad, Ptot, Pst, chunks);
+  hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nq2), dim3(256), 0, st, part, grad, Ptot, Pst, chunks);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

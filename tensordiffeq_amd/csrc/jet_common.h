@@ -123,9 +123,10 @@ static inline int spec_nso(int S, const int* spec) {
   return nso;
 }
 
-// per-workgroup gradient slab row stride: parameter count rounded up to 4 floats, so every slab
-// row is 16-byte aligned for the float4 reduction
-static inline int slab_stride(int P) { return (P + 3) & ~3; }
+// per-workgroup gradient slab row stride: parameter count rounded up to 8 entries, so every slab
+// row is 16-byte aligned for the float4 reduction of fp32 slabs and for the 16-byte (8 x bf16)
+// loads of the bf16 slab reduction (slab_reduce1_body8)
+static inline int slab_stride(int P) { return (P + 7) & ~7; }
 
 // workgroup-chunk count of the first reduction pass (-DTDQ_SLAB_CHUNKS for A/B runs)
 #ifndef TDQ_SLAB_CHUNKS
@@ -162,6 +163,51 @@ __device__ __forceinline__ void slab_reduce1_body(const void* __restrict__ slab,
   }
   for (; wgi < hi; ++wgi) a0 += slab_ld4<H>(slab, wgi, Pst, q);
   reinterpret_cast<f32x4*>(part)[(size_t)c * row + q] = (a0 + a1) + (a2 + a3);
+}
+
+// the same first pass over bf16 slab rows with 16-byte loads: 8 columns (float4 columns 2 q8 and
+// 2 q8 + 1) per thread, 8 rows in flight.  Every column is summed in slab_reduce1_body's order
+// (rows round-robin into four accumulators, the remainder into the first, then (a0 + a1) + (a2 + a3)),
+// so the partials are bit-identical; 8-byte loads ran at 0.54-0.70x the 16-byte rate (guide).
+__device__ __forceinline__ void bf8_add(f32x4& lo, f32x4& hi, const uint4 u) {
+  lo += f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+              __uint_as_float(u.y & 0xffff0000u)};
+  hi += f32x4{__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+              __uint_as_float(u.w & 0xffff0000u)};
+}
+__device__ __forceinline__ void slab_reduce1_body8(const void* __restrict__ slab, float* __restrict__ part, int nwg,
+                                                   int Pst, int chunks, int q8, int c) {
+  const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
+  const uint4* s8 = reinterpret_cast<const uint4*>(slab) + q8;  // row stride Pst / 8 uint4
+  const size_t rs = (size_t)(Pst >> 3);
+  f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();
+  f32x4 b0 = zero4(), b1 = zero4(), b2 = zero4(), b3 = zero4();
+  int w = lo;
+  for (; w + 7 < hi; w += 8) {
+    uint4 u[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = s8[(size_t)(w + k) * rs];
+    bf8_add(a0, b0, u[0]);
+    bf8_add(a1, b1, u[1]);
+    bf8_add(a2, b2, u[2]);
+    bf8_add(a3, b3, u[3]);
+    bf8_add(a0, b0, u[4]);
+    bf8_add(a1, b1, u[5]);
+    bf8_add(a2, b2, u[6]);
+    bf8_add(a3, b3, u[7]);
+  }
+  for (; w + 3 < hi; w += 4) {
+    const uint4 u0 = s8[(size_t)w * rs], u1 = s8[(size_t)(w + 1) * rs], u2 = s8[(size_t)(w + 2) * rs],
+                u3 = s8[(size_t)(w + 3) * rs];
+    bf8_add(a0, b0, u0);
+    bf8_add(a1, b1, u1);
+    bf8_add(a2, b2, u2);
+    bf8_add(a3, b3, u3);
+  }
+  for (; w < hi; ++w) bf8_add(a0, b0, s8[(size_t)w * rs]);
+  f32x4* p4 = reinterpret_cast<f32x4*>(part) + (size_t)c * (size_t)(Pst >> 2) + 2 * q8;
+  p4[0] = (a0 + a1) + (a2 + a3);
+  p4[1] = (b0 + b1) + (b2 + b3);
 }
 
 // second pass: the gradient of float4 column q (fixed summation order: deterministic)

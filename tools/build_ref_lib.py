@@ -47,7 +47,8 @@ def main():
     with cf.ThreadPoolExecutor(8) as ex:
         objs = list(ex.map(comp, sorted(glob.glob(os.path.join(src, "*.hip")))))
     lib = os.path.join(out, "libtdq_hip.so")
-    subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", lib] + objs, check=True)
+    subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lhiprtc"],
+                   check=True)
     for o in objs:
         os.remove(o)
     shutil.rmtree(src)
