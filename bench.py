@@ -121,7 +121,10 @@ def time_steps(eng, ctx, device, steps, warmup, min_warmup_s):
     eng.run(max(1, warmup))
     n_warm = max(1, warmup)
     sync()
-    while time.perf_counter() - t_w < min_warmup_s:
+    # the stop decision is collective (max over ranks): a rank-local clock would let ranks run
+    # different numbers of warm-up steps, i.e. different numbers of all-reduces, and the DP step of
+    # the rank with the extra steps would wait for peers that never arrive
+    while ctx.max_scalar(time.perf_counter() - t_w) < min_warmup_s:
         eng.run(max(10, warmup))
         n_warm += max(10, warmup)
         sync()
@@ -225,6 +228,12 @@ def main(argv=None):
 
     strong = args.global_npts is not None
     n_glob = args.global_npts if strong else args.npts * world
+    if "TDQ_STEP_UNROLL" not in os.environ:
+        # steps per captured graph: a divisor of --steps, so the timed steps are all multi-step graph
+        # replays (a 1-step replay leaves ~9 us idle between graphs; 8 and 16 per graph measured
+        # equal, profiles/r3_m_unroll_ab.jsonl)
+        divs = [k for k in range(16, 3, -1) if args.steps % k == 0]
+        os.environ["TDQ_STEP_UNROLL"] = str(8 if args.steps % 8 == 0 else (divs[0] if divs else 8))
     layers = tuple(int(v) for v in args.layers.split(","))
     model = build_problem(n_glob, world, args.backend, device, dist, args.precision, layers=layers)
     eng = model._get_engine(None, args.warmup + args.steps + 2)

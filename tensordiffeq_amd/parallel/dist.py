@@ -135,7 +135,9 @@ def init_distributed(backend=None, device=None, timeout_s=600, force=None):
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if backend is None:
-        backend = "nccl" if device.type == "cuda" else "gloo"
+        # TDQ_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks sharing one GPU
+        # (RCCL refuses two ranks on one device); the peer all-reduce then carries the bucket
+        backend = os.environ.get("TDQ_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
     initialized = False
     if world > 1 or force:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

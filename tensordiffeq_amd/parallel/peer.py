@@ -117,6 +117,12 @@ class PeerComm:
             self._base = ctypes.c_void_p(0)
 
 
+def _log(msg):
+    if os.environ.get("TDQ_PEER_DEBUG", "0") == "1":
+        import sys
+        print(f"[peer rank {os.environ.get('RANK', '?')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _gather(obj, world):
     out = [None] * world
     dist.all_gather_object(out, obj)
@@ -158,6 +164,7 @@ def setup(ctx, bench_floats=49_408):
     if m == "0" or ctx.device.type != "cuda" or ctx.world < 2 or not _lib.available():
         return None
     W = ctx.world
+    _log("setup: gathering hosts")
     hosts = _gather(socket.gethostname(), W)
     if len(set(hosts)) != 1:
         info["peer"] = "off: ranks on more than one host"
@@ -168,6 +175,7 @@ def setup(ctx, bench_floats=49_408):
         h = comm.handle()
     except Exception as e:  # noqa: BLE001 - reported, every rank falls back together
         h, err = None, f"{type(e).__name__}: {e}"
+    _log(f"setup: allocated ({err or 'ok'}), gathering handles")
     handles = _gather(h, W)
     if any(x is None for x in handles):
         info["peer"] = f"off: setup failed ({err or 'on another rank'})"
@@ -179,6 +187,7 @@ def setup(ctx, bench_floats=49_408):
         ok = True
     except Exception as e:  # noqa: BLE001
         ok, err = False, f"{type(e).__name__}: {e}"
+    _log(f"setup: peers opened ({ok})")
     oks = _gather(ok, W)
     if not all(oks):
         info["peer"] = f"off: IPC open failed ({err or 'on another rank'})"
@@ -188,6 +197,7 @@ def setup(ctx, bench_floats=49_408):
         ok = _self_test(comm, min(comm.cap, bench_floats + 777))
     except Exception as e:  # noqa: BLE001
         ok, err = False, f"{type(e).__name__}: {e}"
+    _log(f"setup: self-test {ok} err={err}")
     oks = _gather(ok, W)
     info["memory"] = _KINDS.get(comm.kind, "?")
     if not all(oks):
@@ -196,10 +206,12 @@ def setup(ctx, bench_floats=49_408):
         return None
     buf = torch.randn(bench_floats, device=ctx.device)
     t_peer = _time_us(comm.all_reduce_, buf)
+    _log(f"setup: peer {t_peer:.1f} us")
     if m == "auto":
         t_ref = _time_us(lambda b: dist.all_reduce(b, op=dist.ReduceOp.SUM), buf)
     else:
         t_ref = float("nan")
+    _log(f"setup: torch.distributed {t_ref:.1f} us")
     ts = _gather([t_peer, t_ref], W)
     t_peer = max(x[0] for x in ts)
     t_ref = max(x[1] for x in ts)
