@@ -69,7 +69,7 @@ def forward_raw(X, P, net, plan, precision=None, pack=True):
     cfg = hip_config(net, plan, precision)
     if is_layered(cfg):
         from . import jet_layered
-        return jet_layered.forward_raw(X.contiguous(), P, net, plan)
+        return jet_layered.forward_raw(X.contiguous(), P, net, plan, cfg["precision"])
     fwd, _, scratch_floats, _ = _fns(lib, cfg)
     X = X.contiguous()
     N = X.shape[0]
@@ -235,7 +235,8 @@ class JetMLPFunction(torch.autograd.Function):
         if ctx.layered is not None:
             saved = ctx.layered
             if dJ is None:
-                dJ = torch.zeros((len(saved[5]), saved[1].shape[0], saved[3].layer_sizes[-1]), device=saved[1].device)
+                dJ = torch.zeros((len(saved[4]) // 3, saved[1].shape[0], saved[3].layer_sizes[-1]),
+                                 device=saved[1].device)
             return None, backward_raw(saved, dJ), None, None, None
         X, P, scratch = ctx.saved_tensors
         cfg, spec, S = ctx.meta

@@ -7,7 +7,9 @@ whole layer stack, which bounds the hidden width at 128.  The reference accepts 
 * the S derivative streams of a layer are stacked into one ``[S*N, W]`` matrix, so every weight
   multiplication of a layer - forward ``Z = H K``, backward ``HB = ZB K^T`` and the weight gradient
   ``dK = H^T ZB`` (reduction over all streams and points at once) - is ONE plain library GEMM
-  (hipBLASLt via ``torch.mm``, fp32);
+  (hipBLASLt via ``torch.mm``) in the requested precision family: fp32, bf16 (operands rounded
+  once, fp32 output) or bf16x3 (hi/lo split, three bf16 GEMMs: hi*hi + hi*lo + lo*hi); every
+  activation / adjoint is converted once and reused by both GEMMs that read it;
 * the bias, the tanh jet (value, first-, second-order streams) and its adjoint run as one fused,
   memory-bound HIP pass per layer (``tdq_layered_epi``), the adjoint from the saved
   post-activations only (no tanh recompute).
@@ -66,6 +68,74 @@ def _epi_bwd_torch(HB, H, spec):
     return HB
 
 
+class _Op:
+    """A GEMM operand in the engine's precision: fp32 as is; ``bf16`` one rounded copy; ``bf16x3``
+    a (hi, lo) split (products hi*hi + hi*lo + lo*hi, fp32 accumulation - the fused kernels'
+    precision families).  Built once per activation / adjoint and reused by every GEMM reading it."""
+
+    def __init__(self, x, prec):
+        self.prec = prec
+        if prec == "fp32" or not x.is_cuda:
+            self.f = x
+        else:
+            self.h = x.to(torch.bfloat16)
+            if prec == "bf16x3":
+                self.l = (x - self.h.float()).to(torch.bfloat16)
+
+    def t(self):
+        o = _Op.__new__(_Op)
+        o.prec = self.prec
+        for k in ("f", "h", "l"):
+            if hasattr(self, k):
+                setattr(o, k, getattr(self, k).t())
+        return o
+
+
+def _mm(a, b, out=None):
+    """a @ b for two :class:`_Op` of the same precision (library GEMMs, fp32 output)."""
+    if hasattr(a, "f"):
+        return torch.mm(a.f, b.f, out=out)
+    f32 = torch.float32
+    r = torch.mm(a.h, b.h, out_dtype=f32)
+    if a.prec == "bf16x3":
+        r += torch.mm(a.h, b.l, out_dtype=f32)
+        r += torch.mm(a.l, b.h, out_dtype=f32)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def _mm_tn(a, b, out):
+    """out = a^T b for :class:`_Op` a [L, M], b [L, N] with a long reduction L = S*N (the weight
+    gradient): as ONE library GEMM its M x N = W x W output is only a few tiles, so a handful of CUs
+    did all the work (bf16 ~50 TF/s, profiles/r3_ag_*).  The reduction is split into C chunks run as
+    one batched GEMM ([C, M, L/C] x [C, L/C, N]) and the C partial products summed in fixed order."""
+    L = (a.f if hasattr(a, "f") else a.h).shape[0]
+    C = 64 if L >= 64 * 1024 else max(1, L // 1024)
+    L0 = L - L % C
+
+    def chunks(x):
+        return x[:L0].view(C, L0 // C, x.shape[1])
+
+    def bmm(x, y):
+        if x.dtype != torch.bfloat16:
+            return torch.bmm(chunks(x).transpose(1, 2), chunks(y))
+        return torch.bmm(chunks(x).transpose(1, 2), chunks(y), out_dtype=torch.float32)
+
+    pairs = [(a.f, b.f)] if hasattr(a, "f") else [(a.h, b.h)] + ([(a.h, b.l), (a.l, b.h)] if a.prec == "bf16x3" else [])
+    r = None
+    for x, y in pairs:
+        p = bmm(x, y).sum(0)
+        if L0 < L:
+            xt, yt = x[L0:], y[L0:]
+            p += (torch.mm(xt.t(), yt) if x.dtype != torch.bfloat16 else
+                  torch.mm(xt.t(), yt, out_dtype=torch.float32))
+        r = p if r is None else r + p
+    out.copy_(r)
+    return out
+
+
 def _epi(fwd, A, B, bias, spec):
     S, N, W = A.shape
     if A.is_cuda:
@@ -79,8 +149,9 @@ def _epi(fwd, A, B, bias, spec):
 
 
 @torch.no_grad()
-def forward_raw(X, P, net, plan):
-    """``(J, saved)``; ``saved`` feeds :func:`backward_raw`."""
+def forward_raw(X, P, net, plan, precision="fp32"):
+    """``(J, saved)``; ``saved`` feeds :func:`backward_raw`.  ``precision`` of the hidden and output
+    GEMMs: ``fp32``, ``bf16`` or ``bf16x3`` (the input layer is exact fp32 in every mode)."""
     spec = _spec(plan)
     ws = net.weights(P)
     S, N = plan.S, X.shape[0]
@@ -92,21 +163,24 @@ def forward_raw(X, P, net, plan):
         if spec[3 * s] == 1:
             Z[s].copy_(K0[spec[3 * s + 1]].expand(N, W0))
     Hs = [_epi(True, Z, None, b0, spec)]
+    Ho = []                                          # GEMM operands of the saved activations
     for K, b in ws[1:-1]:
         Hp = Hs[-1]
-        Z = torch.mm(Hp.view(S * N, Hp.shape[2]), K).view(S, N, K.shape[1])
+        Ho.append(_Op(Hp.view(S * N, Hp.shape[2]), precision))
+        Z = _mm(Ho[-1], _Op(K, precision)).view(S, N, K.shape[1])
         Hs.append(_epi(True, Z, None, b, spec))
     Ko, bo = ws[-1]
     Hl = Hs[-1]
-    J = torch.mm(Hl.view(S * N, Hl.shape[2]), Ko).view(S, N, Ko.shape[1])
+    Ho.append(_Op(Hl.view(S * N, Hl.shape[2]), precision))
+    J = _mm(Ho[-1], _Op(Ko, precision)).view(S, N, Ko.shape[1])
     J[0] += bo
-    return J, ("layered", X, P, net, spec, Hs)
+    return J, ("layered", X, P, net, spec, Hs, Ho, precision)
 
 
 @torch.no_grad()
 def backward_raw(saved, dJ, grad=None):
     """Flat parameter gradient of ``<dJ, J>`` (Keras layer order, like the fused kernels)."""
-    _, X, P, net, spec, Hs = saved
+    _, X, P, net, spec, Hs, Ho, prec = saved
     if grad is None:
         grad = torch.empty_like(P)
     gw = net.weights(grad)
@@ -114,19 +188,22 @@ def backward_raw(saved, dJ, grad=None):
     S, N = dJ.shape[0], dJ.shape[1]
     dJ = dJ.contiguous()
     Ko, _ = ws[-1]
-    Hl = Hs[-1]
-    dJf = dJ.view(S * N, dJ.shape[2])
-    torch.mm(Hl.view(S * N, Hl.shape[2]).t(), dJf, out=gw[-1][0])
+    dJo = _Op(dJ.view(S * N, dJ.shape[2]), prec)
+    _mm_tn(Ho[-1], dJo, gw[-1][0])
     torch.sum(dJ[0], dim=0, out=gw[-1][1])
-    HB = torch.mm(dJf, Ko.t()).view(S, N, Ko.shape[0])
+    if dJ.shape[2] == 1:  # an outer product: a K = 1 GEMM ran 10x slower than this broadcast
+        HB = (dJ.view(S * N, 1) * Ko.view(1, -1)).view(S, N, Ko.shape[0])
+    else:
+        HB = _mm(dJo, _Op(Ko.t().contiguous(), prec)).view(S, N, Ko.shape[0])
     for i in range(len(ws) - 2, 0, -1):
         K, _ = ws[i]
         ZB = _epi(False, HB, Hs[i], None, spec)
-        Hp = Hs[i - 1]
-        ZBf = ZB.view(S * N, ZB.shape[2])
-        torch.mm(Hp.view(S * N, Hp.shape[2]).t(), ZBf, out=gw[i][0])
+        ZBo = _Op(ZB.view(S * N, ZB.shape[2]), prec)
+        _mm_tn(Ho[i - 1], ZBo, gw[i][0])
         torch.sum(ZB[0], dim=0, out=gw[i][1])
-        HB = torch.mm(ZBf, K.t()).view(S, N, K.shape[0])
+        # K^T materialized (W x W): the library's transposed-B kernels for this shape ran ~4x slower
+        # than its row-major ones (rocprofv3, profiles/r3_ag_*)
+        HB = _mm(ZBo, _Op(K.t().contiguous(), prec)).view(S, N, K.shape[0])
     ZB0 = _epi(False, HB, Hs[0], None, spec)
     dK0, db0 = gw[0]
     torch.mm(X.t(), ZB0[0], out=dK0)

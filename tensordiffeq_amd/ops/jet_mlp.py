@@ -77,9 +77,10 @@ def hip_config(net, plan, precision=None):
         raise ValueError(f"precision {precision!r} not in {PRECISIONS}")
     if WT > 8:
         # beyond the fused kernels' register envelope: the layer-wise engine (library GEMMs on the
-        # stacked streams + fused HIP tanh-jet epilogues, ops/jet_layered.py), fp32 throughout
+        # stacked streams in the requested precision family + fused HIP tanh-jet epilogues,
+        # ops/jet_layered.py)
         return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
-                "n_hidden": len(hidden), "precision": "fp32", "engine": "layered"}
+                "n_hidden": len(hidden), "precision": precision, "engine": "layered"}
     if WT not in (1, 2, 4, 8):
         WT = 4 if WT == 3 else 8
     if d_in > 8 or d_out > 4:

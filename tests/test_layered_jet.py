@@ -4,6 +4,8 @@ CPU (float64, torch epilogues): forward streams and the flat parameter gradient 
 jet engine + autograd.  GPU (``-m gpu``): the HIP epilogues (csrc/jet_layered.hip) through the
 normal HIP dispatch for hidden widths > 128, against the float64 reference.
 """
+import math
+
 import pytest
 import torch
 
@@ -53,25 +55,31 @@ def test_layered_engine_cpu_float64(sizes, reqs, N):
     assert torch.allclose(g, gr, rtol=1e-9, atol=1e-11)
 
 
+# (forward, gradient) bounds per GEMM precision family: fp32 library GEMMs (error grows with the
+# reduction length: 3.5e-6 at width 256, 2.1e-5 at 512, gpurun_out r3u); bf16x3 / bf16 like the
+# fused kernels' families (tests/test_hip_kernels.py TOL_*)
+LTOL = {"fp32": (2e-5, 2e-5), "bf16x3": (2.5e-4, 2.5e-5), "bf16": (8e-2, 1.4e-2)}
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3", "bf16"])
 @pytest.mark.parametrize("sizes,reqs,N", GPU_CASES)
-def test_layered_engine_hip(sizes, reqs, N):
+def test_layered_engine_hip(sizes, reqs, N, prec):
     from tensordiffeq_amd.ops import jet_hip, jet_mlp
     net, X, plan = _setup(sizes, reqs, N, "cuda", torch.float32, seed=1)
-    cfg = jet_mlp.hip_config(net, plan, "bf16")
-    assert jet_hip.is_layered(cfg) and not jet_hip.is_split_bf16(cfg)
+    cfg = jet_mlp.hip_config(net, plan, prec)
+    assert jet_hip.is_layered(cfg) and not jet_hip.is_split_bf16(cfg) and cfg["precision"] == prec
     p = net.flat.detach().clone().requires_grad_(True)
-    J = jet_hip.JetMLPFunction.apply(X, p, net, plan, "bf16")
+    J = jet_hip.JetMLPFunction.apply(X, p, net, plan, prec)
     G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
     (J.double() * G).sum().backward()
     Jr, gr = _ref(net, X, plan, G)
     scale = Jr.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
     ferr = ((J.detach().double() - Jr).abs() / scale).max().item()
     rel = ((p.grad.double() - gr).norm() / gr.norm()).item()
-    print(f"KERNEL_ERR layered {sizes} S={plan.S} fwd {ferr:.3e} bwd {rel:.3e}")
-    # fp32 library GEMMs: forward error grows with the reduction length (measured 3.5e-6 at width
-    # 256, 2.1e-5 at 512; gpurun_out r3u)
-    assert ferr < 2e-5 * max(1, max(sizes[1:-1]) // 256) and rel < 2e-5, (ferr, rel)
+    print(f"KERNEL_ERR layered {prec} {sizes} S={plan.S} fwd {ferr:.3e} bwd {rel:.3e}")
+    tf, tb = LTOL[prec]
+    assert ferr < tf * max(1, max(sizes[1:-1]) // 256) and rel < tb, (ferr, rel)
 
 
 @pytest.mark.gpu
@@ -83,7 +91,7 @@ def test_layered_engine_trains_wide_solver():
     layers = (2, 256, 256, 256, 1)
     hist = {}
     for backend in ("auto", "jet"):
-        m = bench.build_problem(4096, 1, backend, torch.device("cuda", 0), False, "bf16", layers=layers)
+        m = bench.build_problem(4096, 1, backend, torch.device("cuda", 0), False, "fp32", layers=layers)
         if backend == "auto":
             assert m.active_backend == "hip"
             prog = m._get_engine(None, 10).program
@@ -93,3 +101,22 @@ def test_layered_engine_trains_wide_solver():
         hist[backend] = ([h["Total Loss"] for h in m.losses], float(m.min_loss["l-bfgs"]))
     assert hist["auto"][0] == pytest.approx(hist["jet"][0], rel=2e-4)
     assert hist["auto"][1] == pytest.approx(hist["jet"][1], rel=2e-3)
+
+
+@pytest.mark.gpu
+def test_layered_engine_trains_in_bf16_families():
+    """The wide solver in the bf16 GEMM families follows the fp32 layered trajectory (SA-PINN: the
+    total loss rises while the SA weights ascend, so closeness is the check, not descent); measured
+    relative differences after 30 Adam steps set the bounds at ~3x."""
+    import bench
+    hist = {}
+    for prec in ("fp32", "bf16x3", "bf16"):
+        m = bench.build_problem(4096, 1, "auto", torch.device("cuda", 0), False, prec, layers=(2, 256, 256, 256, 1))
+        assert m.active_backend == "hip"
+        m.fit(tf_iter=30)
+        hist[prec] = torch.tensor([x["Total Loss"] for x in m.losses], dtype=torch.float64)
+        assert torch.isfinite(hist[prec]).all()
+    for prec, tol in (("bf16x3", 1e-3), ("bf16", 5e-2)):
+        rel = ((hist[prec] - hist["fp32"]).abs() / hist["fp32"].abs()).max().item()
+        print(f"LAYERED_TRAJ {prec} max rel diff vs fp32 {rel:.3e}")
+        assert rel < tol, (prec, rel)

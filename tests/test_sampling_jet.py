@@ -107,13 +107,13 @@ def test_hip_config_unequal_widths():
 
 def test_hip_config_wide_hidden_layers_use_layered_engine():
     """Hidden widths > 128 leave the fused kernels' envelope: the layer-wise engine serves them
-    (library GEMMs + HIP epilogues, fp32), never the fused tail / point ranges."""
+    (library GEMMs in the requested precision + HIP epilogues), never the fused tail / point ranges."""
     from tensordiffeq_amd.jet import JetPlan
     from tensordiffeq_amd.models.networks import TanhMLP
     from tensordiffeq_amd.ops import jet_hip
     from tensordiffeq_amd.ops.jet_mlp import hip_config
     cfg = hip_config(TanhMLP([2, 256, 256, 1], device="cpu"), JetPlan([(0,), (1,), (0, 0)], 2), "bf16")
-    assert jet_hip.is_layered(cfg) and cfg["precision"] == "fp32" and not jet_hip.is_split_bf16(cfg)
+    assert jet_hip.is_layered(cfg) and cfg["precision"] == "bf16" and not jet_hip.is_split_bf16(cfg)
     cfg = hip_config(TanhMLP([2, 64, 200, 1], device="cpu"), JetPlan([(0, 0)], 2), "bf16x3")
     assert jet_hip.is_layered(cfg) and cfg["widths"] == (64, 200)
     assert not jet_hip.is_layered(hip_config(TanhMLP([2, 128, 1], device="cpu"), JetPlan([], 2), "bf16"))
