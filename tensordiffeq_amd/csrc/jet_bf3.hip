@@ -101,14 +101,17 @@ struct TailBook {
   Counters cnt;
 };
 
+// chunks [c0, c0 + gridDim.y) of the first pass; blocks x >= nqb (at most one, and only with
+// gridDim.x > nqb) run the loss reduction + bookkeeping
 __global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restrict__ slab, float* __restrict__ part,
-                                                           int nwg, int Pst, int chunks, int nqb, int half, TailBook tb) {
+                                                           int nwg, int Pst, int chunks, int nqb, int half, int c0,
+                                                           TailBook tb) {
   if ((int)blockIdx.x < nqb) {
-    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int q = blockIdx.x * 256 + threadIdx.x, c = c0 + (int)blockIdx.y;
     if (half) {  // bf16 slabs: 8 columns per thread, 16-byte loads (nqb counts 8-column groups)
-      if (8 * q < Pst) slab_reduce1_body8(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+      if (8 * q < Pst) slab_reduce1_body8(slab, part, nwg, Pst, chunks, q, c);
     } else if (4 * q < Pst) {
-      slab_reduce1_body<false>(slab, part, nwg, Pst, chunks, q, blockIdx.y);
+      slab_reduce1_body<false>(slab, part, nwg, Pst, chunks, q, c);
     }
     return;
   }
@@ -504,7 +507,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
                       int S, int lo, const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses,
                       float* total, float* dscal, float* hist, int64_t hist_rows, int64_t* epoch, float* best_loss,
                       int64_t* best_epoch, int* improved, double* const* counters, int ncnt, const void* groups,
-                      int ngroups, float* snap, void* stream) {
+                      int ngroups, float* snap, int c_first, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -520,6 +523,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
+  if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
   TailBook tb;
   tb.lpart = lpart;
@@ -539,8 +543,9 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   for (int i = 0; i < TDQ_MAX_COUNTERS; ++i) tb.cnt.c[i] = i < ncnt ? counters[i] : nullptr;
   const int half = (int)slab_half(lo != 0);
   const int nqb = (Pst / (half ? 8 : 4) + 255) / 256;
-  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
-                     nqb, half, tb);
+  // chunks [0, c_first) were pre-reduced (tdq_slab_prereduce_bf3) while the other range ran
+  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks - c_first), dim3(256), 0, st, work, part, nwg_b, Pst,
+                     chunks, nqb, half, c_first, tb);
   TDQ_CHECK_LAUNCH();
   TailImg ti{nullptr, nullptr, nullptr, d, WT};
   if (scratch != nullptr) {
@@ -565,7 +570,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
 // (optional): also the summed loss - the L-BFGS objective writes [grad | loss] in place this way.
 int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
-                      float* total, void* stream) {
+                      float* total, int c_first, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -575,6 +580,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
   const int Ptot = param_count(d);
   const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
+  if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
   TailBook tb{};
   tb.lpart = lpart;
@@ -586,10 +592,49 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
   tb.total = total;
   const int half = (int)slab_half(lo != 0);
   const int nqb = (Pst / (half ? 8 : 4) + 255) / 256, nq2 = (Pst / 4 + 255) / 256;
-  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks), dim3(256), 0, st, work, part, nwg_b, Pst, chunks,
-                     nqb, half, tb);
+  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks - c_first), dim3(256), 0, st, work, part, nwg_b, Pst,
+                     chunks, nqb, half, c_first, tb);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nq2), dim3(256), 0, st, part, grad, Ptot, Pst, chunks);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// Geometry of the backward's gradient slabs: out = [points per backward workgroup, slab rows (nwg),
+// first-pass chunks, 0].  fit.point_ranges places a range cut on a chunk boundary (slab_chunk_lo).
+int tdq_bf3_slab_geometry(int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo, int* out) {
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b, chunks = slab_chunks(nwg_b);
+  out[0] = pts_b;
+  out[1] = nwg_b;
+  out[2] = chunks;
+  out[3] = 0;
+  return 0;
+}
+
+// First-pass chunks [c0, c1) of the slab reduction alone (no bookkeeping): launched on the first
+// point range's stream right after its backward, so those rows are reduced while the second range's
+// backward still runs; tdq_step_tail_bf3(c_first = c1) reduces the rest.  Same kernel and partial
+// rows as the full pass: bit-identical.
+int tdq_slab_prereduce_bf3(float* work, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
+                           int c0, int c1, void* stream) {
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
+  const int Ptot = param_count(d);
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
+  const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
+  if (c0 < 0 || c1 > chunks || c1 <= c0) return (int)hipErrorInvalidValue;
+  float* part = work + (size_t)nwg_b * Pst;
+  const int half = (int)slab_half(lo != 0);
+  const int nqb = (Pst / (half ? 8 : 4) + 255) / 256;
+  TailBook tb{};
+  hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb, c1 - c0), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     work, part, nwg_b, Pst, chunks, nqb, half, c0, tb);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -133,6 +133,13 @@ static inline int slab_stride(int P) { return (P + 7) & ~7; }
 #define TDQ_SLAB_CHUNKS 8
 #endif
 static inline int slab_chunks(int nwg) { return nwg < TDQ_SLAB_CHUNKS ? nwg : TDQ_SLAB_CHUNKS; }
+// chunk c of the first pass covers slab rows [floor(nwg c / chunks), floor(nwg (c + 1) / chunks)); a
+// point-range cut placed on one of these row boundaries splits the reduction into chunks of the first
+// range (pre-reduced while the second range's backward runs) and of the second (fit.point_ranges,
+// tdq_slab_prereduce_bf3) without changing any summation order
+__host__ __device__ inline int slab_chunk_lo(int nwg, int chunks, int c) {
+  return (int)(((long long)nwg * c) / chunks);
+}
 
 // four consecutive slab entries (float4 column q of row `row`) as fp32; H: the slab holds bf16
 template <bool H>
@@ -151,7 +158,7 @@ __device__ __forceinline__ f32x4 slab_ld4(const void* __restrict__ slab, size_t 
 template <bool H = false>
 __device__ __forceinline__ void slab_reduce1_body(const void* __restrict__ slab, float* __restrict__ part, int nwg,
                                                   int Pst, int chunks, int q, int c) {
-  const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
+  const int lo = slab_chunk_lo(nwg, chunks, c), hi = slab_chunk_lo(nwg, chunks, c + 1);
   const size_t row = (size_t)(Pst >> 2);
   f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();
   int wgi = lo;
@@ -177,7 +184,7 @@ __device__ __forceinline__ void bf8_add(f32x4& lo, f32x4& hi, const uint4 u) {
 }
 __device__ __forceinline__ void slab_reduce1_body8(const void* __restrict__ slab, float* __restrict__ part, int nwg,
                                                    int Pst, int chunks, int q8, int c) {
-  const int lo = (int)(((long long)nwg * c) / chunks), hi = (int)(((long long)nwg * (c + 1)) / chunks);
+  const int lo = slab_chunk_lo(nwg, chunks, c), hi = slab_chunk_lo(nwg, chunks, c + 1);
   const uint4* s8 = reinterpret_cast<const uint4*>(slab) + q8;  // row stride Pst / 8 uint4
   const size_t rs = (size_t)(Pst >> 3);
   f32x4 a0 = zero4(), a1 = zero4(), a2 = zero4(), a3 = zero4();

@@ -297,14 +297,15 @@ class AdamEngine:
         # images the previous step's tail wrote into this one scratch
         J, saved, work, grad = self._step_buffers()
         rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
-        run_ranges(prog, fop, self.flat, rng, self._streams, pack=not in_graph, bufs=(J, saved, work))
+        pre = prereduce_chunk(prog, rng)
+        run_ranges(prog, fop, self.flat, rng, self._streams, pack=not in_graph, bufs=(J, saved, work), prereduce=pre)
         grads = self._fused_grads(fop, grad, fop.dlam, fop.dscal)
         packed = fused.group_array(self._opt_groups(grads))
         if packed is None:  # gradient tensors the single launch cannot take: reduce, then Adam
             raise RuntimeError("fused step tail: parameter groups do not fit one launch "
                                "(set TDQ_FUSED_TAIL=0)")
         jet_hip.step_tail(saved, work, grad, fop, st, self.counters, packed[0], packed[1], st["best_flat"],
-                          write_images=in_graph)
+                          write_images=in_graph, c_first=pre)
         self._tail_saved = saved
         return fop.total
 
@@ -398,7 +399,8 @@ class AdamEngine:
         # weight images that the previous step's dp_tail_b wrote into this one scratch
         J, saved, work, _ = self._step_buffers()
         rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
-        run_ranges(prog, fop, self.flat, rng, self._streams, pack=False, bufs=(J, saved, work))
+        pre = prereduce_chunk(prog, rng)
+        run_ranges(prog, fop, self.flat, rng, self._streams, pack=False, bufs=(J, saved, work), prereduce=pre)
         n_p = self.flat.numel()
         red_idx = self.red_idx
         if not red_idx or red_idx[0] != 0:
@@ -411,7 +413,7 @@ class AdamEngine:
             buf = self._dp_buf = torch.empty(n_p + n_e + 1 + n_t, dtype=torch.float32, device=self.device)
         grad_view = buf[:n_p]
         jet_hip.dp_tail_a(saved, work, grad_view, fop, total=buf[n_p + n_e:n_p + n_e + 1],
-                          losses=buf[n_p + n_e + 1:])
+                          losses=buf[n_p + n_e + 1:], c_first=pre)
         grads = self._fused_grads(fop, grad_view, fop.dlam, fop.dscal)
         if others:
             torch.cat([grads[i].reshape(-1) for i in others], out=buf[n_p:n_p + n_e])
@@ -574,13 +576,27 @@ def point_ranges(program, fop):
     N = program.X_all.shape[0]
     if N < 8192:
         return None
+    # preferred cuts: a row boundary of the slab reduction's chunks (slab_chunk_lo), so the first
+    # range's rows are pre-reduced while the second range's backward runs (prereduce_chunk) with
+    # every summation order unchanged; else the nearest multiple of 128 points
+    from .ops import jet_hip
+    try:
+        pts_b, nwg, chunks, _ = jet_hip.slab_geometry(cfg, N)
+        bounds = [(nwg * c // chunks) * pts_b for c in range(1, chunks)]
+        bounds = [a for a in bounds if a % 128 == 0]
+    except Exception:  # noqa: BLE001 - no native library: plain 128-point cuts
+        bounds = []
     cuts, blks = [0], [0]
     for f in fracs:
-        a = int(round(f * N / 128)) * 128
-        if a <= cuts[-1] or a >= N:
-            return None
-        b = fop.split_block(a)
-        if b is None or b <= blks[-1]:
+        b = None
+        cands = ([min(bounds, key=lambda a: abs(a - f * N))] if bounds else []) + [int(round(f * N / 128)) * 128]
+        for a in cands:
+            if cuts[-1] < a < N and abs(a - f * N) <= 0.05 * N:
+                b = fop.split_block(a)
+                if b is not None and b > blks[-1]:
+                    break
+            b = None
+        if b is None:
             return None
         cuts.append(a)
         blks.append(b)
@@ -589,11 +605,30 @@ def point_ranges(program, fop):
     return [(cuts[i], cuts[i + 1], blks[i], blks[i + 1] - blks[i]) for i in range(len(cuts) - 1)]
 
 
-def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None):
+def prereduce_chunk(program, ranges):
+    """First-pass chunk index at the cut between two point ranges when the cut lies on a chunk
+    boundary of the slab reduction (those chunks are reduced right after the first range's
+    backward), else 0."""
+    if not ranges or len(ranges) != 2 or os.environ.get("TDQ_PREREDUCE", "1") == "0":
+        return 0
+    from .ops import jet_hip
+    from .ops.jet_mlp import hip_config
+    cfg = hip_config(program.net, program.plan, program.precision)
+    pts_b, nwg, chunks, _ = jet_hip.slab_geometry(cfg, program.X_all.shape[0])
+    cut = ranges[0][1]
+    for c in range(1, chunks):
+        if (nwg * c // chunks) * pts_b == cut:
+            return c
+    return 0
+
+
+def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prereduce=0):
     """Forward -> fused loss -> backward of every point range, each range on its own stream
     (forked from and joined back into the current one; one range runs on the current stream).
     ``bufs``: ``(J, saved, work)`` to reuse (persistent step buffers), else allocated here.
-    Returns ``(saved, work)`` for the fused step tail."""
+    ``prereduce`` (> 0): after the first range's backward, reduce slab chunks ``[0, prereduce)`` on
+    its stream (the fused step tail then starts at that chunk).  Returns ``(saved, work)`` for the
+    fused step tail."""
     from .ops import jet_hip
     if bufs is None:
         J, saved = jet_hip.alloc_forward(program.X_all, flat, program.net, program.plan, program.precision)
@@ -613,11 +648,13 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None):
     cur = torch.cuda.current_stream(flat.device)
     for st in streams[:len(ranges)]:
         st.wait_stream(cur)
-    for (lo, hi, b0, nb), st in zip(ranges, streams):
+    for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
         with torch.cuda.stream(st):
             jet_hip.forward_range(saved, J, lo, hi)
             fop.run_range(J, b0, nb)
             jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
+            if k == 0 and prereduce:
+                jet_hip.slab_prereduce(saved, work, 0, prereduce)
     for st in streams[:len(ranges)]:
         cur.wait_stream(st)
     return saved, work
@@ -664,8 +701,9 @@ class LossGradEngine:
                     self._ranges = point_ranges(prog, fop)
                     self._streams = [torch.cuda.Stream(device=self.flat.device) for _ in (self._ranges or ())]
                 if self._ranges:
-                    saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams)
-                    jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:])
+                    pre = prereduce_chunk(prog, self._ranges)
+                    saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams, prereduce=pre)
+                    jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:], c_first=pre)
                     return fg
                 J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
                 fop(J, with_total=False, reduce=False)

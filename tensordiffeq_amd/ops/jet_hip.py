@@ -196,12 +196,35 @@ def pack_images(saved):
     _lib.check(rc, "tdq_jet_bf3_pack")
 
 
-def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, snapshot, write_images=True):
+def slab_geometry(cfg, N):
+    """``(points per backward workgroup, slab rows, first-pass chunks, rows per chunk)`` of the
+    split-bf16 backward over N points (``tdq_bf3_slab_geometry``)."""
+    lib = _lib.load()
+    out = (ctypes.c_int * 4)()
+    rc = lib.tdq_bf3_slab_geometry(int(N), cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"],
+                                   *_lo_args(cfg), out)
+    _lib.check(rc, "tdq_bf3_slab_geometry")
+    return tuple(out)
+
+
+def slab_prereduce(saved, work, c0, c1):
+    """First-pass chunks ``[c0, c1)`` of the slab reduction on the current stream (the first point
+    range's rows, while the second range's backward runs)."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    rc = lib.tdq_slab_prereduce_bf3(_lib.ptr(work), X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"],
+                                    cfg["n_hidden"], S, *_lo_args(cfg), int(c0), int(c1), _lib.stream_ptr(X.device))
+    _lib.check(rc, "tdq_slab_prereduce_bf3")
+
+
+def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, snapshot, write_images=True,
+              c_first=0):
     """End of a single-process Adam step in two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``):
     slab reduction + loss reduction + bookkeeping, then the reduced gradient fused into Adam
     (theta, SA weights), the best-weights snapshot and - ``write_images`` - the next step's
     weight images.  ``book``: the engine's device state dict; ``group_array``: ctypes array of
-    ``fused._Group`` with theta first."""
+    ``fused._Group`` with theta first; ``c_first``: first-pass chunks below it were pre-reduced
+    (:func:`slab_prereduce`)."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     hist = book["hist"]
@@ -214,7 +237,7 @@ def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, sna
         _lib.ptr(hist), int(hist.shape[0]), _lib.ptr(book["epoch"]), _lib.ptr(book["best_loss"]),
         _lib.ptr(book["best_epoch"]), _lib.ptr(book["improved"]), ctypes.cast(carr, ctypes.c_void_p), len(counters),
         ctypes.cast(group_array, ctypes.c_void_p), n_groups,
-        _lib.ptr(snapshot) if snapshot is not None else None, _lib.stream_ptr(X.device))
+        _lib.ptr(snapshot) if snapshot is not None else None, int(c_first), _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_step_tail_bf3")
 
 
@@ -245,7 +268,7 @@ class JetMLPFunction(torch.autograd.Function):
         return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None
 
 
-def dp_tail_a(saved, work, grad, fop, total=None, losses=None):
+def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0):
     """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
     slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``).  ``total`` (a 1-element
     view): also write the summed loss there; ``losses`` (an ``n_terms`` view, default
@@ -255,7 +278,7 @@ def dp_tail_a(saved, work, grad, fop, total=None, losses=None):
     losses = fop.losses if losses is None else losses
     rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"],
                                cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
-                               fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total),
+                               fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total), int(c_first),
                                _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")
 

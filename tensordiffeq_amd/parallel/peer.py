@@ -143,11 +143,11 @@ def _self_test(comm, n):
     return ok and int(comm.err.item()) == 0
 
 
-def _time_us(fn, buf, reps=30):
+def _time_us(fn, buf, ctx, reps=30):
     for _ in range(3):
         fn(buf)
     torch.cuda.synchronize(buf.device)
-    dist.barrier()
+    ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         fn(buf)
@@ -205,10 +205,10 @@ def setup(ctx, bench_floats=49_408):
         comm.close()
         return None
     buf = torch.randn(bench_floats, device=ctx.device)
-    t_peer = _time_us(comm.all_reduce_, buf)
+    t_peer = _time_us(comm.all_reduce_, buf, ctx)
     _log(f"setup: peer {t_peer:.1f} us")
     if m == "auto":
-        t_ref = _time_us(lambda b: dist.all_reduce(b, op=dist.ReduceOp.SUM), buf)
+        t_ref = _time_us(lambda b: dist.all_reduce(b, op=dist.ReduceOp.SUM), buf, ctx)
     else:
         t_ref = float("nan")
     _log(f"setup: torch.distributed {t_ref:.1f} us")

@@ -47,7 +47,7 @@ def main(argv=None):
     with cf.ThreadPoolExecutor(a.j) as ex:
         objs = list(ex.map(comp, srcs))
     exe = os.path.join(out, "host_check")
-    r = subprocess.run([hipcc(), "--offload-arch=gfx950", "-fsanitize=address,undefined", "-o", exe] + objs,
+    r = subprocess.run([hipcc(), "--offload-arch=gfx950", "-fsanitize=address,undefined", "-o", exe] + objs + ["-lhiprtc"],
                        capture_output=True, text=True)
     if r.returncode:
         print(r.stderr[-3000:])
