@@ -416,6 +416,8 @@ class CollocationSolverND:
             if self.metrics is not None:
                 self.metrics.n_points = self.X_f_local.shape[0]
                 self.metrics.mark(start_epoch)
+                if ctx.is_distributed:  # which collective carries the DP bucket (and its start-up timing)
+                    self.metrics.log_event("allreduce", world=ctx.world, **ctx.allreduce_info)
 
             def progress(done, loss):
                 bar.n = done
