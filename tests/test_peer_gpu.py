@@ -93,3 +93,45 @@ def test_peer_allreduce_two_ranks_one_gpu():
         # halves of the two start values summed, then each later call halves and re-sums S
         v = 0.5 * (float(1 + rep) + float(2 + rep))
         assert np.all(got[0]["graph"][rep] == v) and np.all(got[1]["graph"][rep] == v), rep
+
+
+def _timeout_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE="1", TDQ_PEER_TIMEOUT_S="2")
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(backend="gloo", device="cuda:0")
+    res = {"on": ctx.peer is not None}
+    if ctx.peer is not None:
+        buf = torch.ones(4096, device=ctx.device)
+        if rank == 0:            # rank 1 skips this call: rank 0's waits must time out, not hang
+            ctx.all_reduce_(buf)
+        torch.cuda.synchronize()
+        try:
+            ctx.check_health()
+            res["raised"] = False
+        except RuntimeError as e:
+            res["raised"] = "timed out" in str(e)
+    q.put((rank, res))
+    ctx.barrier()
+    # the communicator's call counters now disagree: do not close through another collective
+    ctx.peer = None
+    pdist.destroy()
+
+
+@pytest.mark.timeout(200)
+def test_peer_allreduce_times_out_instead_of_hanging():
+    """A rank that never arrives: the waiting rank's kernel gives up after TDQ_PEER_TIMEOUT_S, sets
+    its error word and drains (the GPU is never held), and check_health() raises."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0]["on"] and got[1]["on"]
+    assert got[0]["raised"] is True and got[1]["raised"] is False

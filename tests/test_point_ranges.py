@@ -93,3 +93,28 @@ def test_point_ranges_one_cut_at_most(monkeypatch):
     monkeypatch.setenv("TDQ_SPLIT", "0.3,0.6")
     with pytest.raises(ValueError):
         fit.point_ranges(prog, fop)
+
+
+def test_cut_on_slab_chunk_boundary_enables_prereduce(monkeypatch):
+    """bf16 (128-point backward workgroups): the auto cut lands on a row boundary of the slab
+    reduction's chunks, so the first range's chunks are pre-reduced (fit.prereduce_chunk); a cut
+    off the boundaries disables it.  Needs the native library only for the geometry query."""
+    from tensordiffeq_amd.ops import _lib, jet_hip
+    from tensordiffeq_amd.ops.jet_mlp import hip_config
+    if not _lib.available():
+        pytest.skip("native library not built")
+    prog, fop = _program(n_f=50000)
+    prog.precision = "bf16"
+    monkeypatch.setenv("TDQ_SPLIT", "auto")
+    r = fit.point_ranges(prog, fop)
+    N = prog.X_all.shape[0]
+    pts_b, nwg, chunks, _ = jet_hip.slab_geometry(hip_config(prog.net, prog.plan, "bf16"), N)
+    assert pts_b == 128 and nwg == (N + 127) // 128 and chunks == 8
+    c = fit.prereduce_chunk(prog, r)
+    assert 0 < c < chunks and r[0][1] == (nwg * c // chunks) * pts_b
+    assert abs(r[0][1] - 0.38 * N) <= 0.05 * N
+    monkeypatch.setenv("TDQ_PREREDUCE", "0")
+    assert fit.prereduce_chunk(prog, r) == 0
+    monkeypatch.delenv("TDQ_PREREDUCE")
+    off = [(0, r[0][1] + 128) + r[0][2:], (r[0][1] + 128,) + r[1][1:]]
+    assert fit.prereduce_chunk(prog, off) == 0
