@@ -24,9 +24,24 @@ struct LSpec {
   int ia[TDQ_MAXS], ib[TDQ_MAXS];
 };
 
+// bf16 GEMM operands of an output, written by the same pass (nullptr: none): hi = rne(x), lo =
+// rne(x - hi) for the bf16x3 family (ops/jet_layered.py _Op)
+template <int V>
+__device__ __forceinline__ void store_split(__bf16* __restrict__ hi, __bf16* __restrict__ lo, long long off,
+                                            const float (&x)[V]) {
+  if (hi == nullptr) return;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const __bf16 h = (__bf16)x[v];
+    hi[off + v] = h;
+    if (lo != nullptr) lo[off + v] = (__bf16)(x[v] - (float)h);
+  }
+}
+
 template <int S, int V>
 __global__ void __launch_bounds__(256) layered_fwd_kernel(float* __restrict__ Z, const float* __restrict__ bias,
-                                                          long long NW, int W, LSpec sp) {
+                                                          long long NW, int W, LSpec sp, __bf16* __restrict__ bh,
+                                                          __bf16* __restrict__ bl) {
   const long long e = ((long long)blockIdx.x * 256 + threadIdx.x) * V;
   if (e >= NW) return;
   float z[S][V];
@@ -66,12 +81,14 @@ __global__ void __launch_bounds__(256) layered_fwd_kernel(float* __restrict__ Z,
       *reinterpret_cast<float4*>(Z + (long long)s * NW + e) = make_float4(o[s][0], o[s][1], o[s][2], o[s][3]);
     else
       Z[(long long)s * NW + e] = o[s][0];
+    store_split<V>(bh, bl, (long long)s * NW + e, o[s]);
   }
 }
 
 template <int S, int V>
 __global__ void __launch_bounds__(256) layered_bwd_kernel(float* __restrict__ HB, const float* __restrict__ H,
-                                                          long long NW, LSpec sp) {
+                                                          long long NW, LSpec sp, __bf16* __restrict__ bh,
+                                                          __bf16* __restrict__ bl) {
   const long long e = ((long long)blockIdx.x * 256 + threadIdx.x) * V;
   if (e >= NW) return;
   float h[S][V], hb[S][V];
@@ -122,34 +139,38 @@ __global__ void __launch_bounds__(256) layered_bwd_kernel(float* __restrict__ HB
       *reinterpret_cast<float4*>(HB + (long long)s * NW + e) = make_float4(zb[s][0], zb[s][1], zb[s][2], zb[s][3]);
     else
       HB[(long long)s * NW + e] = zb[s][0];
+    store_split<V>(bh, bl, (long long)s * NW + e, zb[s]);
   }
 }
 
 template <int S>
 static int launch_layered(int fwd, float* A, const float* B, const float* bias, long long NW, int W, const LSpec& sp,
-                          hipStream_t st) {
+                          __bf16* bh, __bf16* bl, hipStream_t st) {
   const bool vec = (NW % 4) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0 &&
                    (B == nullptr || (reinterpret_cast<uintptr_t>(B) & 15) == 0);
   const int V = vec ? 4 : 1;
   const long long threads = (NW + V - 1) / V;
   const dim3 grid((unsigned)((threads + 255) / 256));
   if (fwd) {
-    if (vec) hipLaunchKernelGGL((layered_fwd_kernel<S, 4>), grid, dim3(256), 0, st, A, bias, NW, W, sp);
-    else hipLaunchKernelGGL((layered_fwd_kernel<S, 1>), grid, dim3(256), 0, st, A, bias, NW, W, sp);
+    if (vec) hipLaunchKernelGGL((layered_fwd_kernel<S, 4>), grid, dim3(256), 0, st, A, bias, NW, W, sp, bh, bl);
+    else hipLaunchKernelGGL((layered_fwd_kernel<S, 1>), grid, dim3(256), 0, st, A, bias, NW, W, sp, bh, bl);
   } else {
-    if (vec) hipLaunchKernelGGL((layered_bwd_kernel<S, 4>), grid, dim3(256), 0, st, A, B, NW, sp);
-    else hipLaunchKernelGGL((layered_bwd_kernel<S, 1>), grid, dim3(256), 0, st, A, B, NW, sp);
+    if (vec) hipLaunchKernelGGL((layered_bwd_kernel<S, 4>), grid, dim3(256), 0, st, A, B, NW, sp, bh, bl);
+    else hipLaunchKernelGGL((layered_bwd_kernel<S, 1>), grid, dim3(256), 0, st, A, B, NW, sp, bh, bl);
   }
   TDQ_CHECK_LAUNCH();
   return 0;
 }
 
+static inline __bf16* H16(void* p) { return reinterpret_cast<__bf16*>(p); }
+
 extern "C" {
 
 // fwd = 1: A = Z [S][N][W] -> H in place (bias [W] on the value stream).
 // fwd = 0: A = HB [S][N][W] -> ZB in place, B = H (saved post-activations of the same layer).
+// bh / bl (nullable, [S][N][W] bf16): the output's bf16 GEMM operand (hi) and its residual (lo).
 int tdq_layered_epi(int fwd, float* A, const float* B, const float* bias, long long N, int W, int S, const int* spec,
-                    void* stream) {
+                    void* bh, void* bl, void* stream) {
   if (N <= 0) return 0;
   if (S < 1 || S > TDQ_MAXS || W < 1 || A == nullptr || (fwd && bias == nullptr) || (!fwd && B == nullptr))
     return (int)hipErrorInvalidValue;
@@ -167,14 +188,14 @@ int tdq_layered_epi(int fwd, float* A, const float* B, const float* bias, long l
   const long long NW = N * (long long)W;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (S) {
-    case 1: return launch_layered<1>(fwd, A, B, bias, NW, W, sp, st);
-    case 2: return launch_layered<2>(fwd, A, B, bias, NW, W, sp, st);
-    case 3: return launch_layered<3>(fwd, A, B, bias, NW, W, sp, st);
-    case 4: return launch_layered<4>(fwd, A, B, bias, NW, W, sp, st);
-    case 5: return launch_layered<5>(fwd, A, B, bias, NW, W, sp, st);
-    case 6: return launch_layered<6>(fwd, A, B, bias, NW, W, sp, st);
-    case 7: return launch_layered<7>(fwd, A, B, bias, NW, W, sp, st);
-    case 8: return launch_layered<8>(fwd, A, B, bias, NW, W, sp, st);
+    case 1: return launch_layered<1>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 2: return launch_layered<2>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 3: return launch_layered<3>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 4: return launch_layered<4>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 5: return launch_layered<5>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 6: return launch_layered<6>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 7: return launch_layered<7>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
+    case 8: return launch_layered<8>(fwd, A, B, bias, NW, W, sp, H16(bh), H16(bl), st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _lock = threading.Lock()
 _lib = None
@@ -66,6 +66,7 @@ def _declare(lib):
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
         "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P]),
+        "tdq_layered_epi": (I, [I, P, P, P, L, I, I, P, P, P, P]),
         # one-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py)
         "tdq_peer_maxw": (I, []),
         "tdq_peer_chunk": (I, []),

@@ -82,6 +82,15 @@ class _Op:
             if prec == "bf16x3":
                 self.l = (x - self.h.float()).to(torch.bfloat16)
 
+    @classmethod
+    def parts(cls, prec, h, l=None):
+        """An operand whose bf16 hi (/ lo) copies were written by the epilogue pass itself."""
+        o = cls.__new__(cls)
+        o.prec, o.h = prec, h
+        if l is not None:
+            o.l = l
+        return o
+
     def t(self):
         o = _Op.__new__(_Op)
         o.prec = self.prec
@@ -136,16 +145,26 @@ def _mm_tn(a, b, out):
     return out
 
 
-def _epi(fwd, A, B, bias, spec):
+def _epi(fwd, A, B, bias, spec, prec="fp32"):
+    """The fused epilogue pass in place on A; returns ``(A, op)`` with ``op`` the :class:`_Op` of
+    the result viewed ``[S*N, W]`` - in the bf16 families its hi (/ lo) copies are written by the
+    same pass instead of a separate conversion."""
     S, N, W = A.shape
     if A.is_cuda:
         lib = _lib.load(required=True)
         c = (ctypes.c_int * len(spec))(*spec)
+        hi = lo = None
+        if prec in ("bf16", "bf16x3"):
+            hi = torch.empty((S * N, W), dtype=torch.bfloat16, device=A.device)
+            if prec == "bf16x3":
+                lo = torch.empty_like(hi)
         rc = lib.tdq_layered_epi(1 if fwd else 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(bias), N, W, S, c,
-                                 _lib.stream_ptr(A.device))
+                                 _lib.ptr(hi), _lib.ptr(lo), _lib.stream_ptr(A.device))
         _lib.check(rc, "tdq_layered_epi")
-        return A
-    return _epi_fwd_torch(A, bias, spec) if fwd else _epi_bwd_torch(A, B, spec)
+        op = _Op.parts(prec, hi, lo) if hi is not None else _Op(A.view(S * N, W), prec)
+        return A, op
+    A = _epi_fwd_torch(A, bias, spec) if fwd else _epi_bwd_torch(A, B, spec)
+    return A, _Op(A.view(S * N, W), prec)
 
 
 @torch.no_grad()
@@ -162,16 +181,14 @@ def forward_raw(X, P, net, plan, precision="fp32"):
     for s in range(1, S):
         if spec[3 * s] == 1:
             Z[s].copy_(K0[spec[3 * s + 1]].expand(N, W0))
-    Hs = [_epi(True, Z, None, b0, spec)]
-    Ho = []                                          # GEMM operands of the saved activations
+    H, op = _epi(True, Z, None, b0, spec, precision)
+    Hs, Ho = [H], [op]                               # saved activations and their GEMM operands
     for K, b in ws[1:-1]:
-        Hp = Hs[-1]
-        Ho.append(_Op(Hp.view(S * N, Hp.shape[2]), precision))
         Z = _mm(Ho[-1], _Op(K, precision)).view(S, N, K.shape[1])
-        Hs.append(_epi(True, Z, None, b, spec))
+        H, op = _epi(True, Z, None, b, spec, precision)
+        Hs.append(H)
+        Ho.append(op)
     Ko, bo = ws[-1]
-    Hl = Hs[-1]
-    Ho.append(_Op(Hl.view(S * N, Hl.shape[2]), precision))
     J = _mm(Ho[-1], _Op(Ko, precision)).view(S, N, Ko.shape[1])
     J[0] += bo
     return J, ("layered", X, P, net, spec, Hs, Ho, precision)
@@ -197,14 +214,13 @@ def backward_raw(saved, dJ, grad=None):
         HB = _mm(dJo, _Op(Ko.t().contiguous(), prec)).view(S, N, Ko.shape[0])
     for i in range(len(ws) - 2, 0, -1):
         K, _ = ws[i]
-        ZB = _epi(False, HB, Hs[i], None, spec)
-        ZBo = _Op(ZB.view(S * N, ZB.shape[2]), prec)
+        ZB, ZBo = _epi(False, HB, Hs[i], None, spec, prec)
         _mm_tn(Ho[i - 1], ZBo, gw[i][0])
         torch.sum(ZB[0], dim=0, out=gw[i][1])
         # K^T materialized (W x W): the library's transposed-B kernels for this shape ran ~4x slower
         # than its row-major ones (rocprofv3, profiles/r3_ag_*)
         HB = _mm(ZBo, _Op(K.t().contiguous(), prec)).view(S, N, K.shape[0])
-    ZB0 = _epi(False, HB, Hs[0], None, spec)
+    ZB0, _ = _epi(False, HB, Hs[0], None, spec)
     dK0, db0 = gw[0]
     torch.mm(X.t(), ZB0[0], out=dK0)
     for s in range(1, S):
