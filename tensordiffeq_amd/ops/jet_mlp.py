@@ -62,8 +62,6 @@ def hip_config(net, plan, precision=None):
     hidden = sizes[1:-1]
     if len(hidden) < 1:
         raise ValueError("needs at least one hidden layer")
-    if len(hidden) > 16:
-        raise ValueError("more than 16 hidden layers")
     if plan.order > 2:
         raise ValueError("derivative order > 2")
     S = plan.S
@@ -75,28 +73,33 @@ def hip_config(net, plan, precision=None):
     precision = precision or _precision
     if precision not in PRECISIONS:
         raise ValueError(f"precision {precision!r} not in {PRECISIONS}")
-    if WT > 8:
-        # beyond the fused kernels' register envelope: the layer-wise engine (library GEMMs on the
-        # stacked streams in the requested precision family + fused HIP tanh-jet epilogues,
-        # ops/jet_layered.py)
+
+    def layered(why):
+        # outside the fused kernels' envelope: the layer-wise engine (library GEMMs on the stacked
+        # streams in the requested precision family + fused HIP tanh-jet epilogues,
+        # ops/jet_layered.py), which takes any depth, width and input / output width
         return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
-                "n_hidden": len(hidden), "precision": precision, "engine": "layered"}
+                "n_hidden": len(hidden), "precision": precision, "engine": "layered", "why": why}
+
+    if WT > 8:
+        return layered("hidden width > 128")
+    if len(hidden) > 16:
+        return layered("more than 16 hidden layers")
+    if d_in > 8 or d_out > 4:
+        return layered("input width > 8 or output width > 4")
     if WT not in (1, 2, 4, 8):
         WT = 4 if WT == 3 else 8
-    if d_in > 8 or d_out > 4:
-        raise ValueError("input width > 8 or output width > 4")
     if precision in ("bf16x3", "bf16") and WT < 2:
         precision = "fp32"
     # split-bf16 kernels: any S <= 8 at every width class (S x WT > 32: the one-wave-per-SIMD
     # "wide" kernels, csrc/jet_bf3.h); the exact-fp32 family keeps the 2-wave register budget
     if precision == "fp32" and S * WT > 32:
-        raise ValueError(f"fp32 kernels: streams x width tiles = {S * WT} > 32 (register budget); "
-                         f"use precision bf16x3 or bf16")
+        return layered(f"fp32 with streams x width tiles = {S * WT} > 32")
     if precision == "fp32" and not uniform:
         # the split-bf16 kernels pad unequal hidden layers to the widest; the exact-fp32 family
         # takes equal widths only
         if WT < 2:
-            raise ValueError("unequal hidden widths <= 16: no kernel family")
+            return layered("unequal hidden widths <= 16 in fp32")
         precision = "bf16x3"
     return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
             "n_hidden": len(hidden), "precision": precision}

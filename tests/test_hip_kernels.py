@@ -59,15 +59,19 @@ def _setup(sizes, reqs, N, seed=0):
     return net, X, plan
 
 
+def _fused_precision(jet_mlp, net, plan, prec):
+    cfg = jet_mlp.hip_config(net, plan, prec)
+    if cfg.get("engine") == "layered":   # e.g. fp32 wide plans: tests/test_layered_jet.py covers these
+        pytest.skip(f"outside the fused kernels' envelope ({cfg['why']})")
+    return cfg["precision"]
+
+
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("sizes,reqs,N", CASES)
 def test_jet_forward_matches_torch(sizes, reqs, N, prec):
     from tensordiffeq_amd.ops import jet_hip, jet_mlp
     net, X, plan = _setup(sizes, reqs, N)
-    try:
-        prec = jet_mlp.hip_config(net, plan, prec)["precision"]   # e.g. fp32 + unequal widths -> bf16x3
-    except ValueError:
-        pytest.skip("configuration outside the kernel envelope")
+    prec = _fused_precision(jet_mlp, net, plan, prec)   # e.g. fp32 + unequal widths -> bf16x3
     with torch.no_grad():
         J = jet_hip.JetMLPFunction.apply(X, net.flat, net, plan, prec)
         Jref = jet_forward(X.double(), [(k.double(), b.double()) for k, b in net.weights()], plan)
@@ -106,10 +110,7 @@ def test_jet_forward_matches_autograd(prec):
 def test_jet_backward_matches_autograd(sizes, reqs, N, prec):
     from tensordiffeq_amd.ops import jet_hip, jet_mlp
     net, X, plan = _setup(sizes, reqs, N, seed=1)
-    try:
-        prec = jet_mlp.hip_config(net, plan, prec)["precision"]
-    except ValueError:
-        pytest.skip("configuration outside the kernel envelope")
+    prec = _fused_precision(jet_mlp, net, plan, prec)
     G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
     p = net.flat.detach().clone().requires_grad_(True)
     J = jet_hip.JetMLPFunction.apply(X, p, net, plan, prec)

@@ -17,12 +17,23 @@ CASES = [
     ([3, 20, 16, 2], [(0, 0), (1, 1), (0, 1), (2,)], 29),
     ([2, 16, 1], [], 11),
     ([1, 12, 12, 1], [(0, 0)], 17),
+    ([10, 16, 16, 5], [(0,), (9,), (3, 3)], 21),     # input width > 8, output width > 4
 ]
 GPU_CASES = [
     ([2, 256, 256, 256, 256, 1], [(0,), (1,), (0, 0)], 1000),   # AC plan at width 256
     ([3, 256, 256, 1], [(0,), (1,), (2,), (0, 0), (1, 1), (0, 1)], 301),   # S=7, mixed derivative
     ([2, 160, 320, 200, 2], [(0, 0), (1, 1)], 257),               # unequal widths > 128, d_out 2
     ([2, 512, 512, 1], [(0,), (1,)], 130),
+]
+# configurations inside the width envelope that the fused kernels still do not take (hip_config
+# routes them here): input width > 8, output width > 4, > 16 hidden layers, fp32 wide plans
+# (streams x width tiles > 32), unequal widths <= 16 in fp32
+ENVELOPE_CASES = [
+    ([10, 64, 64, 1], [(0,), (9,), (3, 3)], 200, None),
+    ([2, 48, 48, 5], [(0,), (1,), (0, 0)], 150, None),
+    ([2] + [24] * 18 + [1], [(0,), (1,), (0, 0)], 120, None),
+    ([3, 128, 128, 128, 1], [(0,), (1,), (2,), (0, 0), (1, 1), (0, 1)], 300, "fp32"),
+    ([2, 12, 16, 1], [(0,), (0, 0)], 90, "fp32"),
 ]
 
 
@@ -120,3 +131,33 @@ def test_layered_engine_trains_in_bf16_families():
         rel = ((hist[prec] - hist["fp32"]).abs() / hist["fp32"].abs()).max().item()
         print(f"LAYERED_TRAJ {prec} max rel diff vs fp32 {rel:.3e}")
         assert rel < tol, (prec, rel)
+
+
+@pytest.mark.parametrize("sizes,reqs,N,only", ENVELOPE_CASES)
+def test_envelope_routes_to_layered(sizes, reqs, N, only):
+    from tensordiffeq_amd.ops import jet_hip, jet_mlp
+    net, X, plan = _setup(sizes, reqs, N, "cpu", torch.float32)
+    for prec in ([only] if only else ["fp32", "bf16x3", "bf16"]):
+        cfg = jet_mlp.hip_config(net, plan, prec)
+        assert jet_hip.is_layered(cfg) and cfg["precision"] == prec and cfg["why"], cfg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes,reqs,N,only", ENVELOPE_CASES)
+def test_envelope_layered_hip(sizes, reqs, N, only):
+    from tensordiffeq_amd.ops import jet_hip
+    net, X, plan = _setup(sizes, reqs, N, "cuda", torch.float32, seed=2)
+    for prec in ([only] if only else ["fp32", "bf16x3", "bf16"]):
+        p = net.flat.detach().clone().requires_grad_(True)
+        J = jet_hip.JetMLPFunction.apply(X, p, net, plan, prec)
+        G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
+        (J.double() * G).sum().backward()
+        Jr, gr = _ref(net, X, plan, G)
+        scale = Jr.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
+        ferr = ((J.detach().double() - Jr).abs() / scale).max().item()
+        rel = ((p.grad.double() - gr).norm() / gr.norm()).item()
+        print(f"KERNEL_ERR layered-envelope {prec} {sizes} S={plan.S} fwd {ferr:.3e} bwd {rel:.3e}")
+        tf, tb = LTOL[prec]
+        # bf16 over 18 hidden layers: the rounding compounds with depth (x2 bound)
+        deep = 2 if (prec == "bf16" and len(sizes) > 10) else 1
+        assert ferr < tf * deep and rel < tb * deep, (prec, ferr, rel)
