@@ -1,6 +1,6 @@
-"""One-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py) with 2 ranks sharing cuda:0.
+"""One-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py) with 2 and 4 ranks sharing cuda:0.
 
-Two processes on one GPU exercise everything the 8-GPU xGMI path runs except the fabric: the
+Several processes on one GPU exercise everything the 8-GPU xGMI path runs except the fabric: the
 uncached IPC-shared receive slots and flags, the push / flag / bounded wait / rank-order sum
 kernel, the self-test and selection at start-up, graph capture of the kernel, and both receive
 parities.  The control plane (IPC handle exchange) rides on a gloo group.
@@ -69,30 +69,32 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_peer_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_allreduce_ranks_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=250) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    print("PEER", got[0]["info"])
-    assert got[0]["on"] and got[1]["on"], got[0]["info"]
-    assert got[0]["err"] == 0 and got[1]["err"] == 0
+    print("PEER", world, got[0]["info"])
+    for r in range(world):
+        assert got[r]["on"] and got[r]["err"] == 0, (r, got[r]["info"])
     for n in SIZES:
-        a = torch.randn(n, generator=torch.Generator().manual_seed(1000 * n + 0))
-        b = torch.randn(n, generator=torch.Generator().manual_seed(1000 * n + 1))
-        want = ((torch.zeros(n) + a) + b).numpy()        # the kernel's order: rank 0, then rank 1
-        assert np.array_equal(got[0]["outs"][n], want), n
-        assert np.array_equal(got[1]["outs"][n], got[0]["outs"][n]), n
+        want = torch.zeros(n)
+        for r in range(world):                           # the kernel's order: rank 0, 1, ...
+            want = want + torch.randn(n, generator=torch.Generator().manual_seed(1000 * n + r))
+        for r in range(world):
+            assert np.array_equal(got[r]["outs"][n], want.numpy()), (n, r)
     for rep in range(3):
-        # halves of the two start values summed, then each later call halves and re-sums S
-        v = 0.5 * (float(1 + rep) + float(2 + rep))
-        assert np.all(got[0]["graph"][rep] == v) and np.all(got[1]["graph"][rep] == v), rep
+        # halves of the start values summed, then each later call halves and re-sums S (x world / 2)
+        v = 0.5 * sum(float(r + 1 + rep) for r in range(world)) * (0.5 * world) ** 3
+        for r in range(world):
+            assert np.all(got[r]["graph"][rep] == v), (rep, r)
 
 
 def _timeout_worker(rank, world, port, q):
