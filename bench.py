@@ -231,7 +231,8 @@ def main(argv=None):
     if "TDQ_STEP_UNROLL" not in os.environ:
         # steps per captured graph: a divisor of --steps, so the timed steps are all multi-step graph
         # replays (a 1-step replay leaves ~9 us idle between graphs; 8 and 16 per graph measured
-        # equal, profiles/r3_m_unroll_ab.jsonl)
+        # equal, profiles/r3_m_unroll_ab.jsonl; at --steps 20 one 20-step graph measured slower than
+        # two 10-step replays, 0.206-0.211 vs 0.202-0.203 ms, profiles/r3_au_driver_shape_unroll_ab.jsonl)
         divs = [k for k in range(16, 3, -1) if args.steps % k == 0]
         os.environ["TDQ_STEP_UNROLL"] = str(8 if args.steps % 8 == 0 else (divs[0] if divs else 8))
     layers = tuple(int(v) for v in args.layers.split(","))

@@ -530,6 +530,10 @@ class AdamEngine:
         if hi <= lo or os.environ.get("TDQ_NAN_CHECK", "1") == "0":
             return hi
         col = st["hist"][lo:hi, 0]
+        # fast path: one reduction + one read-back (a NaN / Inf anywhere makes the sum non-finite;
+        # a finite-but-overflowing sum falls through to the exact scan, which then finds nothing)
+        if math.isfinite(float(col.sum())):
+            return hi
         bad = ~torch.isfinite(col)
         if bool(bad.any()):
             first = lo + int(torch.nonzero(bad)[0, 0])
