@@ -94,12 +94,13 @@ def test_layered_engine_hip(sizes, reqs, N, prec):
 
 
 @pytest.mark.gpu
-def test_layered_engine_trains_wide_solver():
-    """A width-256 Allen-Cahn SA-PINN picks the HIP backend (layered engine + fused loss) and
-    follows the torch-jet trajectory (both fp32) through Adam and L-BFGS steps."""
+@pytest.mark.parametrize("layers", [(2, 256, 256, 256, 1), (2,) + (24,) * 18 + (1,)])
+def test_layered_engine_trains_wide_solver(layers):
+    """A width-256 (and an 18-hidden-layer) Allen-Cahn SA-PINN picks the HIP backend (layered
+    engine + fused loss) and follows the torch-jet trajectory (both fp32) through Adam and L-BFGS
+    steps."""
     import bench
     from tensordiffeq_amd.ops import jet_hip, jet_mlp
-    layers = (2, 256, 256, 256, 1)
     hist = {}
     for backend in ("auto", "jet"):
         m = bench.build_problem(4096, 1, backend, torch.device("cuda", 0), False, "fp32", layers=layers)
