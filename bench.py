@@ -142,9 +142,55 @@ def time_steps(eng, ctx, device, steps, warmup, min_warmup_s):
     t0 = time.perf_counter()
     eng.run(steps)
     sync()
+    local = time.perf_counter() - t0    # this rank's own steps, before waiting for the others
     ctx.barrier()
     sync()
-    return ctx.max_scalar(time.perf_counter() - t0), n_warm, warm_s
+    el = time.perf_counter() - t0
+    time_steps.rank_ms = (1000.0 * ctx.min_scalar(local) / steps, 1000.0 * ctx.max_scalar(local) / steps)
+    return ctx.max_scalar(el), n_warm, warm_s
+
+
+def allreduce_replay_us(ctx, n_floats, calls=10, reps=20):
+    """Per-call time of the DP step's collective on a bucket-sized buffer, measured the way the
+    step runs it: ``calls`` all-reduces captured in one HIP graph (RCCL / peer kernel in the
+    graph) and replayed ``reps`` times, or launched from the host when the backend keeps the
+    collective out of the graph (gloo).  Max over ranks, microseconds."""
+    dev = ctx.device
+    buf = torch.randn(int(n_floats), device=dev)
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    if ctx.graph_collectives:
+        from tensordiffeq_amd.graphs import capture_graph
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            ctx.all_reduce_(buf)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        sync()
+        g = torch.cuda.CUDAGraph()
+        with capture_graph(g):
+            for _ in range(calls):
+                ctx.all_reduce_(buf)
+        g.replay()
+        sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            g.replay()
+        sync()
+        us = (time.perf_counter() - t0) / (reps * calls) * 1e6
+        mode = "in-graph"
+    else:
+        for _ in range(3):
+            ctx.all_reduce_(buf)
+        sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.all_reduce_(buf)
+        sync()
+        us = (time.perf_counter() - t0) / reps * 1e6
+        mode = "host-launched"
+    return {"us_per_call": round(ctx.max_scalar(us), 2), "floats": int(n_floats), "mode": mode}
 
 
 def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop):
@@ -214,10 +260,14 @@ def main(argv=None):
                          "bf16 = bf16 x bf16 MFMA, fp32 accumulate)")
     args = ap.parse_args(argv)
 
+    from tensordiffeq_amd.parallel import dist as pdist
+    if args.gpus > 1 and not pdist.launcher_env():
+        # one command for N GPUs: re-run this script as N ranks (child processes under
+        # torch.distributed.run, 127.0.0.1); rank 0's JSON line goes straight to our stdout
+        sys.exit(pdist.self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus != world:
-        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
-                 f"'python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}'")
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dist = world > 1
     from tensordiffeq_amd.parallel import init_distributed, get_context
     ctx = init_distributed() if dist else get_context()
@@ -244,6 +294,15 @@ def main(argv=None):
     loss = float(model._state["hist"][int(model._state["epoch_host"]) - 1, 0])
     total_steps = int(model._state["epoch_host"])
     pts_per_s = n_glob * args.steps / elapsed
+    rank_ms = getattr(time_steps, "rank_ms", None)
+    ar = None
+    if dist:
+        bucket = getattr(eng, "_dp_buf", None)
+        n_bucket = bucket.numel() if bucket is not None else model.u_model.flat.numel() + 8
+        try:
+            ar = allreduce_replay_us(ctx, n_bucket)
+        except Exception as e:  # pragma: no cover - reported, never hides the throughput number
+            ar = {"error": f"{type(e).__name__}: {e}"}
     del eng, model
 
     acc, acc_err = None, None
@@ -303,6 +362,8 @@ def main(argv=None):
             # which all-reduce the DP step captured: RCCL, or the one-shot peer kernel (csrc/peer.hip)
             # when its start-up self-test passed and it timed faster on this node
             rec["allreduce"] = dict(ctx.allreduce_info)
+            rec["allreduce"]["replay"] = ar
+            rec["rank_ms_per_step"] = {"min": round(rank_ms[0], 5), "max": round(rank_ms[1], 5)} if rank_ms else None
         if dp is not None:
             rec["forced_dp"] = dp
         print(json.dumps(rec), flush=True)

@@ -45,6 +45,11 @@ def _env_bool(name, default):
     return v.strip().lower() in ("1", "true", "yes", "on")
 
 
+# L-BFGS function-change test used by every entry point (solver, eager_lbfgs, DeviceLBFGS,
+# minimize): "legacy" = the reference's effective |f| < tolX (optimizers.py:273)
+DEFAULT_LBFGS_STOP = "legacy"
+
+
 @dataclasses.dataclass(frozen=True)
 class SolverConfig:
     backend: str = "auto"
@@ -61,7 +66,7 @@ class SolverConfig:
     # the reference's effective test (|f| < tolX, i.e. run to maxIter): on AC-SA it reaches L2
     # 2.2/2.7/2.0e-2 (seeds 0-2) against 3.7/2.7/3.4e-2 with |f - f_old| < tolX, which stops
     # L-BFGS after ~5k of 10k iterations (profiles/r3_lbfgs_stop_ab.jsonl)
-    lbfgs_stop: str = "legacy"
+    lbfgs_stop: str = DEFAULT_LBFGS_STOP
 
     @classmethod
     def from_env(cls, **overrides):

@@ -414,17 +414,6 @@ __device__ __forceinline__ Tl tl_make(const void* uniform_base, int lane) {
 #define TDQ_HS_V16 0
 #endif
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-// The last hidden layer's post-activations are NOT saved: the backward's output phase rebuilds
-// them tile by tile on the matrix cores from h_{Lh-2} (which it reads anyway for dK_{Lh-1}) or,
-// for Lh = 2, from x through h0_jet - the same MFMA sequence and tanh-jet code as the forward, so
-// the same bits (Lh = 1: layer 0 is still saved).
-// It drops 1 of the forward's 3 full saved layers (-30 % of its 217 MB of stores,
-// profiles/r3_pmc_bf16.txt), but measured on MI355X (AC-SA bf16 step, profiles/r3_e_ab.txt) the
-// forward only went 57 -> 54 us while the backward grew 137 -> 157 us: off by default,
-// -DTDQ_RECOMPUTE_TOP=1 builds it.
-#ifndef TDQ_RECOMPUTE_TOP
-#define TDQ_RECOMPUTE_TOP 0
-#endif
 template <int WT, bool LO>
 __host__ __device__ constexpr int hs_wave_floats(int S) {
   return TDQ_HS_HALF(LO) ? WT * ((TDQ_HS_V16 ? 128 : 256) + (S - 1) * 128) : S * WT * 256;
@@ -615,10 +604,8 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       for (int s = 0; s < S; ++s) z[s] = accP[s];
       z[0] += biasP;
       tanh_jet_f<S, NSO>(sp, z, h);
-      if (!(LAST && TDQ_RECOMPUTE_TOP)) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) hs_store<WT, LO>(Hl, s, t, h[s]);
-      }
+      for (int s = 0; s < S; ++s) hs_store<WT, LO>(Hl, s, t, h[s]);
       if (LAST) {
         out_dot<S>(h, Ko, t, g, vout);
       } else {
@@ -887,7 +874,7 @@ __attribute__((amdgpu_waves_per_eu(bf3_wpe(WT, S, LO), bf3_wpe(WT, S, LO))))
 jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Kimg,
                    const float* __restrict__ dJ, const float* __restrict__ Hs, float* __restrict__ slab, int N,
                    int Ptot, NetDims d, JetSpec sp, int rev, int h0r, bf16x4* __restrict__ gstage,
-                   const bf16x8* __restrict__ Fimg, int wg0) {
+                   int wg0) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int W = 16 * WT;
   constexpr int KB = WT / 2;
@@ -923,14 +910,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   constexpr int IBUF = 2 * HL * IMG;          // one buffer's images, in bf16
   constexpr int U1 = (DBUF ? 2 : 1) * IBUF / 2;  // images, in floats
   constexpr int U2 = GST ? 0 : NWV * S * WT * HL * 128;  // per-wave zb fragment stages (bf16 hi(/lo))
-  // TDQ_RECOMPUTE_TOP, bf16 (!LO): the h_{Lh-2} B fragments of the top-layer rebuild live in a
-  // wave-private LDS area right after the output-layer partials (registers are the limit: 2 waves
-  // per SIMD); bf16x3 keeps them in registers (one wave per SIMD, AGPRs)
-  constexpr bool RH_LDS = TDQ_RECOMPUTE_TOP && !LO;
-  constexpr int RH0 = NWV * W * TDQ_MAXO;                  // floats: right after accKo
-  constexpr int U3 = RH_LDS ? RH0 + NWV * S * WT * 128 : 0;  // + one bf16 fragment set per wave
-  constexpr int U12 = U1 > U2 ? U1 : U2;
-  constexpr int U = ((U12 > U3 ? U12 : U3) + 3) / 4 * 4;
+  constexpr int U = ((U1 > U2 ? U1 : U2) + 3) / 4 * 4;
   static_assert(NWV * (W * TDQ_MAXO + TDQ_MAXO + TDQ_MAXD * W) <= U, "partials must fit the union");
   __bf16* img = reinterpret_cast<__bf16*>(lds);
   float* accB = lds + U;                      // [3: layer parity 0/1, layer 0][NWV][W]
@@ -938,9 +918,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // (Ko is reduced right after the output phase, K0 after the last image read)
   float* accKo = lds;                         // [NWV][W * TDQ_MAXO]
   float* accK0 = accKo + NWV * W * TDQ_MAXO + NWV * TDQ_MAXO;  // [NWV][TDQ_MAXD * W]
-  // [NWV][TDQ_MAXO]; with the LDS top-layer fragments (Lh >= 2) in the layer-0 bias slot of accB,
-  // idle until the end of the kernel
-  float* accBo = (RH_LDS && d.n_hidden >= 2) ? accB + 2 * NWV * W : accKo + NWV * W * TDQ_MAXO;
+  float* accBo = accKo + NWV * W * TDQ_MAXO;  // [NWV][TDQ_MAXO]
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -988,90 +966,17 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     for (int q = 0; q < TDQ_MAXO; ++q)
 #pragma unroll
       for (int s = 0; s < S; ++s) ub[s][q] = q < d.d_out ? vmask * dJ[((size_t)s * N + nc) * d.d_out + q] : 0.f;
-#if TDQ_RECOMPUTE_TOP
-    // h_{Lh-1} is rebuilt (see TDQ_RECOMPUTE_TOP): B fragments of h_{Lh-2} first - from x through
-    // h0_jet when Lh - 2 = 0 (exactly the forward's fragments), else from the saved streams (the
-    // value stream fp32, derivative streams as saved: the forward rounded the same values)
-    float xv[TDQ_MAXD];
-#pragma unroll
-    for (int j = 0; j < TDQ_MAXD; ++j) xv[j] = j < d.d_in ? xrow[j] : 0.f;
-    constexpr int KBr = WT / 2, NSTEPr = WT * KBr;
-    constexpr int RHN = RH_LDS ? 1 : S, RKB = RH_LDS ? 1 : KBr;  // register copy only without RH_LDS
-    bf16x8 rh[RHN][RKB], rl[RHN][RKB];
-    // wave-private LDS fragment set ([s][kb][lane] bf16x8, RH_LDS)
-    bf16x8* rlds = reinterpret_cast<bf16x8*>(lds + RH0) + (size_t)w * (S * KBr * 64);
-    if (Lh >= 2) {
-      const Tl Hq = hs_region<WT, LO>(Hs, Lh >= 3 ? Lh - 2 : 0, nwg_f, wg_f, S, w_f, l);
-      bf16x4 qh[S], ql[S];
-#pragma unroll
-      for (int t = 0; t < WT; ++t) {
-        f32x4 hq[S];
-        if (Lh == 2) {
-          h0_jet<WT, S, NSO>(sp, aux, d, xv, t, g, hq);
-        } else {
-#pragma unroll
-          for (int s = 0; s < S; ++s) hq[s] = hs_load_c<WT, LO>(Hq, s, t);
-        }
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          bf16x4 hi, lo;
-          split_or_round<LO>(hq[s], hi, lo);
-          if (t & 1) {
-            if constexpr (RH_LDS) {
-              rlds[(s * KBr + (t >> 1)) * 64 + l] = cat8(qh[s], hi);
-            } else {
-              rh[s][t >> 1] = cat8(qh[s], hi);
-              if constexpr (LO) rl[s][t >> 1] = cat8(ql[s], lo);
-            }
-          } else {
-            qh[s] = hi;
-            if constexpr (LO) ql[s] = lo;
-          }
-        }
-      }
-    }
-    const Tl Wt = tl_make(Fimg + (size_t)(Lh >= 2 ? Lh - 2 : 0) * NSTEPr * 128, l);
-    const float* bt = aux + aux_bh(d, W) + (Lh >= 2 ? Lh - 2 : 0) * W;
-#else
     constexpr int DH = WT < 3 ? WT : 3;  // H tiles in flight
     f32x4 hr[DH][S];
 #pragma unroll
     for (int k = 0; k < DH; ++k) h_tile<S, WT, LO>(hr[k], Hl, k);
-#endif
     bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
       f32x4 h[S];
-#if TDQ_RECOMPUTE_TOP
-      if (Lh >= 2) {  // z = W_{Lh-1} h_{Lh-2} + b: the forward's MFMA order (k-blocks ascending)
-        f32x4 z[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) z[s] = zero4();
-#pragma unroll
-        for (int kb = 0; kb < KBr; ++kb) {
-          bf16x8 Ah, Al;
-          img_frag<LO>(Wt, t * KBr + kb, Ah, Al);
-#pragma unroll
-          for (int s = 0; s < S; ++s) {
-            if constexpr (RH_LDS) {  // wave-private: program order suffices
-              const bf16x8 B = rlds[(s * KBr + kb) * 64 + l];
-              z[s] = mfma_w<LO>(Ah, Al, B, B, z[s]);
-            } else {
-              z[s] = mfma_w<LO>(Ah, Al, rh[s][kb], rl[s][kb], z[s]);
-            }
-          }
-        }
-        z[0] += *reinterpret_cast<const f32x4*>(bt + 16 * t + 4 * g);
-        tanh_jet_f<S, NSO>(sp, z, h);
-      } else {  // Lh = 1: layer 0 is saved whole (save_all); a plain load keeps registers free
-#pragma unroll
-        for (int s = 0; s < S; ++s) h[s] = hs_load<WT, LO>(Hl, s, t);
-      }
-#else
 #pragma unroll
       for (int s = 0; s < S; ++s) h[s] = hr[t % DH][s];
       if (t + DH < WT) h_tile<S, WT, LO>(hr[t % DH], Hl, t + DH);
-#endif
       // hb = Ko ub over the zero-padded 4 output columns: no branches
       f32x4 hbt[S];
 #pragma unroll
@@ -1353,9 +1258,7 @@ inline int h0_recompute() {
 inline size_t bwd_bf3_lds(int WT, int S, bool lo) {
   const int W = 16 * WT, hl = lo ? 2 : 1, nwv = bwd_waves(WT, lo, S);
   const size_t u1 = (size_t)(lo ? 1 : 2) * (2 * hl * 16 * nwv * 144) / 2,
-               u2a = bf3_gstage(WT, S, lo) ? 0 : (size_t)nwv * S * WT * hl * 128,
-               u3 = (TDQ_RECOMPUTE_TOP && !lo) ? (size_t)nwv * W * TDQ_MAXO + (size_t)nwv * S * WT * 128 : 0,
-               u2 = u2a > u3 ? u2a : u3;
+               u2 = bf3_gstage(WT, S, lo) ? 0 : (size_t)nwv * S * WT * hl * 128;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
   return (u + 3 * nwv * W) * sizeof(float);
 }
@@ -1374,7 +1277,6 @@ struct Bf3Args {
   hipStream_t st;
   int lo;            // 1: bf16x3 (operands hi + lo), 0: bf16 (operands rounded to bf16)
   bf16x4* gstage;    // wide bf16x3 plans: global fragment stage (bf3_gstage), else unused
-  const bf16x8* fimg;  // bwd: the forward's weight images (TDQ_RECOMPUTE_TOP)
   // point range [p_lo, p_hi) of this launch (p_lo a multiple of 128, p_hi one too or = N): the
   // kernels index J / dJ, the saved activations and the slabs of the whole set N, so launches
   // over disjoint ranges may run concurrently (separate streams) into the same buffers
@@ -1416,8 +1318,7 @@ int launch_bwd_bf3_lo(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_bwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(64 * NWV), lds, a.st, a.X, a.aux, a.img, a.dJ,
-                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute(), a.gstage, a.fimg,
-                     wg0);
+                     a.Hs, a.slab, a.N, a.Ptot, a.d, a.sp, bwd_reverse_order(), h0_recompute(), a.gstage, wg0);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -422,7 +422,7 @@ int tdq_jet_fwd_bf3_range(const float* X, const float* P, float* J, float* scrat
     if (rc) return rc;
   }
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
-            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), nullptr, p_lo, p_hi};
+            scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), p_lo, p_hi};
   return dispatch(true, WT, S, nso, a);
 }
 
@@ -473,7 +473,7 @@ int tdq_jet_bwd_bf3_range(const float* X, const float* dJ, const float* Hs, floa
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), work, N,
             slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo),
-            reinterpret_cast<const bf16x8*>(img), p_lo, p_hi};
+            p_lo, p_hi};
   return dispatch(false, WT, S, nso, a);
 }
 

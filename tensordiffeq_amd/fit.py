@@ -354,7 +354,7 @@ class AdamEngine:
                 self._graph_saved = self._tail_saved
         else:
             tail = self._tail_eligible()
-            if self.dist.graph_collectives:
+            if self._coll_in_graph():
                 # RCCL: the bucket all-reduce is captured in the step graph - one replay per step
                 g = torch.cuda.CUDAGraph()
                 with capture_graph(g, pool=pool):
@@ -450,6 +450,15 @@ class AdamEngine:
                     loss = self._tail_step(in_graph=True)
         self.graph_k, self.static_loss_k, self._k = g, loss, k
 
+    def _bucket_floats(self):
+        """Upper bound of the per-step DP bucket: every reduced gradient + loss + terms."""
+        return sum(self.wrt[i].numel() for i in self.red_idx) + 1 + len(self.term_names)
+
+    def _coll_in_graph(self):
+        """Capture the bucket all-reduce inside the step graph (RCCL, or the peer kernel when it
+        takes a bucket of this size; ADVICE r3: a gloo fallback must never be captured)."""
+        return self.dist.capturable(self._bucket_floats())
+
     def _replay(self):
         self.graph_a.replay()
         if self.graph_b is not None:
@@ -513,7 +522,7 @@ class AdamEngine:
         """Steps per multi-step graph (``TDQ_STEP_UNROLL``, default 8): fused-tail steps, single
         process or DP with the all-reduce captured in the graph (RCCL / peer); 1 = one graph per
         step."""
-        if not self._tail_eligible() or (self.dist.is_distributed and not self.dist.graph_collectives):
+        if not self._tail_eligible() or (self.dist.is_distributed and not self._coll_in_graph()):
             return 1
         return max(1, int(os.environ.get("TDQ_STEP_UNROLL", "8")))
 
@@ -734,7 +743,9 @@ class LossGradEngine:
         with torch.no_grad():
             self.flat.copy_(x)
         use_graph = _use_graphs(self.flat.device)
-        in_graph = self.dist.graph_collectives   # the all-reduce is captured with the evaluation
+        # the all-reduce is captured with the evaluation (RCCL, or the peer kernel if it takes
+        # the [grad | loss] buffer)
+        in_graph = self.dist.capturable(self.flat.numel() + 1)
         if use_graph and self.graph is None and self.n_evals >= 1:
             stream = torch.cuda.Stream(device=self.flat.device)
             stream.wait_stream(torch.cuda.current_stream(self.flat.device))
@@ -757,6 +768,10 @@ class LossGradEngine:
         self.n_evals += 1
         if self.dist.is_distributed and not reduced:
             self.dist.all_reduce_(buf)
+        if in_graph and self.dist.peer is not None and self.n_evals % 32 == 0:
+            # a peer all-reduce that timed out inside the replayed graph summed stale slots: raise
+            # instead of handing the optimizer a corrupted gradient
+            self.dist.check_health()
         return buf[-1], buf[:-1]
 
 

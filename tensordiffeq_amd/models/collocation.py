@@ -103,7 +103,7 @@ class CollocationSolverND:
             from ..utils.seeding import set_seed
             set_seed(seed)
         self.dist = bool(dist)
-        self.dist_ctx = pdist.init_distributed() if dist else pdist.get_context(device)
+        self.dist_ctx = pdist.init_distributed(auto_launch=True) if dist else pdist.get_context(device)
         self.device = torch.device(device) if device is not None else (
             self.dist_ctx.device if dist else default_device())
         self.tf_optimizer = Adam(lr=0.005, beta_1=0.99)
@@ -500,6 +500,7 @@ class CollocationSolverND:
             from ..optimizers import lbfgs_device
 
             def on_poll(opt):
+                ctx.check_health()   # a peer all-reduce timeout inside the L-BFGS graph
                 it = opt.n_iter
                 f = float(opt.st[lbfgs_device.F])
                 if self.metrics is not None:
@@ -510,10 +511,11 @@ class CollocationSolverND:
 
             opt = lbfgs_device.minimize(eng.evaluate_fg, flat.data, newton_iter, lr=0.8,
                                         all_reduce=ctx.all_reduce_ if ctx.is_distributed else None,
-                                        capture_all_reduce=ctx.graph_collectives,
+                                        capture_all_reduce=ctx.capturable(flat.numel() + 1),
                                         use_graph=_use_graphs(self.device),
                                         poll_every=max(1, min(int(self.log_every), 64)), on_poll=on_poll,
                                         stop=stop)
+            ctx.check_health()
             with torch.no_grad():
                 flat.copy_(opt.best_x)
             self.min_loss["l-bfgs"] = opt.min_loss
@@ -526,6 +528,7 @@ class CollocationSolverND:
             x, _, fe, best_w, min_loss, best_epoch = eager_lbfgs(
                 eng, flat.detach().clone(), state=state, maxIter=newton_iter, learningRate=0.8, on_eval=on_eval,
                 stop=stop)
+            ctx.check_health()
             with torch.no_grad():
                 flat.copy_(best_w)
             self.min_loss["l-bfgs"] = float(min_loss)
@@ -534,6 +537,7 @@ class CollocationSolverND:
                     "reason": getattr(state, "reason", "?")}
         else:
             x, _ = graph_lbfgs(eng, flat.detach().clone(), newton_iter, on_eval=on_eval)
+            ctx.check_health()
             with torch.no_grad():
                 flat.copy_(x)
             f, _ = eng(flat.detach().clone())

@@ -47,7 +47,7 @@ class DiscoveryModel:
         if seed is not None:
             from ..utils.seeding import set_seed
             set_seed(seed)
-        self.dist_ctx = pdist.init_distributed() if dist else pdist.get_context(device)
+        self.dist_ctx = pdist.init_distributed(auto_launch=True) if dist else pdist.get_context(device)
         self.device = torch.device(device) if device is not None else (
             self.dist_ctx.device if dist else default_device())
         ctx = self.dist_ctx

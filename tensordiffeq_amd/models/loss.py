@@ -194,6 +194,9 @@ class LossProgram:
                     raise RuntimeError("HIP jet backend unavailable: " + why)
         self.backend = backend
         self.reasons = reasons
+        if backend == "autograd" and self.requested_backend == "auto" and isinstance(self.net, TanhMLP):
+            _warn_once("the loss callables run on the nested-autograd path (one to two orders of magnitude "
+                       "slower than the jet kernels): " + "; ".join(reasons or ["not jet-expressible"]))
 
     def _validate_jet(self, recorded, requests):
         """Re-run every recorded callable in a :class:`~tensordiffeq_amd.autodiff.JetContext` on
@@ -418,6 +421,18 @@ class LossProgram:
             o = o if isinstance(o, (tuple, list)) else (o,)
             outs.append([x.detach().reshape(Xc.shape[0], -1) for x in o])
         return [torch.cat([c[i] for c in outs], dim=0) for i in range(len(outs[0]))] if outs else []
+
+
+_WARNED = set()
+
+
+def _warn_once(msg):
+    """One warning per distinct message per process (a fallback is decided once per program,
+    but solvers rebuild programs per precision / minibatch)."""
+    import warnings
+    if msg not in _WARNED:
+        _WARNED.add(msg)
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
 def _as_list(o):

@@ -96,11 +96,9 @@ def hip_config(net, plan, precision=None):
     if precision == "fp32" and S * WT > 32:
         return layered(f"fp32 with streams x width tiles = {S * WT} > 32")
     if precision == "fp32" and not uniform:
-        # the split-bf16 kernels pad unequal hidden layers to the widest; the exact-fp32 family
-        # takes equal widths only
-        if WT < 2:
-            return layered("unequal hidden widths <= 16 in fp32")
-        precision = "bf16x3"
+        # the exact-fp32 fused family takes equal widths only; unequal widths keep the requested
+        # precision on the layer-wise engine (no silent switch to split-bf16)
+        return layered("unequal hidden widths in fp32")
     return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
             "n_hidden": len(hidden), "precision": precision}
 

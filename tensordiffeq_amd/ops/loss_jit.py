@@ -208,12 +208,27 @@ def generate(op):
     return "\n".join(out) + "\n"
 
 
+def device_arch():
+    """hipRTC target: the current device's ISA (``gcnArchName`` without feature suffixes), else
+    ``TDQ_OFFLOAD_ARCH`` (what ``csrc/build.py`` compiles the library for), else gfx950."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            name = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+            if name:
+                return name.split(":")[0]
+    except Exception:  # noqa: BLE001 - fall through to the build setting
+        pass
+    return os.environ.get("TDQ_OFFLOAD_ARCH", "gfx950")
+
+
 class LossKernel:
     """A compiled specialized loss kernel (module + function handle), launched like the
     interpreter over any block range."""
 
-    def __init__(self, src, arch="gfx950"):
+    def __init__(self, src, arch=None):
         lib = _lib.load(required=True)
+        arch = arch or device_arch()
         key = hashlib.sha256((arch + src).encode()).hexdigest()
         if key not in _CACHE:
             code, size = ctypes.c_void_p(0), ctypes.c_longlong(0)

@@ -24,6 +24,8 @@ import math
 
 import torch
 
+from ..config import DEFAULT_LBFGS_STOP as DEFAULT_STOP
+
 
 class Struct:
     """Lua-like struct: missing attributes read as 0 (reference optimizers.py:312-320)."""
@@ -84,7 +86,7 @@ def compact_direction(g, hist, hdiag):
 
 
 def eager_lbfgs(opfunc, x, state=None, maxIter=100, learningRate=1.0, do_verbose=True,
-                nCorrection=50, tolFun=1e-12, tolX=1e-12, progress=None, on_eval=None, stop="fixed"):
+                nCorrection=50, tolFun=1e-12, tolX=1e-12, progress=None, on_eval=None, stop=DEFAULT_STOP):
     """Reference-semantics L-BFGS.  Returns ``(x, f_hist, funcEval, best_w, min_loss, best_epoch)``;
     ``state.reason`` / ``state.nIter`` record why and when it stopped.  ``stop="legacy"``: the
     reference's effective function-change test ``|f| < tolX`` (optimizers.py:273) instead of
@@ -191,4 +193,8 @@ class LBFGSWolfe:
 
 
 def graph_lbfgs(loss_and_grad, x0, max_iterations, tolerance=1e-20, history_size=10, on_eval=None):
+    """Strong-Wolfe L-BFGS (the reference's TFP path, fit.py:115-122).  Like
+    ``tfp.optimizer.lbfgs_minimize`` it has no function-change stop: it runs until
+    ``max_iterations`` or a gradient below ``tolerance``, so the ``stop`` rule of the eager /
+    device L-BFGS does not apply here."""
     return LBFGSWolfe(history_size, tolerance).minimize(loss_and_grad, x0, max_iterations, on_eval)

@@ -28,6 +28,8 @@ import math
 
 import torch
 
+from ..config import DEFAULT_LBFGS_STOP as DEFAULT_STOP
+
 from ..graphs import capture_graph
 from ..ops import _lib
 
@@ -56,7 +58,7 @@ class DeviceLBFGS:
     """L-BFGS state for a flat fp32 parameter vector ``x`` (updated in place by :meth:`axpy`)."""
 
     def __init__(self, x, m=50, max_iter=100, lr=0.8, tol_fun=1e-12, tol_x=1e-12, max_eval=None,
-                 record_history=True, stop="fixed"):
+                 record_history=True, stop=DEFAULT_STOP):
         if not (1 <= m <= MAXM):
             raise ValueError(f"history size must be in [1, {MAXM}]")
         if stop not in STOP_MODES:
@@ -298,7 +300,7 @@ class DeviceLBFGS:
 
 
 def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, all_reduce=None,
-             use_graph=None, poll_every=32, on_poll=None, capture_all_reduce=False, stop="fixed"):
+             use_graph=None, poll_every=32, on_poll=None, capture_all_reduce=False, stop=DEFAULT_STOP):
     """Run device L-BFGS on ``x`` (in place) for at most ``max_iter`` iterations.
 
     ``evaluate()`` returns ``fg = [grad | loss]`` at the current ``x`` (a float32 device vector;

@@ -58,6 +58,16 @@ class DistContext:
         return (self.is_distributed and (self.backend == "nccl" or self.peer is not None)
                 and self.device.type == "cuda" and os.environ.get("TDQ_DP_GRAPH", "1") != "0")
 
+    def capturable(self, n_floats):
+        """Whether an all-reduce of ``n_floats`` fp32 may be captured in a HIP graph: RCCL always;
+        under another backend (the gloo rehearsal) only when the peer kernel takes the buffer -
+        a larger one would fall back to a host collective, which cannot run inside a capture."""
+        if not self.graph_collectives:
+            return False
+        if self.backend == "nccl":
+            return True
+        return self.peer is not None and int(n_floats) <= self.peer.cap
+
     def barrier(self):
         if self.is_distributed:
             if self.backend == "nccl":
@@ -91,6 +101,9 @@ class DistContext:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def min_scalar(self, v):
+        return -self.max_scalar(-float(v))
+
     def __repr__(self):
         return (f"DistContext(rank={self.rank}, world={self.world}, device={self.device}, "
                 f"backend={self.backend})")
@@ -116,13 +129,82 @@ def _free_port():
     return port
 
 
-def init_distributed(backend=None, device=None, timeout_s=600, force=None):
+def launcher_env():
+    """True when a launcher (torchrun / torch.distributed.run / an MPI-style wrapper) already
+    set up this process as one rank."""
+    return "WORLD_SIZE" in os.environ
+
+
+def visible_devices():
+    """Number of GPUs this process could use.  ``torch.cuda.device_count()`` does not
+    initialise the HIP runtime, so this is safe before a self-launch (``TDQ_DIST_NPROC``
+    overrides: tests rehearse the self-launch on CPU ranks)."""
+    env = os.environ.get("TDQ_DIST_NPROC")
+    if env:
+        return int(env)
+    return torch.cuda.device_count()
+
+
+def self_launch(nproc, argv=None, env=None):
+    """Run the current program as ``nproc`` ranks of one node and return their exit code.
+
+    The reference's ``compile(..., dist=True)`` uses every visible GPU from a plain ``python``
+    process (``tf.distribute.MirroredStrategy``, tensordiffeq/models.py:230-243).  Here DP is
+    one process per GPU, so a plain process that asks for DP re-runs its own script under
+    ``torch.distributed.run`` as CHILD processes (never ``exec``: this process may already hold
+    the GPU), streams their output through and exits with their code.  Rendezvous on
+    127.0.0.1 with a free port."""
+    import subprocess
+    import sys
+    argv = list(sys.argv if argv is None else argv)
+    if not argv or not argv[0] or argv[0] == "-c" or not os.path.exists(argv[0]):
+        raise RuntimeError("cannot self-launch ranks: the program was not started from a script file; "
+                           "use 'python -m torch.distributed.run --nproc-per-node N script.py'")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(nproc)}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + argv
+    child_env = dict(os.environ if env is None else env)
+    child_env["TDQ_SELF_LAUNCHED"] = "1"
+    child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    child_env.pop("TDQ_DIST_NPROC", None)
+    r = subprocess.run(cmd, env=child_env)
+    return r.returncode
+
+
+def maybe_self_launch(n=None, why="dist=True"):
+    """Relaunch as ``n`` ranks (default: every visible device) when no launcher set this process
+    up and more than one device is visible; returns normally only when this process should go
+    on at world 1 (it prints why).  ``TDQ_DIST_AUTOLAUNCH=0`` disables the relaunch."""
+    import sys
+    import warnings
+    if launcher_env() or os.environ.get("TDQ_SELF_LAUNCHED") == "1":
+        return
+    n = visible_devices() if n is None else int(n)
+    if n <= 1:
+        warnings.warn(f"{why}: one visible device and no launcher - training at world 1 "
+                      "(launch with 'torch.distributed.run --nproc-per-node N' for N ranks)", stacklevel=3)
+        return
+    if os.environ.get("TDQ_DIST_AUTOLAUNCH", "1") == "0":
+        warnings.warn(f"{why}: {n} devices visible but TDQ_DIST_AUTOLAUNCH=0 and no launcher - training at "
+                      "world 1", stacklevel=3)
+        return
+    print(f"[tensordiffeq_amd] {why}: launching {n} ranks (one per device) with torch.distributed.run",
+          file=sys.stderr, flush=True)
+    sys.stdout.flush()
+    rc = self_launch(n)
+    sys.exit(rc)
+
+
+def init_distributed(backend=None, device=None, timeout_s=600, force=None, auto_launch=False):
     """Initialise (once) from the torchrun environment; returns the process' DistContext.
-    ``force`` (default ``TDQ_FORCE_DP``): build the process group even at world 1."""
+    ``force`` (default ``TDQ_FORCE_DP``): build the process group even at world 1.
+    ``auto_launch``: with no launcher and several visible devices, re-run this program as one
+    rank per device first (:func:`maybe_self_launch`; the solver's ``compile(dist=True)``)."""
     global _CTX
     if _CTX is not None:
         return _CTX
     force = force_dp_requested() if force is None else bool(force)
+    if auto_launch and not force:
+        maybe_self_launch()
     world = env_world()
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))

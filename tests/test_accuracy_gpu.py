@@ -39,11 +39,20 @@ def test_burgers_reference_schedule_l2():
 
 @pytest.mark.timeout(300)
 def test_ac_sa_reference_schedule_l2():
-    """Allen-Cahn SA-PINN [2,128x4,1], N_f 50k, Adam 10k (bf16) + L-BFGS 10k (bf16x3), seed 0:
-    L2 < 3e-2 (SA-PINN paper: 2.1e-2), and L-BFGS ran the reference's full 10k iterations."""
-    res = _example("AC-SA").main(["--device", "cuda", "--quiet", "--precision", "bf16",
-                                  "--newton-precision", "bf16x3", "--seed", "0"])
-    print(f"ACCURACY ac-sa l2 {res['l2_error']:.3e} lbfgs {res['lbfgs_n_iter']} {res['lbfgs_reason']}")
-    assert res["backend"] == "hip"
-    assert res["l2_error"] < 3e-2, res
-    assert res["lbfgs_n_iter"] == 10000
+    """Allen-Cahn SA-PINN [2,128x4,1], N_f 50k, Adam 10k (bf16) + L-BFGS 10k (bf16x3), seeds 0-2:
+    the MEDIAN L2 < 3e-2 (SA-PINN paper: 2.1e-2; measured 2.04-2.54e-2 over seeds 0-2, up to 3.2e-2
+    over seeds 3-5 - a single-seed bound would fit one seed rather than the method), every seed
+    < 4.5e-2, and L-BFGS ran the reference's full 10k iterations (~7 s per seed)."""
+    l2s = []
+    for seed in (0, 1, 2):
+        res = _example("AC-SA").main(["--device", "cuda", "--quiet", "--precision", "bf16",
+                                      "--newton-precision", "bf16x3", "--seed", str(seed)])
+        print(f"ACCURACY ac-sa seed {seed} l2 {res['l2_error']:.3e} lbfgs {res['lbfgs_n_iter']} "
+              f"{res['lbfgs_reason']}", flush=True)
+        assert res["backend"] == "hip"
+        assert res["lbfgs_n_iter"] == 10000
+        l2s.append(res["l2_error"])
+    med = sorted(l2s)[1]
+    print(f"ACCURACY ac-sa median l2 {med:.3e}")
+    assert med < 3e-2, l2s
+    assert max(l2s) < 4.5e-2, l2s

@@ -67,3 +67,72 @@ def test_bench_two_ranks_gloo_json():
     rec = _last_json(r.stdout)
     _check(rec, 2)
     assert rec["allreduce"]["impl"] == "torch.distributed"     # CPU ranks: no peer all-reduce
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launch_two_ranks_json():
+    """``python bench.py --gpus 2`` with no launcher: bench.py re-runs itself as 2 ranks (child
+    processes under torch.distributed.run) and relays rank 0's single JSON line."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL, capture_output=True,
+                       text=True, env=_env(), timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    _check(rec, 2)
+    assert rec["rank_ms_per_step"]["min"] <= rec["rank_ms_per_step"]["max"]
+    assert rec["allreduce"]["replay"]["us_per_call"] > 0
+    assert rec["allreduce"]["replay"]["mode"] == "host-launched"    # gloo keeps it out of graphs
+
+
+SCRIPT_DIST = r'''
+import os, sys, json
+import numpy as np, torch
+import tensordiffeq_amd as tdq
+from tensordiffeq_amd.boundaries import DomainND, dirichletBC
+D = DomainND(["x", "t"], time_var="t")
+D.add("x", [-1.0, 1.0], 16); D.add("t", [0.0, 1.0], 8)
+tdq.set_seed(0)
+D.generate_collocation_points(256)
+def f_model(u_model, x, t):
+    u = u_model(torch.cat([x, t], 1))
+    return tdq.grad(u, t) - 0.1 * tdq.grad(tdq.grad(u, x), x)
+bcs = [dirichletBC(D, val=0.0, var="x", target="upper")]
+m = tdq.CollocationSolverND(verbose=False)
+m.compile([2, 8, 8, 1], f_model, D, bcs, dist=True, seed=0)
+m.fit(tf_iter=3)
+ctx = m.dist_ctx
+with open(os.path.join(os.environ["OUT_DIR"], f"rank{ctx.rank}.json"), "w") as f:
+    json.dump({"rank": ctx.rank, "world": ctx.world, "dist": ctx.is_distributed,
+               "loss": m.losses[-1]["Total Loss"]}, f)
+'''
+
+
+@pytest.mark.timeout(300)
+def test_compile_dist_true_self_launches(tmp_path):
+    """Reference semantics (models.py:230-243, MirroredStrategy): ``compile(dist=True)`` in a plain
+    ``python`` process trains on every visible device.  Here the script is re-run as one rank per
+    device; TDQ_DIST_NPROC stands in for two visible devices on the CPU."""
+    p = tmp_path / "dist_script.py"
+    p.write_text(SCRIPT_DIST)
+    env = _env()
+    env["TDQ_DIST_NPROC"] = "2"
+    env["OUT_DIR"] = str(tmp_path)
+    r = subprocess.run([sys.executable, str(p)], capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(q.read_text()) for q in sorted(tmp_path.glob("rank*.json"))]
+    assert sorted(x["rank"] for x in recs) == [0, 1], r.stdout
+    assert all(x["world"] == 2 and x["dist"] for x in recs)
+    assert recs[0]["loss"] == pytest.approx(recs[1]["loss"], rel=1e-6)
+
+
+@pytest.mark.timeout(300)
+def test_compile_dist_true_one_device_warns(tmp_path):
+    """With one (here: no) visible device and no launcher, dist=True says that it trains at world 1."""
+    p = tmp_path / "dist_script.py"
+    p.write_text(SCRIPT_DIST)
+    env = _env()
+    env["OUT_DIR"] = str(tmp_path)
+    r = subprocess.run([sys.executable, str(p)], capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "training at world 1" in r.stderr
+    recs = [json.loads(q.read_text()) for q in sorted(tmp_path.glob("rank*.json"))]
+    assert len(recs) == 1 and recs[0]["world"] == 1 and not recs[0]["dist"]

@@ -92,7 +92,7 @@ def test_jet_gradients_match_autograd():
 
 def test_hip_config_unequal_widths():
     """Unequal hidden widths are served by the split-bf16 kernels (padded to the widest layer);
-    an exact-fp32 request with unequal widths is promoted to bf16x3."""
+    an exact-fp32 request with unequal widths keeps fp32 on the layer-wise engine."""
     from tensordiffeq_amd.jet import JetPlan
     from tensordiffeq_amd.models.networks import TanhMLP
     from tensordiffeq_amd.ops.jet_mlp import hip_config
@@ -100,7 +100,8 @@ def test_hip_config_unequal_widths():
     plan = JetPlan([(0,), (1,), (0, 0)], 2)
     cfg = hip_config(net, plan, "bf16")
     assert cfg["WT"] == 8 and cfg["widths"] == (64, 128, 32) and cfg["width"] == 128
-    assert hip_config(net, plan, "fp32")["precision"] == "bf16x3"
+    cfg32 = hip_config(net, plan, "fp32")
+    assert cfg32["precision"] == "fp32" and cfg32["engine"] == "layered" and "unequal" in cfg32["why"]
     cfg = hip_config(TanhMLP([2, 128, 128, 128, 128, 1], device="cpu"), JetPlan([(0, 0), (1, 1)], 2), "bf16")
     assert cfg["S"] == 5 and cfg["WT"] == 8   # a wide plan
 
