@@ -56,9 +56,11 @@ PRECISION_NOTES = {
 
 
 def build_problem(n_glob, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
-                  lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1)):
+                  lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1), problem="ac-sa"):
     """The AC-SA problem of BASELINE.json with ``n_glob`` collocation points in total (sharded over
-    ``world`` ranks when ``dist``)."""
+    ``world`` ranks when ``dist``).  ``problem="ac-baseline"``: the reference's AC-baseline /
+    AC-dist-new program instead (examples/AC-baseline.py:14-52, AC-dist-new.py:14-48): no
+    self-adaptive weights, periodic BC on u, u_x, u_xxx and u_xxxx."""
     import tensordiffeq_amd as tdq
     from tensordiffeq_amd.boundaries import DomainND, IC, periodicBC
 
@@ -76,6 +78,14 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
         u_x = tdq.grad(u, x)
         return u, u_x
 
+    def deriv_model4(u_model, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        u_x = tdq.grad(u, x)
+        u_xx = tdq.grad(u_x, x)
+        u_xxx = tdq.grad(u_xx, x)
+        u_xxxx = tdq.grad(u_xxx, x)
+        return u, u_x, u_xxx, u_xxxx
+
     def f_model(u_model, x, t):
         u = u_model(torch.cat([x, t], 1))
         u_x = tdq.grad(u, x)
@@ -84,6 +94,12 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
         return u_t - 0.0001 * u_xx + 5.0 * u * u * u - 5.0 * u
 
     init = IC(D, [func_ic], var=[["x"]])
+    if problem == "ac-baseline":
+        model = tdq.CollocationSolverND(verbose=False)
+        model.compile(list(layers), f_model, D, [init, periodicBC(D, ["x"], [deriv_model4])],
+                      backend=backend, device=device, dist=dist, precision=precision,
+                      newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+        return model
     x_periodic = periodicBC(D, ["x"], [deriv_model])
     g = torch.Generator().manual_seed(99 if seed == 1234 else seed)
     init_weights = {"residual": [torch.rand(n_glob, 1, generator=g)],
@@ -193,13 +209,13 @@ def allreduce_replay_us(ctx, n_floats, calls=10, reps=20):
     return {"us_per_call": round(ctx.max_scalar(us), 2), "floats": int(n_floats), "mode": mode}
 
 
-def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop):
+def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop, problem="ac-sa"):
     """Reference AC-SA schedule per seed (examples/AC-SA.py:9-88): L2 on AC.mat, phase times,
     L-BFGS stop reason."""
     out = []
     for sd in seeds:
         m = build_problem(50000, 1, backend, device, False, precision, seed=sd,
-                          newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+                          newton_precision=newton_precision, lbfgs_stop=lbfgs_stop, problem=problem)
         m.fit(tf_iter=iters)
         m.fit(newton_iter=newton)
         info = m.fit_info
@@ -234,6 +250,9 @@ def forced_dp_timing(n_glob, backend, device, precision, steps, warmup, min_warm
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--problem", default="ac-sa", choices=["ac-sa", "ac-baseline"],
+                    help="ac-sa: the BASELINE.json flagship (examples/AC-SA.py); ac-baseline: the reference's "
+                         "AC-baseline / AC-dist-new program (no SA weights, periodic u, u_x, u_xxx, u_xxxx)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--min-warmup-s", type=float, default=1.0,
@@ -286,7 +305,8 @@ def main(argv=None):
         divs = [k for k in range(16, 3, -1) if args.steps % k == 0]
         os.environ["TDQ_STEP_UNROLL"] = str(8 if args.steps % 8 == 0 else (divs[0] if divs else 8))
     layers = tuple(int(v) for v in args.layers.split(","))
-    model = build_problem(n_glob, world, args.backend, device, dist, args.precision, layers=layers)
+    model = build_problem(n_glob, world, args.backend, device, dist, args.precision, layers=layers,
+                          problem=args.problem)
     eng = model._get_engine(None, args.warmup + args.steps + 2)
     backend = model.active_backend
     elapsed, n_warm, warm_s = time_steps(eng, ctx, device, args.steps, args.warmup, args.min_warmup_s)
@@ -309,7 +329,7 @@ def main(argv=None):
     if not args.no_l2 and world == 1 and args.acc_seeds:
         try:
             acc = accuracy_runs(args.acc_seeds, device, args.backend, args.precision, args.newton_precision,
-                                args.acc_iters, args.acc_newton, args.lbfgs_stop)
+                                args.acc_iters, args.acc_newton, args.lbfgs_stop, problem=args.problem)
         except Exception as e:  # pragma: no cover - reported, never hides the throughput number
             acc_err = f"{type(e).__name__}: {e}"
     dp = None
@@ -334,11 +354,14 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16" if (backend == "hip" and args.precision != "fp32") else "fp32",
             "data": "synthetic (LHS collocation points, random Keras-init weights); L2 on data/AC.mat",
-            "config": {"model": f"Allen-Cahn SA-PINN tanh MLP [{','.join(map(str, layers))}]",
+            "config": {"model": (f"Allen-Cahn SA-PINN tanh MLP [{','.join(map(str, layers))}]" if args.problem == "ac-sa"
+                                 else f"Allen-Cahn baseline PINN tanh MLP [{','.join(map(str, layers))}]"),
+                       "problem": args.problem,
                        "global_batch": n_glob, "seq_len": None, "parallelism": f"dp{world}",
                        "points_per_gpu": n_glob // world, "backend": backend,
                        "precision": PRECISION_NOTES[args.precision] if backend == "hip" else "fp32",
-                       "bc_points": "IC 512 (SA) + periodic 2x201 (u, u_x)"},
+                       "bc_points": ("IC 512 (SA) + periodic 2x201 (u, u_x)" if args.problem == "ac-sa" else
+                                     "IC 512 + periodic 2x201 (u, u_x, u_xxx, u_xxxx; order 3/4 on jet_hi.hip)")},
             "warmup_steps_run": n_warm,
             "warmup_s": round(warm_s, 3),
             "loss_after": loss,

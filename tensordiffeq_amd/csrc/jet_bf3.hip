@@ -145,14 +145,15 @@ __global__ void __launch_bounds__(256) tail_reduce1_kernel(const float* __restri
                    tb.improved, tb.cnt);
 }
 
+// gx (optional): a second gradient added element-wise (the high-order points' part, jet_hi.hip)
 __global__ void __launch_bounds__(256) slab_reduce2_bf3(const float* __restrict__ part, float* __restrict__ grad, int P,
-                                                        int Pst, int chunks) {
+                                                        int Pst, int chunks, const float* __restrict__ gx) {
   const int q = blockIdx.x * 256 + threadIdx.x;
   if (4 * q >= P) return;
   const f32x4 a = slab_reduce2_sum(part, Pst, chunks, q);
 #pragma unroll
   for (int e = 0; e < 4; ++e)
-    if (4 * q + e < P) grad[4 * q + e] = a[e];
+    if (4 * q + e < P) grad[4 * q + e] = gx != nullptr ? a[e] + gx[4 * q + e] : a[e];
 }
 
 struct TailImg {
@@ -219,10 +220,12 @@ __device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti)
 #if TDQ_TAIL_ELEM
 // Adam over every group, one ELEMENT per thread (args.start in elements); group 0 = theta, whose
 // gradient is the second slab pass of its column (the f32x4 pass's summation order, so the
-// result is bit-identical), written to args.grp[0].g as well
+// result is bit-identical) plus gx[e] when given (the high-order points' gradient, jet_hi.hip),
+// written to args.grp[0].g as well
 __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const float* __restrict__ part, int Pst,
                                                         int chunks, const int* __restrict__ improved,
-                                                        float* __restrict__ snap, TailImg ti) {
+                                                        float* __restrict__ snap, TailImg ti,
+                                                        const float* __restrict__ gx) {
   const bool do_snap = snap != nullptr && *improved != 0;
   const int64_t total = args.start[args.ngroups];
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
@@ -240,6 +243,7 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
       }
       if (c < chunks) a0 += part[(size_t)c * Pst + e];
       g = a0 + a1;
+      if (gx != nullptr) g += gx[e];
       const_cast<float*>(gr.g)[e] = g;
     } else {
       g = gr.g[e];
@@ -259,7 +263,8 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
 // column (slot == column), written to args.grp[0].g as well
 __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const float* __restrict__ part, int Pst,
                                                         int chunks, const int* __restrict__ improved,
-                                                        float* __restrict__ snap, TailImg ti) {
+                                                        float* __restrict__ snap, TailImg ti,
+                                                        const float* __restrict__ gx) {
   const bool do_snap = snap != nullptr && *improved != 0;
   const int64_t total = args.start[args.ngroups];
   for (int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x; slot < total; slot += (int64_t)gridDim.x * 256) {
@@ -272,7 +277,12 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
     float* gout = const_cast<float*>(gr.g);
     const bool red = th && part != nullptr;  // theta gradient from the slab partials (else: gr.g)
     f32x4 g = zero4();
-    if (red) g = slab_reduce2_sum(part, Pst, chunks, (int)slot);
+    if (red) {
+      g = slab_reduce2_sum(part, Pst, chunks, (int)slot);
+      if (gx != nullptr)
+        for (int c = 0; c < 4; ++c)
+          if (e0 + c < gr.n) g[c] += gx[e0 + c];
+    }
     const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
     if (aligned && e0 + 4 <= gr.n) {
       f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
@@ -507,7 +517,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
                       int S, int lo, const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses,
                       float* total, float* dscal, float* hist, int64_t hist_rows, int64_t* epoch, float* best_loss,
                       int64_t* best_epoch, int* improved, double* const* counters, int ncnt, const void* groups,
-                      int ngroups, float* snap, int c_first, void* stream) {
+                      int ngroups, float* snap, int c_first, const float* gx, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -560,17 +570,18 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(tail_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, args, part, Pst, chunks, improved,
-                     snap, ti);
+                     snap, ti, gx);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
 
 // Data-parallel step, first half (before the all-reduce): slab pass 1 + the loss reduction in one
-// launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad.  total
-// (optional): also the summed loss - the L-BFGS objective writes [grad | loss] in place this way.
+// launch (no bookkeeping: it needs the all-reduced terms), then slab pass 2 into grad (+ gx, the
+// high-order points' gradient, when given).  total (optional): also the summed loss - the L-BFGS
+// objective writes [grad | loss] in place this way.
 int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
-                      float* total, int c_first, void* stream) {
+                      float* total, int c_first, const float* gx, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -595,7 +606,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks - c_first), dim3(256), 0, st, work, part, nwg_b, Pst,
                      chunks, nqb, half, c_first, tb);
   TDQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nq2), dim3(256), 0, st, part, grad, Ptot, Pst, chunks);
+  hipLaunchKernelGGL(slab_reduce2_bf3, dim3(nq2), dim3(256), 0, st, part, grad, Ptot, Pst, chunks, gx);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -665,7 +676,7 @@ int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(tail_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     args, nullptr, 0, 0, improved, snap, ti);
+                     args, nullptr, 0, 0, improved, snap, ti, nullptr);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -168,10 +168,16 @@ class AdamEngine:
         # holds every SIMD's registers, so the side kernels only delay its workgroups.)
         from .ops import jet_hip
         prog = self.program
-        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+        hi = prog.hi_op
+        J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                       rows=fop.fl.n_streams)
+        if hi is not None:   # order 3 / 4 streams of the high-order points (ops/jet_hi.py)
+            hi.forward(J, self.flat)
         # inside an optimizer step the bookkeeping kernel (fused.step_book) sums the terms
         total, losses, dJ, dlam, dscal = fop(J, with_total=not for_step)
         gflat = jet_hip.backward_raw(saved, dJ)
+        if hi is not None:
+            gflat = gflat + hi.backward(dJ, self.flat)
         grads = self._fused_grads(fop, gflat, dlam, dscal)
         return total, grads, losses   # losses: contiguous per-term vector
 
@@ -270,7 +276,8 @@ class AdamEngine:
         if getattr(self, "_bufs", None) is None:
             from .ops import jet_hip
             prog = self.program
-            J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+            J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                             rows=prog.fused_op.fl.n_streams)
             self._bufs = (J, saved, jet_hip.alloc_backward(saved), torch.empty_like(self.flat))
         return self._bufs
 
@@ -304,8 +311,9 @@ class AdamEngine:
         if packed is None:  # gradient tensors the single launch cannot take: reduce, then Adam
             raise RuntimeError("fused step tail: parameter groups do not fit one launch "
                                "(set TDQ_FUSED_TAIL=0)")
+        hi = prog.hi_op
         jet_hip.step_tail(saved, work, grad, fop, st, self.counters, packed[0], packed[1], st["best_flat"],
-                          write_images=in_graph, c_first=pre)
+                          write_images=in_graph, c_first=pre, gextra=hi.grad if hi is not None else None)
         self._tail_saved = saved
         return fop.total
 
@@ -412,8 +420,9 @@ class AdamEngine:
         if buf is None or buf.numel() != n_p + n_e + 1 + n_t:
             buf = self._dp_buf = torch.empty(n_p + n_e + 1 + n_t, dtype=torch.float32, device=self.device)
         grad_view = buf[:n_p]
+        hi = prog.hi_op
         jet_hip.dp_tail_a(saved, work, grad_view, fop, total=buf[n_p + n_e:n_p + n_e + 1],
-                          losses=buf[n_p + n_e + 1:], c_first=pre)
+                          losses=buf[n_p + n_e + 1:], c_first=pre, gextra=hi.grad if hi is not None else None)
         grads = self._fused_grads(fop, grad_view, fop.dlam, fop.dscal)
         if others:
             torch.cat([grads[i].reshape(-1) for i in others], out=buf[n_p:n_p + n_e])
@@ -640,20 +649,30 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
     (forked from and joined back into the current one; one range runs on the current stream).
     ``bufs``: ``(J, saved, work)`` to reuse (persistent step buffers), else allocated here.
     ``prereduce`` (> 0): after the first range's backward, reduce slab chunks ``[0, prereduce)`` on
-    its stream (the fused step tail then starts at that chunk).  Returns ``(saved, work)`` for the
-    fused step tail."""
+    its stream (the fused step tail then starts at that chunk).  Mixed programs (``program.hi_op``):
+    the high-order points ``[0, n_hi)`` lie in the first range, whose chain also runs their extra
+    streams (before its loss launch) and the gradient of those streams' adjoints (after it) - off
+    the longer second range's critical path.  Returns ``(saved, work)`` for the fused step tail."""
     from .ops import jet_hip
+    hop = program.hi_op
     if bufs is None:
-        J, saved = jet_hip.alloc_forward(program.X_all, flat, program.net, program.plan, program.precision)
+        J, saved = jet_hip.alloc_forward(program.X_all, flat, program.net, program.plan, program.precision,
+                                         rows=fop.fl.n_streams)
         work = jet_hip.alloc_backward(saved)
     else:
         J, saved, work = bufs
     if pack:
         jet_hip.pack_images(saved)
+    if hop is not None and ranges[0][1] < program.n_hi:
+        raise RuntimeError("point ranges: the first range must hold the high-order points")
     if len(ranges) == 1:
         lo, hi, b0, nb = ranges[0]
+        if hop is not None:
+            hop.forward(J, flat)
         jet_hip.forward_range(saved, J, lo, hi)
         fop.run_range(J, b0, nb)
+        if hop is not None:
+            hop.backward(fop.dJ, flat)
         jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
         return saved, work
     # (keeping one range on the current stream measured the same: the graph runtime picks the
@@ -663,8 +682,12 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
         st.wait_stream(cur)
     for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
         with torch.cuda.stream(st):
+            if k == 0 and hop is not None:
+                hop.forward(J, flat)
             jet_hip.forward_range(saved, J, lo, hi)
             fop.run_range(J, b0, nb)
+            if k == 0 and hop is not None:
+                hop.backward(fop.dJ, flat)
             jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
             if k == 0 and prereduce:
                 jet_hip.slab_prereduce(saved, work, 0, prereduce)
@@ -713,19 +736,32 @@ class LossGradEngine:
                 if getattr(self, "_ranges", 0) == 0:
                     self._ranges = point_ranges(prog, fop)
                     self._streams = [torch.cuda.Stream(device=self.flat.device) for _ in (self._ranges or ())]
+                hi = prog.hi_op
+                gx = hi.grad if hi is not None else None
                 if self._ranges:
                     pre = prereduce_chunk(prog, self._ranges)
                     saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams, prereduce=pre)
-                    jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:], c_first=pre)
+                    jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:], c_first=pre, gextra=gx)
                     return fg
-                J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+                J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                               rows=fop.fl.n_streams)
+                if hi is not None:
+                    hi.forward(J, self.flat)
                 fop(J, with_total=False, reduce=False)
+                if hi is not None:
+                    hi.backward(fop.dJ, self.flat)
                 grad, work = jet_hip.backward_raw(saved, fop.dJ, reduce=False, grad=fg[:-1])
-                jet_hip.dp_tail_a(saved, work, grad, fop, total=fg[-1:])
+                jet_hip.dp_tail_a(saved, work, grad, fop, total=fg[-1:], gextra=gx)
                 return fg
-            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision)
+            hi = prog.hi_op
+            J, saved = jet_hip.forward_raw(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                           rows=fop.fl.n_streams)
+            if hi is not None:
+                hi.forward(J, self.flat)
             total, _, dJ, _, _ = fop(J)
             g = jet_hip.backward_raw(saved, dJ)
+            if hi is not None:
+                g = g + hi.backward(dJ, self.flat)
             return torch.cat([g.reshape(-1), total.reshape(1)])
         p = self.flat.detach().requires_grad_(True)
         lams = [l.detach() for l in self.lambdas]

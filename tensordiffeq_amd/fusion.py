@@ -371,8 +371,8 @@ def build(prog, lambdas, extras_example=None):
 
 def _build(prog, lambdas):
     fl = FusedLoss()
-    fl.n_streams = prog.plan.S
-    stream_index = prog.plan.index
+    # mixed programs: the main plan's rows, then the high-order rows (LossProgram.fused_streams)
+    stream_index, fl.n_streams = prog.fused_streams()
     g_by_seg = {}
     gs = []
     lam_id = {}

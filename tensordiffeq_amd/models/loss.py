@@ -21,10 +21,13 @@ Loss definitions (SURVEY.md §2.5 "Exact numerics to match"):
                           type 2 lam*mean(f^2); one lambda per residual (B11 fixed).
 Adaptive periodic / Neumann terms, which the reference rejects (B13), take per-point weights.
 
-Mixed plans: when some callables need derivatives beyond the HIP kernels' order-2 envelope (e.g. the
-periodic u_xxx, u_xxxx of AC-baseline on 2 x 201 boundary points) the segments that only need
-order <= 2 (the collocation points) still run on the HIP kernels, and the few high-order segments
-run through the differentiable torch jet engine; the loss then composes both with autograd.
+Mixed plans: when some callables need derivatives beyond the fused kernels' order-2 envelope (e.g.
+the periodic u_xxx, u_xxxx of AC-baseline on 2 x 201 boundary points) every point still runs on the
+fused kernels with the order <= 2 plan, and the few high-order points get their extra streams from
+the high-order jet kernels (``ops/jet_hi.py``) in extra rows of the same jet buffer, so the fused loss,
+the fused step tail and the K-step graphs stay on (``hi_op``).  Where those kernels or the fused loss
+cannot serve the program, the high-order segments run through the differentiable torch jet engine and
+the loss is composed with autograd.
 
 Data parallel: the collocation segment is this rank's shard; residual means divide by the global
 count and every replicated term is scaled by ``1/world``, so per-rank losses sum to the global one.
@@ -45,7 +48,8 @@ class Segment:
         self.name = name
         self.X = X
         self.offset = 0
-        self.part = 0     # 0: X_all (main plan); 1: X_hi (high-order plan, mixed mode)
+        self.hi = False       # mixed mode: needs the high-order plan (also in X_hi, at hi_offset)
+        self.hi_offset = 0
 
     @property
     def n(self):
@@ -92,6 +96,8 @@ class LossProgram:
         self.X_hi = None
         self.reasons = []
         self.fused_op = None
+        self.hi_op = None     # ops.jet_hi.HiJetOp: high-order streams of the X_hi points, fused path
+        self.n_hi = 0
 
     # ---------------------------------------------------------------- building -------
     def add_segment(self, name, X):
@@ -108,17 +114,24 @@ class LossProgram:
         self.callables.append((fn, seg_idx, extra_args))
 
     def finalize(self):
+        """Plan, then lay out ``X_all``: every segment (high-order ones FIRST, so the high-order jet
+        kernels see one contiguous block ``[0, n_hi)``); mixed mode also keeps ``X_hi``."""
         self._plan()
-        parts = ([s for s in self.segments if s.part == 0], [s for s in self.segments if s.part == 1])
-        for segs in parts:
-            off = 0
-            for s in segs:
-                s.offset = off
-                off += s.n
+        hi = [s for s in self.segments if s.hi]
+        order = hi + [s for s in self.segments if not s.hi]
+        off = 0
+        for s in order:
+            s.offset = off
+            off += s.n
+        off = 0
+        for s in hi:
+            s.hi_offset = off
+            off += s.n
+        self.n_hi = off
         cat = lambda segs: torch.cat([s.X for s in segs], dim=0).contiguous() if segs \
             else torch.zeros(0, self.d_in, device=self.device)
-        self.X_all = cat(parts[0])
-        self.X_hi = cat(parts[1]) if parts[1] else None
+        self.X_all = cat(order)
+        self.X_hi = cat(hi) if hi else None
 
     @property
     def mixed(self):
@@ -155,7 +168,7 @@ class LossProgram:
                 reasons.append(why)
         backend = self.requested_backend
         for s in self.segments:
-            s.part = 0
+            s.hi = False
         if backend in ("auto", "hip") and jetable:
             plan = JetPlan(requests, self.d_in)
             ok, why = jet_mlp.hip_eligible(self.net, plan, self.device)
@@ -167,7 +180,7 @@ class LossProgram:
                     n_lo = sum(sg.n for sg in self.segments) - n_hi
                     if ok_lo and n_lo >= n_hi:
                         for i in hi:
-                            self.segments[i].part = 1
+                            self.segments[i].hi = True
                         self.plan = JetPlan(lo_req, self.d_in)
                         self.plan_hi = JetPlan(hi_req, self.d_in)
                         self.backend = "hip"
@@ -251,8 +264,8 @@ class LossProgram:
     def seg_view(self, J, si):
         s = self.segments[si]
         if isinstance(J, JetParts):
-            src, plan = (J.hi, self.plan_hi) if s.part == 1 else (J.lo, self.plan)
-            return jet_dict(src[:, s.offset:s.offset + s.n], plan)
+            src, plan, off = (J.hi, self.plan_hi, s.hi_offset) if s.hi else (J.lo, self.plan, s.offset)
+            return jet_dict(src[:, off:off + s.n], plan)
         return jet_dict(J[:, s.offset:s.offset + s.n], self.plan)
 
     def jet(self, params, X=None, plan=None):
@@ -272,7 +285,7 @@ class LossProgram:
         """Plan that serves callable ``fn`` (the high-order one if ``fn`` runs on a hi segment)."""
         if self.mixed:
             for f, si, _ in self.callables:
-                if f is fn and self.segments[si].part == 1:
+                if f is fn and self.segments[si].hi:
                     return self.plan_hi
         return self.plan
 
@@ -294,7 +307,9 @@ class LossProgram:
             return getattr(self, "_cur_net", self.net)(self.segments[si].X)
         s = self.segments[si]
         if isinstance(J, JetParts):
-            J = J.hi if s.part == 1 else J.lo
+            if s.hi:
+                return J.hi[0, s.hi_offset:s.hi_offset + s.n]
+            J = J.lo
         return J[0, s.offset:s.offset + s.n]
 
     def evaluate(self, params=None, lambdas=None, extras=None):
@@ -387,8 +402,14 @@ class LossProgram:
         import os
         from .. import fusion
         self.fused_op = None
-        if self.backend != "hip" or self.mixed or os.environ.get("TDQ_FUSED_LOSS", "1") == "0":
+        self.hi_op = None
+        if self.backend != "hip" or os.environ.get("TDQ_FUSED_LOSS", "1") == "0":
             return False
+        if self.mixed:
+            ok, why = self._hi_kernels_ok()
+            if not ok:
+                self.reasons.append(f"high-order segments on the torch jet: {why}")
+                return False
         fl = fusion.build(self, lambdas)
         if fl is None:
             return False
@@ -398,7 +419,41 @@ class LossProgram:
             self.fused_op = FusedLossOp(fl, self, lambdas, scalars, fl.lam_offsets)
         except ValueError:
             return False
+        if self.mixed:
+            from ..ops.jet_hi import HiJetOp
+            idx, _ = self.fused_streams()
+            extra = {m: idx[m] for m in self.plan_hi.streams if m not in self.plan.index}
+            self.hi_op = HiJetOp(self.net, self.plan_hi, extra, self.X_all, self.n_hi, self.device)
         return True
+
+    def fused_streams(self):
+        """``(stream -> J row, rows)`` of the fused loss: the main plan's streams, then (mixed mode)
+        the high-order plan's streams the main plan lacks - the rows :class:`~..ops.jet_hi.HiJetOp`
+        fills for the high-order points."""
+        idx = dict(self.plan.index)
+        if self.mixed:
+            for m in self.plan_hi.streams:
+                if m not in idx:
+                    idx[m] = len(idx)
+        return idx, len(idx)
+
+    def _hi_kernels_ok(self):
+        """Mixed mode on the fused path: the main plan on the split-bf16 kernels and the high-order
+        plan within ops/jet_hi.py's envelope (``TDQ_HI_KERNEL=0`` keeps the torch jet)."""
+        import os
+        from ..ops import jet_hi, jet_hip
+        from ..ops.jet_mlp import hip_config
+        if os.environ.get("TDQ_HI_KERNEL", "1") == "0":
+            return False, "TDQ_HI_KERNEL=0"
+        if self.device.type != "cuda":
+            return False, "not on a GPU"
+        try:
+            cfg = hip_config(self.net, self.plan, self.precision)
+        except ValueError as e:
+            return False, str(e)
+        if not jet_hip.is_split_bf16(cfg):
+            return False, f"main kernels {cfg['precision']}/{cfg.get('engine', 'fused')} (needs the split-bf16 kernels)"
+        return jet_hi.eligible(self.net, self.plan_hi)
 
     # ---------------------------------------------------------------- prediction -----
     def residual_on(self, fn, X, params=None, extra=(), chunk=65536):

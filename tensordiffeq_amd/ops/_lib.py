@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _lock = threading.Lock()
 _lib = None
@@ -48,10 +48,10 @@ def _declare(lib):
         "tdq_jet_bwd_bf3_range": (I, [P, P, P, P, I, I, I, I, P, I, I, I, P, I, P]),
         "tdq_jet_bf3_pack": (I, [P, P, I, I, P, I, I, I, P]),
         "tdq_step_tail_bf3": (I, [P, P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P] + [P, L, P, P, P, P]
-                              + [P, I, P, I, P, I, P]),
+                              + [P, I, P, I, P, I, P, P]),
         "tdq_bf3_slab_geometry": (I, [I, I, P, I, I, I, I, P]),
         "tdq_slab_prereduce_bf3": (I, [P, I, I, P, I, I, I, I, I, I, P]),
-        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, I, P]),
+        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, I, P, P]),
         "tdq_dp_tail_b_bf3": (I, [P, I, I, P, I, I, I, P, I, P, P, P]),
         "tdq_jet_bf3_scratch_floats": (L, [I, I, P, I, I, I]),
         "tdq_jet_bf3_slab_floats": (L, [I, I, P, I, I]),
@@ -67,6 +67,12 @@ def _declare(lib):
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
         "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_layered_epi": (I, [I, P, P, P, L, I, I, P, P, P, P]),
+        # high-order (<= 4) jets of small point sets (csrc/jet_hi.hip, ops/jet_hi.py)
+        "tdq_jet_hi_scratch_floats": (L, [I, I]),
+        "tdq_jet_hi_work_floats": (L, [I, I, P, I, I]),
+        "tdq_jet_hi_fwd": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P]),
+        "tdq_jet_hi_bwd": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P, P, P]),
+        "tdq_jet_hi_limits": (I, [P]),
         # one-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py)
         "tdq_peer_maxw": (I, []),
         "tdq_peer_chunk": (I, []),

@@ -58,13 +58,14 @@ def _lo_args(cfg):
     return ()
 
 
-def forward_raw(X, P, net, plan, precision=None, pack=True):
+def forward_raw(X, P, net, plan, precision=None, pack=True, rows=None):
     """Autograd-free forward: returns ``(J, saved)`` where ``saved`` feeds :func:`backward_raw`.
 
     ``precision``: ``"bf16x3"`` / ``"bf16"`` (csrc/jet_bf3.hip, saves post-activations) or ``"fp32"``
     (csrc/jet_mlp.hip, saves pre-activations); the saved buffer only fits its own backward.
     ``pack=False`` (split-bf16 only): the weight images inside the scratch are already current
-    (a captured Adam step whose fused tail rewrote them, see :func:`step_tail`)."""
+    (a captured Adam step whose fused tail rewrote them, see :func:`step_tail`).  ``rows``: jet rows
+    of ``J`` (default ``plan.S``; more leave room for the high-order streams of ops/jet_hi.py)."""
     lib = _lib.load()
     cfg = hip_config(net, plan, precision)
     if is_layered(cfg):
@@ -76,7 +77,7 @@ def forward_raw(X, P, net, plan, precision=None, pack=True):
     S = plan.S
     spec = stream_spec(plan)
     spec_c = (ctypes.c_int * len(spec))(*spec)
-    J = torch.empty((S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
+    J = torch.empty((max(S, rows or S), N, cfg["d_out"]), dtype=torch.float32, device=X.device)
     nscr = scratch_floats(N)
     if nscr < 0:
         raise ValueError(f"jet kernels cannot serve {cfg}")
@@ -126,7 +127,7 @@ def backward_raw(saved, dJ, reduce=True, grad=None):
     return grad
 
 
-def alloc_forward(X, P, net, plan, precision=None):
+def alloc_forward(X, P, net, plan, precision=None, rows=None):
     """Buffers of a split-bf16 forward over the whole point set, nothing launched: ``(J, saved)``
     for :func:`pack_images`, :func:`forward_range` and :func:`backward_range`."""
     cfg = hip_config(net, plan, precision)
@@ -139,7 +140,7 @@ def alloc_forward(X, P, net, plan, precision=None):
     nscr = scratch_floats(N)
     if nscr < 0:
         raise ValueError(f"jet kernels cannot serve {cfg}")
-    J = torch.empty((plan.S, N, cfg["d_out"]), dtype=torch.float32, device=X.device)
+    J = torch.empty((max(plan.S, rows or plan.S), N, cfg["d_out"]), dtype=torch.float32, device=X.device)
     scratch = torch.empty(max(int(nscr), 1), dtype=torch.float32, device=X.device)
     return J, (X, P, scratch, cfg, stream_spec(plan), plan.S)
 
@@ -218,13 +219,14 @@ def slab_prereduce(saved, work, c0, c1):
 
 
 def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, snapshot, write_images=True,
-              c_first=0):
+              c_first=0, gextra=None):
     """End of a single-process Adam step in two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``):
     slab reduction + loss reduction + bookkeeping, then the reduced gradient fused into Adam
     (theta, SA weights), the best-weights snapshot and - ``write_images`` - the next step's
     weight images.  ``book``: the engine's device state dict; ``group_array``: ctypes array of
     ``fused._Group`` with theta first; ``c_first``: first-pass chunks below it were pre-reduced
-    (:func:`slab_prereduce`)."""
+    (:func:`slab_prereduce`); ``gextra``: a gradient added to theta's (the high-order points',
+    :class:`~tensordiffeq_amd.ops.jet_hi.HiJetOp`)."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     hist = book["hist"]
@@ -237,7 +239,8 @@ def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, sna
         _lib.ptr(hist), int(hist.shape[0]), _lib.ptr(book["epoch"]), _lib.ptr(book["best_loss"]),
         _lib.ptr(book["best_epoch"]), _lib.ptr(book["improved"]), ctypes.cast(carr, ctypes.c_void_p), len(counters),
         ctypes.cast(group_array, ctypes.c_void_p), n_groups,
-        _lib.ptr(snapshot) if snapshot is not None else None, int(c_first), _lib.stream_ptr(X.device))
+        _lib.ptr(snapshot) if snapshot is not None else None, int(c_first), _lib.ptr(gextra),
+        _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_step_tail_bf3")
 
 
@@ -268,7 +271,7 @@ class JetMLPFunction(torch.autograd.Function):
         return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None
 
 
-def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0):
+def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0, gextra=None):
     """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
     slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``).  ``total`` (a 1-element
     view): also write the summed loss there; ``losses`` (an ``n_terms`` view, default
@@ -279,7 +282,7 @@ def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0):
     rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"],
                                cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
                                fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total), int(c_first),
-                               _lib.stream_ptr(X.device))
+                               _lib.ptr(gextra), _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")
 
 
