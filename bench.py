@@ -113,6 +113,105 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
     return model
 
 
+def build_discovery(n_data, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
+                    lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1)):
+    """The reference's AC-discovery program (examples/AC-discovery.py:14-66): learn c1, c2 of
+    u_t - c1 u_xx + c2 u^3 - c2 u = 0 (truth 1e-4, 5) from the AC.mat field (102,912 points, or a
+    seeded subsample of ``n_data``), self-adaptive collocation weights (col-weight Adam beta_1 0.95)."""
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.models import DiscoveryModel
+    from tensordiffeq_amd.optimizers import Adam
+    import scipy.io
+    tdq.set_seed(seed)
+    data = scipy.io.loadmat(os.path.join(HERE, "data", "AC.mat"))
+    x, t = data["x"].flatten(), data["tt"].flatten()
+    X, T = np.meshgrid(x, t)
+    X_star = np.hstack((X.flatten()[:, None], T.flatten()[:, None]))
+    u_star = np.real(data["uu"]).T.flatten()[:, None]
+    if n_data and n_data < X_star.shape[0]:
+        idx = np.random.default_rng(seed).choice(X_star.shape[0], n_data, replace=False)
+        X_star, u_star = X_star[idx], u_star[idx]
+    params = [tdq.Variable(0.0), tdq.Variable(0.0)]
+
+    def f_model(u_model, var, x, t):
+        u = u_model(torch.cat([x, t], 1))
+        u_x = tdq.grad(u, x)
+        u_xx = tdq.grad(u_x, x)
+        u_t = tdq.grad(u, t)
+        return u_t - var[0] * u_xx + var[1] * u * u * u - var[1] * u
+
+    g = torch.Generator().manual_seed(99 if seed == 1234 else seed)
+    col_weights = torch.rand(X_star.shape[0], 1, generator=g)
+    m = DiscoveryModel(verbose=False)
+    m.compile(list(layers), f_model, [X_star[:, 0:1], X_star[:, 1:2]], u_star, params, col_weights=col_weights,
+              backend=backend, device=device, dist=dist, precision=precision, newton_precision=newton_precision,
+              lbfgs_stop=lbfgs_stop)
+    m.tf_optimizer_weights = Adam(lr=0.005, beta_1=0.95)
+    return m
+
+
+def build_poisson(n_glob, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
+                  lbfgs_stop=None, layers=(2, 50, 50, 50, 50, 1)):
+    """The reference's 2-D steady-state (Helmholtz-type) program, examples/steady-state.py:10-55:
+    u_xx + u_yy + u = q on [-1, 1]^2, exact u = sin(pi x) sin(4 pi y), 4 Dirichlet faces of 1001
+    points, [2, 50x4, 1]; BASELINE.json sizes it at 10M collocation points per GPU."""
+    import tensordiffeq_amd as tdq
+    from tensordiffeq_amd.boundaries import DomainND, dirichletBC
+    tdq.set_seed(seed)
+    D = DomainND(["x", "y"])
+    D.add("x", [-1.0, 1.0], 1001)
+    D.add("y", [-1.0, 1.0], 1001)
+    D.generate_collocation_points(n_glob, device=device if device.type == "cuda" else None)
+
+    def f_model(u_model, x, y):
+        u = u_model(torch.cat([x, y], 1))
+        u_xx = tdq.grad(tdq.grad(u, x), x)
+        u_yy = tdq.grad(tdq.grad(u, y), y)
+        s = torch.sin(math.pi * x) * torch.sin(4 * math.pi * y)
+        return u_xx + u_yy + u - (-(math.pi ** 2) * s - (4 * math.pi) ** 2 * s + s)
+
+    bcs = [dirichletBC(D, 0.0, v, tg) for v in ("x", "y") for tg in ("upper", "lower")]
+    m = tdq.CollocationSolverND(verbose=False)
+    m.compile(list(layers), f_model, D, bcs, backend=backend, device=device, dist=dist, precision=precision,
+              newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+    return m
+
+
+# BASELINE.json configs: builder, default points (per GPU for weak scaling, total for strong),
+# scaling, default net, model name, BC description, unit of the throughput
+PROBLEMS = {
+    "ac-sa": dict(build=lambda *a, **k: build_problem(*a, problem="ac-sa", **k), npts=50000, scaling="weak",
+                  layers="2,128,128,128,128,1", model="Allen-Cahn SA-PINN tanh MLP",
+                  bc="IC 512 (SA) + periodic 2x201 (u, u_x)", unit="collocation-pts/s"),
+    "ac-baseline": dict(build=lambda *a, **k: build_problem(*a, problem="ac-baseline", **k), npts=50000,
+                        scaling="weak", layers="2,128,128,128,128,1", model="Allen-Cahn baseline PINN tanh MLP",
+                        bc="IC 512 + periodic 2x201 (u, u_x, u_xxx, u_xxxx; order 3/4 on jet_hi.hip)",
+                        unit="collocation-pts/s"),
+    "ac-dist": dict(build=lambda *a, **k: build_problem(*a, problem="ac-baseline", **k), npts=500000,
+                    scaling="strong", layers="2,128,128,128,128,1",
+                    model="Allen-Cahn distributed (AC-dist-new) tanh MLP",
+                    bc="IC 512 + periodic 2x201 (u, u_x, u_xxx, u_xxxx)", unit="collocation-pts/s"),
+    "discovery": dict(build=build_discovery, npts=102912, scaling="strong", layers="2,128,128,128,128,1",
+                      model="Allen-Cahn discovery (c1, c2) tanh MLP", bc="AC.mat data points (SA col weights)",
+                      unit="data-pts/s"),
+    "poisson": dict(build=build_poisson, npts=10_000_000, scaling="weak", layers="2,50,50,50,50,1",
+                    model="2-D steady-state Helmholtz/Poisson tanh MLP", bc="4 Dirichlet faces x 1001",
+                    unit="collocation-pts/s"),
+}
+
+
+def get_engine(model, n_hint):
+    """The model's captured Adam engine (solver and discovery models name it differently)."""
+    from tensordiffeq_amd.models.discovery import DiscoveryModel
+    if isinstance(model, DiscoveryModel):
+        return model._get_engine(n_hint)
+    return model._get_engine(None, n_hint)
+
+
+def backend_of(model):
+    return model.program().backend
+
+
 def l2_on_ac_grid(model):
     import scipy.io
     data = scipy.io.loadmat(os.path.join(HERE, "data", "AC.mat"))
@@ -209,22 +308,33 @@ def allreduce_replay_us(ctx, n_floats, calls=10, reps=20):
     return {"us_per_call": round(ctx.max_scalar(us), 2), "floats": int(n_floats), "mode": mode}
 
 
-def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop, problem="ac-sa"):
-    """Reference AC-SA schedule per seed (examples/AC-SA.py:9-88): L2 on AC.mat, phase times,
-    L-BFGS stop reason."""
+def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop, problem="ac-sa",
+                  layers=None):
+    """Reference schedule per seed (AC-SA / AC-baseline: examples/AC-SA.py:9-88, Adam + L-BFGS, L2 on
+    AC.mat; discovery: examples/AC-discovery.py, Adam + L-BFGS over network and coefficients,
+    c1 / c2 errors), with phase times and the L-BFGS stop reason."""
     out = []
+    spec = PROBLEMS[problem]
+    layers = layers or tuple(int(v) for v in spec["layers"].split(","))
     for sd in seeds:
-        m = build_problem(50000, 1, backend, device, False, precision, seed=sd,
-                          newton_precision=newton_precision, lbfgs_stop=lbfgs_stop, problem=problem)
-        m.fit(tf_iter=iters)
-        m.fit(newton_iter=newton)
+        n = spec["npts"] if problem == "discovery" else 50000
+        m = spec["build"](n, 1, backend, device, False, precision, seed=sd, newton_precision=newton_precision,
+                          lbfgs_stop=lbfgs_stop, layers=layers)
+        if problem == "discovery":
+            m.fit(tf_iter=iters, newton_iter=newton)
+            c1, c2 = (float(v.detach()) for v in m.vars)
+            res = {"seed": sd, "c1": c1, "c2": c2, "c1_rel_err": abs(c1 - 1e-4) / 1e-4, "c2_rel_err": abs(c2 - 5.0) / 5.0}
+        else:
+            m.fit(tf_iter=iters)
+            m.fit(newton_iter=newton)
+            res = {"seed": sd, "l2": float(l2_on_ac_grid(m))}
         info = m.fit_info
         lb = info.get("lbfgs", {})
-        out.append({"seed": sd, "l2": float(l2_on_ac_grid(m)),
-                    "adam_s": round(info.get("adam", {}).get("wall_s", 0.0), 3),
+        res.update({"adam_s": round(info.get("adam", {}).get("wall_s", 0.0), 3),
                     "lbfgs_s": round(lb.get("wall_s", 0.0), 3),
                     "lbfgs_n_iter": lb.get("n_iter"), "lbfgs_reason": lb.get("reason"),
                     "lbfgs_stop": lb.get("stop")})
+        out.append(res)
         del m
         if device.type == "cuda":
             torch.cuda.empty_cache()
@@ -239,7 +349,7 @@ def forced_dp_timing(n_glob, backend, device, precision, steps, warmup, min_warm
     ctx = pdist.init_distributed(device=device, force=True)
     try:
         m = build_problem(n_glob, 1, backend, device, True, precision)
-        eng = m._get_engine(None, warmup + steps + 2)
+        eng = get_engine(m, warmup + steps + 2)
         el, _, _ = time_steps(eng, ctx, device, steps, warmup, min_warmup_s)
         return {"ms_per_step": 1000.0 * el / steps, "backend": ctx.backend,
                 "collective_in_graph": bool(ctx.graph_collectives)}
@@ -250,25 +360,31 @@ def forced_dp_timing(n_glob, backend, device, precision, steps, warmup, min_warm
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--problem", default="ac-sa", choices=["ac-sa", "ac-baseline"],
-                    help="ac-sa: the BASELINE.json flagship (examples/AC-SA.py); ac-baseline: the reference's "
-                         "AC-baseline / AC-dist-new program (no SA weights, periodic u, u_x, u_xxx, u_xxxx)")
+    ap.add_argument("--problem", default="ac-sa", choices=sorted(PROBLEMS),
+                    help="ac-sa: the BASELINE.json flagship (examples/AC-SA.py, 50k pts/GPU); ac-baseline: the "
+                         "reference's AC-baseline program (no SA weights, periodic u, u_x, u_xxx, u_xxxx; 50k/GPU); "
+                         "ac-dist: AC-dist-new (the same program, 500k points in total, strong scaling); "
+                         "discovery: AC-discovery (102,912 AC.mat points in total, c1/c2 errors); "
+                         "poisson: 2-D steady state at 10M points per GPU")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--min-warmup-s", type=float, default=1.0,
                     help="keep warming up (untimed) until this much time has passed")
-    ap.add_argument("--npts", type=int, default=50000, help="collocation points per GPU (weak scaling)")
+    ap.add_argument("--npts", type=int, default=None,
+                    help="collocation points per GPU (weak scaling; default: the problem's)")
     ap.add_argument("--global-npts", type=int, default=None,
-                    help="total collocation points, split over the GPUs (strong scaling)")
+                    help="total collocation points, split over the GPUs (strong scaling; default for "
+                         "ac-dist / discovery)")
     ap.add_argument("--backend", default="auto")
-    ap.add_argument("--layers", default="2,128,128,128,128,1",
-                    help="network layer sizes (default: the AC-SA net of BASELINE.json; widths > 128 run the "
+    ap.add_argument("--layers", default=None,
+                    help="network layer sizes (default: the problem's reference net; widths > 128 run the "
                          "layer-wise engine)")
     ap.add_argument("--no-l2", action="store_true", help="skip the accuracy runs")
     ap.add_argument("--acc-seeds", type=int, nargs="*", default=[0, 1, 2],
                     help="seeds of the full-schedule accuracy runs (single GPU only)")
     ap.add_argument("--acc-iters", type=int, default=10000)
-    ap.add_argument("--acc-newton", type=int, default=10000)
+    ap.add_argument("--acc-newton", type=int, default=None,
+                    help="L-BFGS iterations of the accuracy runs (default 10000; discovery 5000)")
     ap.add_argument("--newton-precision", default="bf16x3")
     ap.add_argument("--lbfgs-stop", default=None, choices=["fixed", "legacy"],
                     help="L-BFGS function-change test (default: the library's, legacy = the reference's)")
@@ -295,8 +411,17 @@ def main(argv=None):
     if device.type == "cuda":
         torch.cuda.set_device(device)
 
-    strong = args.global_npts is not None
-    n_glob = args.global_npts if strong else args.npts * world
+    spec = PROBLEMS[args.problem]
+    strong = args.global_npts is not None or (args.npts is None and spec["scaling"] == "strong")
+    if strong:
+        n_glob = args.global_npts if args.global_npts is not None else spec["npts"]
+    else:
+        n_glob = (args.npts if args.npts is not None else spec["npts"]) * world
+    if args.acc_newton is None:
+        args.acc_newton = 5000 if args.problem == "discovery" else 10000
+    # accuracy runs: the reference schedules of the single-GPU configs (AC-dist-new runs Adam 1001
+    # twice without L-BFGS and the 10M-point Poisson config is a throughput sizing)
+    acc_ok = args.problem in ("ac-sa", "ac-baseline", "discovery")
     if "TDQ_STEP_UNROLL" not in os.environ:
         # steps per captured graph: a divisor of --steps, so the timed steps are all multi-step graph
         # replays (a 1-step replay leaves ~9 us idle between graphs; 8 and 16 per graph measured
@@ -304,11 +429,10 @@ def main(argv=None):
         # two 10-step replays, 0.206-0.211 vs 0.202-0.203 ms, profiles/r3_au_driver_shape_unroll_ab.jsonl)
         divs = [k for k in range(16, 3, -1) if args.steps % k == 0]
         os.environ["TDQ_STEP_UNROLL"] = str(8 if args.steps % 8 == 0 else (divs[0] if divs else 8))
-    layers = tuple(int(v) for v in args.layers.split(","))
-    model = build_problem(n_glob, world, args.backend, device, dist, args.precision, layers=layers,
-                          problem=args.problem)
-    eng = model._get_engine(None, args.warmup + args.steps + 2)
-    backend = model.active_backend
+    layers = tuple(int(v) for v in (args.layers or spec["layers"]).split(","))
+    model = spec["build"](n_glob, world, args.backend, device, dist, args.precision, layers=layers)
+    eng = get_engine(model, args.warmup + args.steps + 2)
+    backend = backend_of(model)
     elapsed, n_warm, warm_s = time_steps(eng, ctx, device, args.steps, args.warmup, args.min_warmup_s)
     steps_per_graph = eng._unroll()
     loss = float(model._state["hist"][int(model._state["epoch_host"]) - 1, 0])
@@ -326,14 +450,15 @@ def main(argv=None):
     del eng, model
 
     acc, acc_err = None, None
-    if not args.no_l2 and world == 1 and args.acc_seeds:
+    if not args.no_l2 and world == 1 and args.acc_seeds and acc_ok:
         try:
             acc = accuracy_runs(args.acc_seeds, device, args.backend, args.precision, args.newton_precision,
-                                args.acc_iters, args.acc_newton, args.lbfgs_stop, problem=args.problem)
+                                args.acc_iters, args.acc_newton, args.lbfgs_stop, problem=args.problem,
+                                layers=layers)
         except Exception as e:  # pragma: no cover - reported, never hides the throughput number
             acc_err = f"{type(e).__name__}: {e}"
     dp = None
-    if args.force_dp and world == 1 and device.type == "cuda":
+    if args.force_dp and world == 1 and device.type == "cuda" and args.problem == "ac-sa":
         try:
             dp = forced_dp_timing(n_glob, args.backend, device, args.precision, args.steps, args.warmup,
                                   args.min_warmup_s)
@@ -344,7 +469,7 @@ def main(argv=None):
         rec = {
             "metric": METRIC,
             "value": pts_per_s,
-            "unit": "collocation-pts/s",
+            "unit": spec["unit"],
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -353,26 +478,34 @@ def main(argv=None):
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "bf16" if (backend == "hip" and args.precision != "fp32") else "fp32",
-            "data": "synthetic (LHS collocation points, random Keras-init weights); L2 on data/AC.mat",
-            "config": {"model": (f"Allen-Cahn SA-PINN tanh MLP [{','.join(map(str, layers))}]" if args.problem == "ac-sa"
-                                 else f"Allen-Cahn baseline PINN tanh MLP [{','.join(map(str, layers))}]"),
+            "data": ("AC.mat observations (102,912-point field), random Keras-init weights" if args.problem == "discovery"
+                     else "synthetic (LHS collocation points, random Keras-init weights)"
+                     + ("; L2 on data/AC.mat" if args.problem.startswith("ac") else "")),
+            "config": {"model": f"{spec['model']} [{','.join(map(str, layers))}]",
                        "problem": args.problem,
                        "global_batch": n_glob, "seq_len": None, "parallelism": f"dp{world}",
                        "points_per_gpu": n_glob // world, "backend": backend,
                        "precision": PRECISION_NOTES[args.precision] if backend == "hip" else "fp32",
-                       "bc_points": ("IC 512 (SA) + periodic 2x201 (u, u_x)" if args.problem == "ac-sa" else
-                                     "IC 512 + periodic 2x201 (u, u_x, u_xxx, u_xxxx; order 3/4 on jet_hi.hip)")},
+                       "bc_points": spec["bc"]},
             "warmup_steps_run": n_warm,
             "warmup_s": round(warm_s, 3),
             "loss_after": loss,
             "total_adam_steps": total_steps,
         }
-        if acc is not None:
+        if acc is not None and args.problem == "discovery":
+            rec["coefficients"] = [{k: a[k] for k in ("seed", "c1", "c2", "c1_rel_err", "c2_rel_err")} for a in acc]
+            rec["accuracy_schedule"] = (f"Adam {args.acc_iters} ({args.precision}) + L-BFGS {args.acc_newton} "
+                                        f"({args.newton_precision}) over network + c1, c2; reference "
+                                        f"examples/AC-discovery.py (Adam 10k); seeds {args.acc_seeds}")
+            rec["time_to_solution_s"] = [{"adam_s": a["adam_s"], "lbfgs_s": a["lbfgs_s"]} for a in acc]
+            rec["lbfgs"] = [{"reason": a["lbfgs_reason"], "n_iter": a["lbfgs_n_iter"]} for a in acc]
+        elif acc is not None:
             l2s = sorted(a["l2"] for a in acc)
             rec["l2_full_schedule"] = l2s[len(l2s) // 2]
             rec["l2_full_schedule_seeds"] = [a["l2"] for a in acc]
+            ref = "AC-SA" if args.problem == "ac-sa" else "AC-baseline"
             rec["accuracy_schedule"] = (f"Adam {args.acc_iters} ({args.precision}) + L-BFGS {args.acc_newton} "
-                                        f"({args.newton_precision}), N_f 50000, reference examples/AC-SA.py; "
+                                        f"({args.newton_precision}), N_f 50000, reference examples/{ref}.py; "
                                         f"median over seeds {args.acc_seeds}")
             rec["time_to_solution_s"] = [{"adam_s": a["adam_s"], "lbfgs_s": a["lbfgs_s"]} for a in acc]
             rec["lbfgs"] = [{"reason": a["lbfgs_reason"], "n_iter": a["lbfgs_n_iter"], "stop": a["lbfgs_stop"]}

@@ -30,3 +30,7 @@ python -c "import json;d=json.loads(open('$O/bench_acb.json').read().splitlines(
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_acb -o run --output-format csv -- python3 $R/bench.py --problem ac-baseline --steps 200 --warmup 5 --min-warmup-s 0 --no-l2 > $R/$O/prof_acb.log 2>&1) || { tail -20 $O/prof_acb.log; exit 1; }
 python tools/kernel_stats.py $O/prof_acb/run_kernel_stats.csv --steps 205 > $O/kernel_stats_acb.txt 2>&1
 head -14 $O/kernel_stats_acb.txt | cut -c1-150
+timeout -k 10 400 python bench.py --problem discovery --steps 20 --warmup 5 --acc-seeds 0 > $O/bench_disc.json 2> $O/bench_disc.err || { tail -20 $O/bench_disc.err; exit 1; }
+python -c "import json;d=json.loads(open('$O/bench_disc.json').read().splitlines()[-1]);print({k:d.get(k) for k in ['ms_per_step','value','coefficients','time_to_solution_s','lbfgs']})"
+timeout -k 10 300 python bench.py --problem poisson --steps 20 --warmup 3 --no-l2 > $O/bench_poisson.json 2> $O/bench_poisson.err || { tail -20 $O/bench_poisson.err; exit 1; }
+python -c "import json;d=json.loads(open('$O/bench_poisson.json').read().splitlines()[-1]);print({k:d.get(k) for k in ['ms_per_step','value','config']})"
