@@ -56,7 +56,7 @@ PRECISION_NOTES = {
 
 
 def build_problem(n_glob, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
-                  lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1), problem="ac-sa"):
+                  lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1), problem="ac-sa", newton_schedule=None):
     """The AC-SA problem of BASELINE.json with ``n_glob`` collocation points in total (sharded over
     ``world`` ranks when ``dist``).  ``problem="ac-baseline"``: the reference's AC-baseline /
     AC-dist-new program instead (examples/AC-baseline.py:14-52, AC-dist-new.py:14-48): no
@@ -98,7 +98,7 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
         model = tdq.CollocationSolverND(verbose=False)
         model.compile(list(layers), f_model, D, [init, periodicBC(D, ["x"], [deriv_model4])],
                       backend=backend, device=device, dist=dist, precision=precision,
-                      newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+                      newton_precision=newton_precision, lbfgs_stop=lbfgs_stop, newton_schedule=newton_schedule)
         return model
     x_periodic = periodicBC(D, ["x"], [deriv_model])
     g = torch.Generator().manual_seed(99 if seed == 1234 else seed)
@@ -109,12 +109,13 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
                   Adaptive_type="self-adaptive",
                   dict_adaptive={"residual": [True], "BCs": [True, False]},
                   init_weights=init_weights, backend=backend, device=device, dist=dist,
-                  precision=precision, newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+                  precision=precision, newton_precision=newton_precision, lbfgs_stop=lbfgs_stop,
+                  newton_schedule=newton_schedule)
     return model
 
 
 def build_discovery(n_data, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
-                    lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1)):
+                    lbfgs_stop=None, layers=(2, 128, 128, 128, 128, 1), newton_schedule=None):
     """The reference's AC-discovery program (examples/AC-discovery.py:14-66): learn c1, c2 of
     u_t - c1 u_xx + c2 u^3 - c2 u = 0 (truth 1e-4, 5) from the AC.mat field (102,912 points, or a
     seeded subsample of ``n_data``), self-adaptive collocation weights (col-weight Adam beta_1 0.95)."""
@@ -151,7 +152,7 @@ def build_discovery(n_data, world, backend, device, dist, precision=None, seed=1
 
 
 def build_poisson(n_glob, world, backend, device, dist, precision=None, seed=1234, newton_precision=None,
-                  lbfgs_stop=None, layers=(2, 50, 50, 50, 50, 1)):
+                  lbfgs_stop=None, layers=(2, 50, 50, 50, 50, 1), newton_schedule=None):
     """The reference's 2-D steady-state (Helmholtz-type) program, examples/steady-state.py:10-55:
     u_xx + u_yy + u = q on [-1, 1]^2, exact u = sin(pi x) sin(4 pi y), 4 Dirichlet faces of 1001
     points, [2, 50x4, 1]; BASELINE.json sizes it at 10M collocation points per GPU."""
@@ -173,7 +174,7 @@ def build_poisson(n_glob, world, backend, device, dist, precision=None, seed=123
     bcs = [dirichletBC(D, 0.0, v, tg) for v in ("x", "y") for tg in ("upper", "lower")]
     m = tdq.CollocationSolverND(verbose=False)
     m.compile(list(layers), f_model, D, bcs, backend=backend, device=device, dist=dist, precision=precision,
-              newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+              newton_precision=newton_precision, lbfgs_stop=lbfgs_stop, newton_schedule=newton_schedule)
     return m
 
 
@@ -309,7 +310,7 @@ def allreduce_replay_us(ctx, n_floats, calls=10, reps=20):
 
 
 def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop, problem="ac-sa",
-                  layers=None):
+                  layers=None, newton_schedule=None):
     """Reference schedule per seed (AC-SA / AC-baseline: examples/AC-SA.py:9-88, Adam + L-BFGS, L2 on
     AC.mat; discovery: examples/AC-discovery.py, Adam + L-BFGS over network and coefficients,
     c1 / c2 errors), with phase times and the L-BFGS stop reason."""
@@ -319,7 +320,7 @@ def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, ne
     for sd in seeds:
         n = spec["npts"] if problem == "discovery" else 50000
         m = spec["build"](n, 1, backend, device, False, precision, seed=sd, newton_precision=newton_precision,
-                          lbfgs_stop=lbfgs_stop, layers=layers)
+                          lbfgs_stop=lbfgs_stop, layers=layers, newton_schedule=newton_schedule)
         if problem == "discovery":
             m.fit(tf_iter=iters, newton_iter=newton)
             c1, c2 = (float(v.detach()) for v in m.vars)
@@ -330,6 +331,8 @@ def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, ne
             res = {"seed": sd, "l2": float(l2_on_ac_grid(m))}
         info = m.fit_info
         lb = info.get("lbfgs", {})
+        if lb.get("phases"):
+            res["lbfgs_phases"] = lb["phases"]
         res.update({"adam_s": round(info.get("adam", {}).get("wall_s", 0.0), 3),
                     "lbfgs_s": round(lb.get("wall_s", 0.0), 3),
                     "lbfgs_n_iter": lb.get("n_iter"), "lbfgs_reason": lb.get("reason"),
@@ -386,6 +389,8 @@ def main(argv=None):
     ap.add_argument("--acc-newton", type=int, default=None,
                     help="L-BFGS iterations of the accuracy runs (default 10000; discovery 5000)")
     ap.add_argument("--newton-precision", default="bf16x3")
+    ap.add_argument("--newton-schedule", default=None,
+                    help="leading L-BFGS phases of the accuracy runs, 'prec:iters,...' (e.g. bf16:7000)")
     ap.add_argument("--lbfgs-stop", default=None, choices=["fixed", "legacy"],
                     help="L-BFGS function-change test (default: the library's, legacy = the reference's)")
     ap.add_argument("--force-dp", action="store_true",
@@ -454,7 +459,7 @@ def main(argv=None):
         try:
             acc = accuracy_runs(args.acc_seeds, device, args.backend, args.precision, args.newton_precision,
                                 args.acc_iters, args.acc_newton, args.lbfgs_stop, problem=args.problem,
-                                layers=layers)
+                                layers=layers, newton_schedule=args.newton_schedule)
         except Exception as e:  # pragma: no cover - reported, never hides the throughput number
             acc_err = f"{type(e).__name__}: {e}"
     dp = None
@@ -508,8 +513,8 @@ def main(argv=None):
                                         f"({args.newton_precision}), N_f 50000, reference examples/{ref}.py; "
                                         f"median over seeds {args.acc_seeds}")
             rec["time_to_solution_s"] = [{"adam_s": a["adam_s"], "lbfgs_s": a["lbfgs_s"]} for a in acc]
-            rec["lbfgs"] = [{"reason": a["lbfgs_reason"], "n_iter": a["lbfgs_n_iter"], "stop": a["lbfgs_stop"]}
-                            for a in acc]
+            rec["lbfgs"] = [{"reason": a["lbfgs_reason"], "n_iter": a["lbfgs_n_iter"], "stop": a["lbfgs_stop"],
+                             **({"phases": a["lbfgs_phases"]} if a.get("lbfgs_phases") else {})} for a in acc]
         elif acc_err is not None:
             rec["l2_full_schedule"] = None
             rec["accuracy_error"] = acc_err

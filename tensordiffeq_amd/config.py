@@ -9,6 +9,8 @@ backend                TDQ_BACKEND                 auto | hip | jet | autograd
 precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 MFMA operands,
                                                    fp32 accumulate / jets / master weights) | fp32
 newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision)
+newton_schedule        TDQ_NEWTON_SCHEDULE         leading L-BFGS phases "prec:iters,..." before the
+                                                   newton_precision phase (e.g. "bf16:7000")
 seed                   TDQ_SEED                    global seed applied at compile
 periodic_legacy        TDQ_PERIODIC_LEGACY         1: reference periodic-BC quirk (B12)
 log_every              TDQ_LOG_EVERY               progress / metrics cadence (steps)
@@ -55,6 +57,9 @@ class SolverConfig:
     backend: str = "auto"
     precision: str = "bf16x3"
     newton_precision: str | None = None
+    # L-BFGS precision schedule: leading phases "prec:iters[,prec:iters...]" before the
+    # newton_precision phase takes the remaining iterations (e.g. "bf16:7000")
+    newton_schedule: str | None = None
     seed: int | None = None
     periodic_legacy: bool = False
     log_every: int = 100
@@ -76,6 +81,7 @@ class SolverConfig:
             "backend": e.get("TDQ_BACKEND", cls.backend),
             "precision": e.get("TDQ_PRECISION", cls.precision),
             "newton_precision": e.get("TDQ_NEWTON_PRECISION") or None,
+            "newton_schedule": e.get("TDQ_NEWTON_SCHEDULE") or None,
             "seed": int(e["TDQ_SEED"]) if "TDQ_SEED" in e else None,
             "periodic_legacy": _env_bool("TDQ_PERIODIC_LEGACY", False),
             "log_every": int(e.get("TDQ_LOG_EVERY", cls.log_every)),
@@ -98,6 +104,7 @@ class SolverConfig:
             raise ValueError(f"precision {self.precision!r}")
         if self.newton_precision not in (None, "bf16x3", "bf16", "fp32"):
             raise ValueError(f"newton_precision {self.newton_precision!r}")
+        parse_newton_schedule(self.newton_schedule)
         if self.log_every < 1:
             raise ValueError("log_every must be >= 1")
         if self.lbfgs not in ("auto", "device", "host"):
@@ -110,3 +117,16 @@ class SolverConfig:
         os.environ["TDQ_FUSED_LOSS"] = "1" if self.fused_loss else "0"
         os.environ["TDQ_NO_GRAPH"] = "0" if self.graphs else "1"
         os.environ["TDQ_ALLOW_TORCH_FALLBACK"] = "1" if self.allow_torch_fallback else "0"
+
+
+def parse_newton_schedule(spec):
+    """``"bf16:7000,bf16x3:1000"`` -> ``[("bf16", 7000), ("bf16x3", 1000)]`` (leading L-BFGS phases)."""
+    if not spec:
+        return []
+    out = []
+    for part in str(spec).split(","):
+        prec, _, n = part.strip().partition(":")
+        if prec not in ("bf16x3", "bf16", "fp32") or not n.strip().isdigit():
+            raise ValueError(f"newton_schedule entry {part!r}: want precision:iterations")
+        out.append((prec, int(n)))
+    return out

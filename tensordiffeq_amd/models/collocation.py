@@ -85,17 +85,22 @@ class CollocationSolverND:
     def compile(self, layer_sizes, f_model, domain, bcs, Adaptive_type=0, dict_adaptive=None,
                 init_weights=None, g=None, dist=False, backend="auto", device=None,
                 periodic_legacy=False, seed=None, network=None, precision=None, metrics_path=None,
-                log_every=None, newton_precision=None, lbfgs_stop=None):
+                log_every=None, newton_precision=None, lbfgs_stop=None, newton_schedule=None):
         from ..config import SolverConfig
         self.config = SolverConfig.from_env(backend=None if backend == "auto" else backend, precision=precision,
                                             seed=seed, metrics_path=metrics_path, log_every=log_every,
-                                            newton_precision=newton_precision, lbfgs_stop=lbfgs_stop)
+                                            newton_precision=newton_precision, lbfgs_stop=lbfgs_stop,
+                                            newton_schedule=newton_schedule)
         backend = self.config.backend
         precision = self.config.precision
         # jet-GEMM precision of the L-BFGS phase (None: same as the Adam phase).  L-BFGS's
         # curvature pairs need the accurate gradient; Adam tolerates bf16 activations
         # (profiles/r2_v2_accuracy_mixed.jsonl)
         self.newton_precision = self.config.newton_precision
+        # leading L-BFGS phases in other precisions, e.g. [("bf16", 7000)]: cheaper iterations first,
+        # the newton_precision phase (fresh history from the best iterate) polishes
+        from ..config import parse_newton_schedule
+        self.newton_schedule = parse_newton_schedule(self.config.newton_schedule)
         seed = self.config.seed
         periodic_legacy = periodic_legacy or self.config.periodic_legacy
         self.log_every = self.config.log_every
@@ -359,7 +364,14 @@ class CollocationSolverND:
         eng = self._get_lbfgs_engine()
         return lambda w: eng(torch.as_tensor(w, dtype=torch.float32, device=self.device))
 
-    def _get_lbfgs_engine(self):
+    def _get_lbfgs_engine(self, precision=None):
+        if precision is not None and precision != (self.newton_precision or self.precision):
+            key = ("lbfgs_engine", precision)
+            eng = self._programs.get(key)
+            prog = self.program(precision=precision)
+            if eng is None or eng.program is not prog:
+                eng = self._programs[key] = LossGradEngine(self, prog, self.lambdas)
+            return eng
         if self._lbfgs_engine is None:
             self._lbfgs_engine = LossGradEngine(self, self.program(precision=self.newton_precision), self.lambdas)
         return self._lbfgs_engine
@@ -478,12 +490,36 @@ class CollocationSolverND:
             print(f"L-BFGS stopped after {info['n_iter']} iterations: {info['reason']}")
 
     def _fit_lbfgs_body(self, newton_iter, newton_eager):
-        """Run L-BFGS; returns ``{"impl", "n_iter", "func_evals", "reason", "stop"}``."""
+        """Run L-BFGS; returns ``{"impl", "n_iter", "func_evals", "reason", "stop"}``.  With a
+        ``newton_schedule`` the leading phases run first (each from the previous phase's best
+        iterate, device L-BFGS only), then the ``newton_precision`` phase takes the rest."""
+        sched = list(getattr(self, "newton_schedule", None) or [])
+        if sched and newton_eager and self._use_device_lbfgs():
+            phases = []
+            left = int(newton_iter)
+            for prec, n in sched:
+                n = min(n, left)
+                if n <= 0:
+                    break
+                info = self._fit_lbfgs_phase(n, self._get_lbfgs_engine(prec))
+                phases.append({"precision": prec, **{k: info[k] for k in ("n_iter", "reason")}})
+                left -= n
+            if left > 0:
+                info = self._fit_lbfgs_phase(left, self._get_lbfgs_engine())
+                phases.append({"precision": self.newton_precision or self.precision,
+                               **{k: info[k] for k in ("n_iter", "reason")}})
+            info = dict(info)
+            info["n_iter"] = sum(p["n_iter"] for p in phases)
+            info["phases"] = phases
+            return info
+        return self._fit_lbfgs_phase(newton_iter, None, newton_eager)
+
+    def _fit_lbfgs_phase(self, newton_iter, eng=None, newton_eager=True):
         ctx = self.dist_ctx
         stop = getattr(getattr(self, "config", None), "lbfgs_stop", "legacy")
         if self.verbose and ctx.rank == 0:
             print("Starting L-BFGS training")
-        eng = self._get_lbfgs_engine()
+        eng = eng if eng is not None else self._get_lbfgs_engine()
         flat = self._flat()
         bar = tqdm(total=newton_iter, disable=not (self.verbose and ctx.rank == 0), desc="L-BFGS")
 

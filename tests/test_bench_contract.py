@@ -136,3 +136,28 @@ def test_compile_dist_true_one_device_warns(tmp_path):
     assert "training at world 1" in r.stderr
     recs = [json.loads(q.read_text()) for q in sorted(tmp_path.glob("rank*.json"))]
     assert len(recs) == 1 and recs[0]["world"] == 1 and not recs[0]["dist"]
+
+
+PROBLEM_ARGS = {"ac-sa": ["--npts", "256"], "ac-baseline": ["--npts", "256"], "poisson": ["--npts", "256"],
+                "ac-dist": ["--global-npts", "512"], "discovery": ["--global-npts", "512"]}
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("problem", sorted(PROBLEM_ARGS))
+def test_bench_problems_json(problem, n):
+    """Every BASELINE.json config through the same bench contract, single process and 2 gloo ranks
+    (self-launched): one JSON line, the problem's scaling mode and point count."""
+    args = ["--steps", "2", "--warmup", "1", "--no-l2", "--min-warmup-s", "0.01", "--problem", problem,
+            "--gpus", str(n)] + PROBLEM_ARGS[problem]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       env=_env(), timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    assert rec["n_gpus"] == n and rec["config"]["problem"] == problem and rec["value"] > 0
+    strong = "--global-npts" in PROBLEM_ARGS[problem]
+    assert rec["scaling"] == ("strong" if strong else "weak")
+    assert rec["config"]["global_batch"] == (512 if strong else 256 * n)
+    assert rec["config"]["parallelism"] == f"dp{n}"
+    if problem == "discovery":
+        assert rec["unit"] == "data-pts/s"
