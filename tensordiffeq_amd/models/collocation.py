@@ -101,6 +101,12 @@ class CollocationSolverND:
         # the newton_precision phase (fresh history from the best iterate) polishes
         from ..config import parse_newton_schedule
         self.newton_schedule = parse_newton_schedule(self.config.newton_schedule)
+        if precision == "bf16" and (self.newton_precision or precision) == "bf16":
+            from .loss import _warn_once
+            _warn_once("precision='bf16' also for L-BFGS: its curvature pairs need accurate gradients (AC-SA "
+                       "stalls at L2 6-7e-2 vs 2.2e-2 with newton_precision='bf16x3'), and residuals dominated by "
+                       "second derivatives with large sources lose accuracy in bf16 (Helmholtz L2 9.4e-2 vs 7.9e-3 "
+                       "in bf16x3); consider newton_precision='bf16x3' or precision='bf16x3'")
         seed = self.config.seed
         periodic_legacy = periodic_legacy or self.config.periodic_legacy
         self.log_every = self.config.log_every
@@ -179,7 +185,12 @@ class CollocationSolverND:
                                     dtype=torch.float32).to(self.device)
                 if ctx.is_distributed:
                     ctx.broadcast_(t)
-                sharded = key == "residual" and t.numel() == self.N_f and ctx.is_distributed
+                # per-point residual weights are sharded with the points - except under
+                # Adaptive_type 2 ("outside sum": (sum_i w_i) * mean(r^2), reference utils.py:38-44),
+                # whose sum over ALL weights multiplies every rank's partial mean: those weights stay
+                # replicated and their gradient (the global mean) is all-reduced like theta's
+                sharded = (key == "residual" and t.numel() == self.N_f and ctx.is_distributed
+                           and not self.weight_outside_sum)
                 if sharded:
                     t = t.reshape(-1, 1)[self._lo:self._hi]
                 t = t.reshape(-1, 1).contiguous() if t.numel() > 1 else t.reshape(()).contiguous()
@@ -188,9 +199,6 @@ class CollocationSolverND:
                 idx.append(len(lambdas) - 1)
                 lam_for[(kinds[-1], j)] = len(lambdas) - 1
             lmap[key.lower()] = idx
-        if self.weight_outside_sum and ctx.world > 1 and any(
-                k == "residual" and l.numel() > 1 for l, k in zip(lambdas, kinds)):
-            raise NotImplementedError("Adaptive_type=2 with per-point residual weights under DP")
         self.lambdas, self.lambdas_map, self._lam_kind = lambdas, lmap, kinds
         self._lam_for = lam_for
 
@@ -346,7 +354,7 @@ class CollocationSolverND:
 
     def _lam_replicated(self):
         ctx = self.dist_ctx
-        return [not (k == "residual" and ctx.is_distributed and l.numel() > 1)
+        return [not (k == "residual" and ctx.is_distributed and l.numel() > 1 and not self.weight_outside_sum)
                 for l, k in zip(self.lambdas, self._lam_kind)]
 
     # ================================================================== loss API =========

@@ -179,6 +179,10 @@ def maybe_self_launch(n=None, why="dist=True"):
     if launcher_env() or os.environ.get("TDQ_SELF_LAUNCHED") == "1":
         return
     n = visible_devices() if n is None else int(n)
+    if n > 1 and "PYTEST_CURRENT_TEST" in os.environ:
+        # never re-run a test runner as N ranks
+        warnings.warn(f"{why}: {n} devices visible but running under pytest - training at world 1", stacklevel=3)
+        return
     if n <= 1:
         warnings.warn(f"{why}: one visible device and no launcher - training at world 1 "
                       "(launch with 'torch.distributed.run --nproc-per-node N' for N ranks)", stacklevel=3)

@@ -56,3 +56,30 @@ def test_ac_sa_reference_schedule_l2():
     print(f"ACCURACY ac-sa median l2 {med:.3e}")
     assert med < 3e-2, l2s
     assert max(l2s) < 4.5e-2, l2s
+
+
+@pytest.mark.timeout(300)
+def test_helmholtz_steady_state_reference_schedule_l2():
+    """2-D steady state (examples/steady-state.py: u_xx + u_yy + u = q, exact sin(pi x) sin(4 pi y)),
+    [2,50x4,1], N_f 10k, Adam 10k + L-BFGS 10k in bf16x3: L2 < 2e-2 (measured 7.9e-3)."""
+    res = _example("steady-state").main(["--device", "cuda", "--quiet", "--precision", "bf16x3"])
+    print(f"ACCURACY helmholtz l2 {res['l2_error']:.3e}")
+    assert res["backend"] == "hip"
+    assert res["l2_error"] < 2e-2, res
+
+
+@pytest.mark.timeout(300)
+def test_ac_discovery_recovers_coefficients():
+    """AC-discovery (examples/AC-discovery.py) on the full AC.mat field: Adam 10k (the reference
+    schedule, SA collocation weights) + 5k L-BFGS over network and coefficients: c2 within 2 %,
+    c1 within 30 % (truth 1e-4, 5; the reference marks its Adam-only version "doesnt work quite
+    yet", so parity is unpinned), in under 30 s."""
+    import time
+    t0 = time.perf_counter()
+    res = _example("AC-discovery").main(["--device", "cuda", "--quiet", "--newton", "5000"])
+    dt = time.perf_counter() - t0
+    print(f"ACCURACY discovery c1 {res['c1']:.4e} ({res['c1_rel_err']:.3f}) c2 {res['c2']:.4f} "
+          f"({res['c2_rel_err']:.4f}) wall {dt:.1f} s {res.get('wall_s')} lbfgs {res.get('lbfgs')}")
+    assert res["backend"] == "hip"
+    assert res["c2_rel_err"] < 0.02, res
+    assert res["c1_rel_err"] < 0.30, res

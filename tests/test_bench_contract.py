@@ -28,6 +28,7 @@ def _env():
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env.pop("WORLD_SIZE", None)
+    env.pop("PYTEST_CURRENT_TEST", None)   # the scripts run as plain programs, not under pytest
     env["CUDA_VISIBLE_DEVICES"] = ""
     return env
 

@@ -243,3 +243,54 @@ def test_forced_dp_world1_matches_single_process(monkeypatch):
     assert torch.allclose(torch.from_numpy(res["flat"]), ref.u_model.flat.detach(), rtol=1e-6, atol=1e-7)
     assert res["lbfgs"] == pytest.approx(ref.min_loss["l-bfgs"], rel=1e-6)
     assert res["red"] == 2   # theta + the IC's SA weights; residual SA weights stay local
+
+
+def _build_type2(dist):
+    from tests.test_solver import allen_cahn
+    D, bcs, f, _ = allen_cahn(n_f=301, sa=False)
+    g = torch.Generator().manual_seed(3)
+    kw = dict(Adaptive_type=2, dict_adaptive={"residual": [True], "BCs": [False, False]},
+              init_weights={"residual": [torch.rand(301, 1, generator=g)], "BCs": [None, None]})
+    torch.manual_seed(0)
+    m = tdq.CollocationSolverND(verbose=False)
+    m.compile([2, 12, 12, 1], f, D, bcs, backend="jet", device="cpu", dist=dist, **kw)
+    return m
+
+
+def _worker_type2(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from tensordiffeq_amd.parallel import dist as pdist
+    pdist.reset_context()
+    ctx = pdist.init_distributed(backend="gloo", device="cpu")
+    m = _build_type2(True)
+    m.fit(tf_iter=5)
+    res = {"hist": [h["Total Loss"] for h in m.losses], "flat": _np(m.u_model.flat), "lam": _np(m.lambdas[0])}
+    if rank == 0:
+        q.put(res)
+    ctx.barrier()
+    pdist.destroy()
+
+
+@pytest.mark.timeout(300)
+def test_dp_adaptive_type2_per_point_weights():
+    """Adaptive_type 2 ("loss-weights": (sum_i w_i) * mean(r^2), reference utils.py:38-44) with
+    per-point residual weights under DP: the weights stay replicated (their sum multiplies every
+    rank's partial mean) and their gradient is all-reduced - the trajectory equals single-process."""
+    ref = _build_type2(False)
+    ref.fit(tf_iter=5)
+    ref_hist = [h["Total Loss"] for h in ref.losses]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_type2, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=280)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res["hist"] == pytest.approx(ref_hist, rel=1e-4)
+    assert torch.allclose(_t(res["flat"]), ref.u_model.flat.detach(), atol=1e-5)
+    assert torch.allclose(_t(res["lam"]), ref.lambdas[0].detach(), atol=1e-5)

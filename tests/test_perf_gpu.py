@@ -1,0 +1,42 @@
+"""Step-time regression bounds on MI355X (loose: ~1.5x the measured values, box-to-box spread is
+~5 %): the flagship AC-SA bf16 Adam step (driver r03: 0.198 ms) and the AC-baseline step with its
+order-4 periodic BC on the fused path (jet_hi.hip)."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _step_ms(problem, steps=80):
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    from tensordiffeq_amd.parallel import get_context
+    dev = torch.device("cuda", 0)
+    os.environ.setdefault("TDQ_STEP_UNROLL", "8")
+    m = bench.PROBLEMS[problem]["build"](50000, 1, "auto", dev, False, "bf16",
+                                         layers=(2, 128, 128, 128, 128, 1))
+    eng = bench.get_engine(m, steps + 40)
+    el, _, _ = bench.time_steps(eng, get_context(dev), dev, steps, 10, 0.5)
+    return 1000.0 * el / steps, m
+
+
+@pytest.mark.timeout(240)
+def test_ac_sa_step_time():
+    ms, m = _step_ms("ac-sa")
+    print(f"PERF ac-sa {ms:.4f} ms/step")
+    assert m.active_backend == "hip"
+    assert ms < 0.30, ms
+
+
+@pytest.mark.timeout(240)
+def test_ac_baseline_step_time_on_fused_path():
+    ms, m = _step_ms("ac-baseline")
+    print(f"PERF ac-baseline {ms:.4f} ms/step")
+    prog = m.program()
+    assert prog.hi_op is not None and prog.fused_op is not None
+    assert ms < 0.40, ms
