@@ -570,7 +570,7 @@ template <int WT, int S, int NSO, bool LO, bool LAST>
 __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)[S][WT / 2], const Tl& Wi,
                                            const float* __restrict__ bi, const Tl& Hl, bf16x4* stage,
                                            const float* __restrict__ Ko, float (&vout)[S][TDQ_MAXO],
-                                           const JetSpec& sp, int l, int g, bool save = true) {
+                                           const JetSpec& sp, int l, int g) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, D = NSTEP < 4 ? NSTEP : 4, HL = LO ? 2 : 1;
   bf16x8 wh[D], wl[D];
 #pragma unroll
@@ -604,10 +604,8 @@ __device__ __forceinline__ void fwd_hidden(bf16x8 (&ah)[S][WT / 2], bf16x8 (&al)
       for (int s = 0; s < S; ++s) z[s] = accP[s];
       z[0] += biasP;
       tanh_jet_f<S, NSO>(sp, z, h);
-      if (save) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) hs_store<WT, LO>(Hl, s, t, h[s]);
-      }
+      for (int s = 0; s < S; ++s) hs_store<WT, LO>(Hl, s, t, h[s]);
       if (LAST) {
         out_dot<S>(h, Ko, t, g, vout);
       } else {
@@ -638,7 +636,7 @@ template <int WT, int S, int NSO, bool LO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(bf3_wpe(WT, S, LO), bf3_wpe(WT, S, LO))))
 jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, const bf16x8* __restrict__ Wimg,
                    float* __restrict__ J, float* __restrict__ Hs, int N, NetDims d, JetSpec sp, int h0r,
-                   bf16x4* __restrict__ gstage, int wg0, int save) {
+                   bf16x4* __restrict__ gstage, int wg0) {
   constexpr int KB = WT / 2, NSTEP = WT * KB, W = 16 * WT;
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -673,9 +671,8 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   // ---- layer 0 (input -> width) on VALU ---------------------------------------------------
   {
     const Tl H0 = hs_region<WT, LO>(Hs, 0, nwg, wg, S, w, l);
-    // save = 0: the backward recomputes the forward (jet_bwdr.h) - only J is written
-    const bool save_all = save && (!h0r || Lh == 1);  // else the backward rebuilds streams >= 1 (h0_stream)
-    const bool save0 = save != 0;  // (Lh = 1: the backward's output phase reads the saved layer 0)
+    const bool save_all = !h0r || Lh == 1;  // else the backward rebuilds streams >= 1 (h0_stream)
+    const bool save0 = true;  // (Lh = 1: the backward's output phase reads the saved layer 0)
     bf16x4 ph[S], pl[S];
 #pragma unroll
     for (int t = 0; t < WT; ++t) {
@@ -712,14 +709,14 @@ jet_fwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
   for (int i = 1; i < Lh - 1; ++i) {
     fwd_hidden<WT, S, NSO, LO, false>(ah, al, tl_make(Wimg + (size_t)(i - 1) * NSTEP * 128, l),
                                       aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT, LO>(Hs, i, nwg, wg, S, w, l), stage,
-                                      Ko, v, sp, l, g, save != 0);
+                                      Ko, v, sp, l, g);
     TDQ_TS(1 + i);
   }
   if (Lh >= 2) {
     const int i = Lh - 1;
     fwd_hidden<WT, S, NSO, LO, true>(ah, al, tl_make(Wimg + (size_t)(i - 1) * NSTEP * 128, l),
                                      aux + aux_bh(d, W) + (i - 1) * W, hs_region<WT, LO>(Hs, i, nwg, wg, S, w, l), stage,
-                                     Ko, v, sp, l, g, save != 0);
+                                     Ko, v, sp, l, g);
     TDQ_TS(1 + i);
   }
 
@@ -1284,8 +1281,6 @@ struct Bf3Args {
   // kernels index J / dJ, the saved activations and the slabs of the whole set N, so launches
   // over disjoint ranges may run concurrently (separate streams) into the same buffers
   int p_lo = 0, p_hi = -1;
-  const bf16x8* fimg = nullptr;  // recompute backward (jet_bwdr.h): the forward A image
-  int save = 1;                  // forward: write the saved activations (0: J only)
 };
 
 template <int WT, int S, int NSO, bool LO>
@@ -1300,7 +1295,7 @@ int launch_fwd_bf3_lo(const Bf3Args& a) {
     attr = true;
   }
   hipLaunchKernelGGL((jet_fwd_bf3_kernel<WT, S, NSO, LO>), dim3(nwg), dim3(256), lds, a.st, a.X, a.aux, a.img, a.J,
-                     a.Hs, a.N, a.d, a.sp, h0_recompute(), a.gstage, wg0, a.save);
+                     a.Hs, a.N, a.d, a.sp, h0_recompute(), a.gstage, wg0);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -1331,16 +1326,6 @@ int launch_bwd_bf3_lo(const Bf3Args& a) {
 template <int WT, int S, int NSO>
 int launch_bwd_bf3(const Bf3Args& a) {
   return a.lo ? launch_bwd_bf3_lo<WT, S, NSO, true>(a) : launch_bwd_bf3_lo<WT, S, NSO, false>(a);
-}
-
-// recompute backward (jet_bwdr.hip): active for this geometry / precision?
-bool bwdr_active(int WT, int S, int n_hidden, int lo);
-int bwdr_dispatch(int WT, int S, int nso, int n_hidden, const Bf3Args& a);
-
-// points per backward workgroup = the gradient slab row granularity: 64 for the recompute
-// backward, else 16 x bwd_waves
-inline int bwd_pts(int WT, int S, int n_hidden, int lo) {
-  return bwdr_active(WT, S, n_hidden, lo) ? 64 : 16 * bwd_waves(WT, lo != 0, S);
 }
 
 // per-width-class entry points (jet_bf3_w{2,4,8}.hip); return hipErrorInvalidValue when

@@ -433,8 +433,6 @@ int tdq_jet_fwd_bf3_range(const float* X, const float* P, float* J, float* scrat
   }
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
             scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), p_lo, p_hi};
-  // the recompute backward rebuilds the activations: the forward writes J only
-  a.save = bwdr_active(WT, S, n_hidden, lo) ? 0 : 1;
   return dispatch(true, WT, S, nso, a);
 }
 
@@ -486,11 +484,6 @@ int tdq_jet_bwd_bf3_range(const float* X, const float* dJ, const float* Hs, floa
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), work, N,
             slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo),
             p_lo, p_hi};
-  if (bwdr_active(WT, S, n_hidden, lo)) {  // jet_bwdr.h: the forward recomputed on chip
-    if (p_lo % 64 != 0) return (int)hipErrorInvalidValue;
-    a.fimg = reinterpret_cast<const bf16x8*>(img);
-    return bwdr_dispatch(WT, S, nso, n_hidden, a);
-  }
   return dispatch(false, WT, S, nso, a);
 }
 
@@ -505,7 +498,7 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   NetDims d;
   make_dims(d, d_in, widths, 0, d_out, n_hidden);
   const int WT = width_tiles(d.width);
-  const int pts_b = bwd_pts(WT, S, n_hidden, lo), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
   const int Ptot = param_count(d);
   return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, slab_chunks(nwg_b), (int)slab_half(lo != 0), stream);
 }
@@ -538,7 +531,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
   args.grp[0].g = grad;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int pts_b = bwd_pts(WT, S, n_hidden, lo), nwg_b = (N + pts_b - 1) / pts_b;
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -596,7 +589,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
     return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d);
-  const int pts_b = bwd_pts(WT, S, n_hidden, lo), nwg_b = (N + pts_b - 1) / pts_b;
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -625,7 +618,7 @@ int tdq_bf3_slab_geometry(int N, int d_in, const int* widths, int d_out, int n_h
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
-  const int pts_b = bwd_pts(WT, S, n_hidden, lo), nwg_b = (N + pts_b - 1) / pts_b, chunks = slab_chunks(nwg_b);
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b, chunks = slab_chunks(nwg_b);
   out[0] = pts_b;
   out[1] = nwg_b;
   out[2] = chunks;
@@ -644,7 +637,7 @@ int tdq_slab_prereduce_bf3(float* work, int N, int d_in, const int* widths, int 
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
   const int Ptot = param_count(d);
-  const int pts_b = bwd_pts(WT, S, n_hidden, lo), nwg_b = (N + pts_b - 1) / pts_b;
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c0 < 0 || c1 > chunks || c1 <= c0) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;

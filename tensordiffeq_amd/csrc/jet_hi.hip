@@ -19,19 +19,30 @@
 // d/dz tanh^(k) = tanh^(k+1).  The forward saves every hidden layer's PRE-activation streams z
 // (fp32, [layer][point][stream][feature]) - order >= 3 adjoints need z itself, not only h.
 //
-// Layout: one workgroup = 256 threads = NP points; thread t owns feature f = t & 127 of the points
-// p = (t >> 7) * NP/2 + pp; a layer's weights are staged in LDS (row stride 129 floats: the
-// forward reads W[k][f] along f, the backward W[k][f] along k, both conflict-free), activations
-// / adjoints of the workgroup's points live in LDS for the GEMMs.  dK partials of a workgroup
-// are one slab row (flat Keras order); tdq_jet_hi_bwd reduces the rows in a fixed order
+// Layout: one workgroup = 1024 threads = 8 points; thread t owns feature f = t & 127 of point
+// p = t >> 7 (GEMM rows = the point's S streams); a layer's weights are staged in LDS (row stride
+// 129 floats: the forward reads W[k][f] along f, the backward W[k][f] along k, both conflict-free),
+// activations / adjoints of the workgroup's points live in LDS for the GEMMs.  dK partials of a
+// workgroup are one slab row (flat Keras order); tdq_jet_hi_bwd reduces the rows in a fixed order
 // (deterministic) into its own gradient vector, which the fused step tail adds to theta's.
+// The stream count is a template parameter, and the common plan - the univariate chain
+// u, u_v, u_vv, u_vvv(, u_vvvv) of the reference's periodic BCs - has its tanh jet and adjoint as
+// straight-line code; other plans interpret the partition table (uniform kernel-argument reads).
+// First build (256 threads, 4 points, interpreted jets, table in LDS): 0.31 + 0.40 ms per AC-baseline
+// step (profiles/r4b_kernel_stats_ac_baseline_slow_hi.txt).
 #include "jet_common.h"
 
 #define HI_MAXS 8
 #define HI_MAXT 48
 #define HI_MAXB 4
 #define HI_W 128
-#define HI_NP 4
+#define HI_TG 2                      // 128-thread groups per workgroup (one feature per thread)
+#define HI_PT 2                      // points per thread
+#define HI_NP (HI_TG * HI_PT)        // points per workgroup
+#define HI_THREADS (HI_W * HI_TG)
+#define HI_WS (HI_W + 4)             // LDS row strides (float4 rows, conflict-free)
+#define HI_AS (HI_W + 4)
+#define HI_KS 8                      // point splits of the weight-gradient pass (slab rows)
 
 struct HiSpec {
   int S;
@@ -43,17 +54,11 @@ struct HiSpec {
   float tc[HI_MAXT];   // coefficient
   int tnb[HI_MAXT];    // factor count
   int tb[HI_MAXT][HI_MAXB];  // factor streams
+  int chain;           // 1: streams are the univariate chain (), (v), (v,v), ... of one variable
 };
 
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-
-// uniform (wave-invariant) index into an SGPR: dynamic vector element access then lowers to
-// v_movrels / v_movreld with M0 instead of a private-memory array (a select chain over a register
-// array is turned back into scratch indexing by LLVM)
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
 // tanh and its derivatives 1..5 at z: sg[0] = h, sg[k] = tanh^(k)(z)
-__device__ __forceinline__ f32x8 hi_sigmas(float z) {
+__device__ __forceinline__ void hi_sigmas(float z, float (&sg)[6]) {
   const float az = fabsf(z);
   const float e = __expf(-2.f * az);
   const float r = 1.f / (1.f + e);
@@ -63,52 +68,107 @@ __device__ __forceinline__ f32x8 hi_sigmas(float z) {
   const float h = copysignf(t, z);
   const float s1 = 4.f * e * (r * r);
   const float h2 = h * h;
-  f32x8 sg = {h, s1, -2.f * h * s1, s1 * fmaf(6.f, h2, -2.f), s1 * h * fmaf(-24.f, h2, 16.f),
-              s1 * fmaf(h2, fmaf(120.f, h2, -120.f), 16.f), 0.f, 0.f};
-  return sg;
+  sg[0] = h;
+  sg[1] = s1;
+  sg[2] = -2.f * h * s1;
+  sg[3] = s1 * fmaf(6.f, h2, -2.f);
+  sg[4] = s1 * h * fmaf(-24.f, h2, 16.f);
+  sg[5] = s1 * fmaf(h2, fmaf(120.f, h2, -120.f), 16.f);
 }
 
-// forward tanh jet of one (point, feature): z -> h (streams as vector lanes)
-__device__ __forceinline__ f32x8 hi_tanh_f(const HiSpec& sp, const f32x8 z) {
-  const f32x8 sg = hi_sigmas(z[0]);
-  f32x8 h = {sg[0], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int S = uni(sp.S);
+// univariate chain z_k = d^k z / dv^k (k < S): Faa di Bruno written out, order <= 4
+template <int S>
+__device__ __forceinline__ void chain_f(const float (&z)[S], float (&h)[S]) {
+  float sg[6];
+  hi_sigmas(z[0], sg);
+  h[0] = sg[0];
+  if constexpr (S > 1) h[1] = sg[1] * z[1];
+  if constexpr (S > 2) h[2] = fmaf(sg[1], z[2], sg[2] * z[1] * z[1]);
+  if constexpr (S > 3) h[3] = sg[1] * z[3] + 3.f * sg[2] * z[1] * z[2] + sg[3] * z[1] * z[1] * z[1];
+  if constexpr (S > 4)
+    h[4] = sg[1] * z[4] + sg[2] * (4.f * z[1] * z[3] + 3.f * z[2] * z[2]) + 6.f * sg[3] * z[1] * z[1] * z[2] +
+           sg[4] * z[1] * z[1] * z[1] * z[1];
+}
+template <int S>
+__device__ __forceinline__ void chain_b(const float (&z)[S], const float (&hb)[S], float (&zb)[S]) {
+  float sg[6];
+  hi_sigmas(z[0], sg);
+  zb[0] = sg[1] * hb[0];
+  if constexpr (S > 1) {
+    zb[0] += sg[2] * z[1] * hb[1];
+    zb[1] = sg[1] * hb[1];
+  }
+  if constexpr (S > 2) {
+    zb[0] += (sg[2] * z[2] + sg[3] * z[1] * z[1]) * hb[2];
+    zb[1] += 2.f * sg[2] * z[1] * hb[2];
+    zb[2] = sg[1] * hb[2];
+  }
+  if constexpr (S > 3) {
+    zb[0] += (sg[2] * z[3] + 3.f * sg[3] * z[1] * z[2] + sg[4] * z[1] * z[1] * z[1]) * hb[3];
+    zb[1] += (3.f * sg[2] * z[2] + 3.f * sg[3] * z[1] * z[1]) * hb[3];
+    zb[2] += 3.f * sg[2] * z[1] * hb[3];
+    zb[3] = sg[1] * hb[3];
+  }
+  if constexpr (S > 4) {
+    zb[0] += (sg[2] * z[4] + sg[3] * (4.f * z[1] * z[3] + 3.f * z[2] * z[2]) + 6.f * sg[4] * z[1] * z[1] * z[2] +
+              sg[5] * z[1] * z[1] * z[1] * z[1]) * hb[4];
+    zb[1] += (4.f * sg[2] * z[3] + 12.f * sg[3] * z[1] * z[2] + 4.f * sg[4] * z[1] * z[1] * z[1]) * hb[4];
+    zb[2] += (6.f * sg[2] * z[2] + 6.f * sg[3] * z[1] * z[1]) * hb[4];
+    zb[3] += 4.f * sg[2] * z[1] * hb[4];
+    zb[4] = sg[1] * hb[4];
+  }
+}
+
+// generic plans: the partition table, read with wave-uniform indices from the kernel arguments
+template <int S>
+__device__ __forceinline__ float zsel(const float (&z)[S], int idx) {
+  float r = z[0];
+#pragma unroll
+  for (int q = 1; q < S; ++q) r = idx == q ? z[q] : r;
+  return r;
+}
+template <int S>
+__device__ __forceinline__ void table_f(const HiSpec& sp, const float (&z)[S], float (&h)[S]) {
+  float sg[6];
+  hi_sigmas(z[0], sg);
+  h[0] = sg[0];
+#pragma unroll
   for (int s = 1; s < S; ++s) {
     float a = 0.f;
-    const int t0 = uni(sp.t0[s]), t1 = t0 + uni(sp.nt[s]);
-    for (int t = t0; t < t1; ++t) {
-      float v = sp.tc[t] * sg[uni(sp.tk[t])];
-      const int nb = uni(sp.tnb[t]);
-      for (int b = 0; b < nb; ++b) v *= z[uni(sp.tb[t][b])];
+    for (int t = sp.t0[s]; t < sp.t0[s] + sp.nt[s]; ++t) {
+      const int k = sp.tk[t];
+      float v = sp.tc[t] * (k == 1 ? sg[1] : k == 2 ? sg[2] : k == 3 ? sg[3] : sg[4]);
+      for (int b = 0; b < sp.tnb[t]; ++b) v *= zsel(z, sp.tb[t][b]);
       a += v;
     }
     h[s] = a;
   }
-  return h;
 }
-
-// adjoint of the tanh jet: (z, hb) -> zb
-__device__ __forceinline__ f32x8 hi_tanh_b(const HiSpec& sp, const f32x8 z, const f32x8 hb) {
-  const f32x8 sg = hi_sigmas(z[0]);
-  f32x8 zb = {hb[0] * sg[1], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int S = uni(sp.S);
+template <int S>
+__device__ __forceinline__ void table_b(const HiSpec& sp, const float (&z)[S], const float (&hb)[S], float (&zb)[S]) {
+  float sg[6];
+  hi_sigmas(z[0], sg);
+#pragma unroll
+  for (int s = 0; s < S; ++s) zb[s] = 0.f;
+  zb[0] = hb[0] * sg[1];
+#pragma unroll
   for (int s = 1; s < S; ++s) {
     const float g = hb[s];
-    const int t0 = uni(sp.t0[s]), t1 = t0 + uni(sp.nt[s]);
-    for (int t = t0; t < t1; ++t) {
-      const int k = uni(sp.tk[t]), nb = uni(sp.tnb[t]);
+    for (int t = sp.t0[s]; t < sp.t0[s] + sp.nt[s]; ++t) {
+      const int k = sp.tk[t], nb = sp.tnb[t];
       const float base = sp.tc[t] * g;
-      int ib[HI_MAXB];
       float fac[HI_MAXB];
+      int ib[HI_MAXB];
       float prod = 1.f;
 #pragma unroll
       for (int b = 0; b < HI_MAXB; ++b) {
-        ib[b] = b < nb ? uni(sp.tb[t][b]) : 0;
-        fac[b] = b < nb ? z[ib[b]] : 1.f;
+        ib[b] = b < nb ? sp.tb[t][b] : 0;
+        fac[b] = b < nb ? zsel(z, ib[b]) : 1.f;
         prod *= fac[b];
       }
-      zb[0] += base * sg[k + 1] * prod;  // d tanh^(k)(z0) / dz0 = tanh^(k+1)
-      const float bk = base * sg[k];
+      const float sk = k == 1 ? sg[1] : k == 2 ? sg[2] : k == 3 ? sg[3] : sg[4];
+      const float sk1 = k == 1 ? sg[2] : k == 2 ? sg[3] : k == 3 ? sg[4] : sg[5];
+      zb[0] += base * sk1 * prod;  // d tanh^(k)(z0) / dz0 = tanh^(k+1)
 #pragma unroll
       for (int b = 0; b < HI_MAXB; ++b) {
         if (b >= nb) continue;
@@ -116,292 +176,337 @@ __device__ __forceinline__ f32x8 hi_tanh_b(const HiSpec& sp, const f32x8 z, cons
 #pragma unroll
         for (int c = 0; c < HI_MAXB; ++c)
           if (c != b) others *= fac[c];
-        zb[ib[b]] += bk * others;
+        const float v = base * sk * others;
+#pragma unroll
+        for (int q = 0; q < S; ++q) zb[q] += ib[b] == q ? v : 0.f;
       }
     }
   }
-  return zb;
 }
 
+template <int S, bool CH>
+__device__ __forceinline__ void hi_tanh_f(const HiSpec& sp, const float (&z)[S], float (&h)[S]) {
+  if constexpr (CH)
+    chain_f<S>(z, h);
+  else
+    table_f<S>(sp, z, h);
+}
+template <int S, bool CH>
+__device__ __forceinline__ void hi_tanh_b(const HiSpec& sp, const float (&z)[S], const float (&hb)[S], float (&zb)[S]) {
+  if constexpr (CH)
+    chain_b<S>(z, hb, zb);
+  else
+    table_b<S>(sp, z, hb, zb);
+}
+
+// LDS of the chain kernels: one layer's weights (row stride 132: the forward reads W[k][f] along f,
+// the backward float4 rows W[f][o..o+3], both conflict-free) + the workgroup's activations /
+// adjoints (read as float4 broadcasts: every lane of a 128-thread group reads the same point)
 struct HiShared {
-  float W[HI_W][HI_W + 1];
-  float A[HI_NP][HI_MAXS][HI_W];  // activations h of the workgroup's points (GEMM operand)
-  float G[HI_NP][HI_MAXS][HI_W];  // adjoints zb (backward)
-  float red[2][HI_W * TDQ_MAXO];  // per-half partials of bias / K0 / Ko gradients
-  HiSpec sp;
+  float W[HI_W][HI_WS];
+  float A[HI_NP][HI_MAXS][HI_AS];
 };
 
-__device__ __forceinline__ void hi_load_spec(HiSpec& dst, const HiSpec& src) {
-  const int n = (int)(sizeof(HiSpec) / 4);
-  for (int e = threadIdx.x; e < n; e += blockDim.x) reinterpret_cast<int*>(&dst)[e] = reinterpret_cast<const int*>(&src)[e];
-}
-
-// W (in x out, row-major) of dense layer `layer` into LDS
+// W (in x out) of dense layer `layer` into LDS, zero-padded to HI_W columns and to a multiple of 4 rows
 __device__ __forceinline__ void hi_stage_w(HiShared& sh, const float* __restrict__ P, const NetDims& d, int layer) {
   const float* K = P + off_layer(d, layer);
-  const int win = hw(d, layer - 1), wout = hw(d, layer);
-  for (int e = threadIdx.x; e < win * wout; e += blockDim.x) {
-    const int k = e / wout, f = e - k * wout;
-    sh.W[k][f] = K[e];
+  const int win = hw(d, layer - 1), wout = hw(d, layer), rows = (win + 3) & ~3;
+  for (int e = threadIdx.x; e < rows * HI_W; e += blockDim.x) {
+    const int k = e >> 7, f = e & (HI_W - 1);
+    sh.W[k][f] = (k < win && f < wout) ? K[k * wout + f] : 0.f;
   }
 }
 
-// Z scratch: [layer][point][stream][HI_W]
-__device__ __forceinline__ size_t hi_zoff(int layer, int n, int s, int f, int N) {
-  return (((size_t)layer * N + n) * HI_MAXS + s) * HI_W + f;
+// activation-sized scratch: [layer][n * S + s][HI_W] (Z: pre-activations, H: post-activations,
+// B: adjoints of the pre-activations)
+__device__ __forceinline__ size_t hi_row(int layer, int n, int s, int S, int N) {
+  return (((size_t)layer * N + n) * S + s) * HI_W;
 }
 
-__global__ void __launch_bounds__(256) jet_hi_fwd_kernel(const float* __restrict__ X, int N, const float* __restrict__ P,
-                                                         NetDims d, HiSpec spk, float* __restrict__ J, int ldJ, int j0,
-                                                         float* __restrict__ Z) {
+// thread (f, pg): feature f of points 2 pg, 2 pg + 1 of the workgroup's HI_NP
+template <int S, bool CH>
+__global__ void __launch_bounds__(HI_THREADS) jet_hi_fwd_kernel(const float* __restrict__ X, int N,
+                                                                const float* __restrict__ P, NetDims d, HiSpec sp,
+                                                                float* __restrict__ J, int ldJ, int j0,
+                                                                float* __restrict__ Zb, float* __restrict__ Hb) {
   extern __shared__ __attribute__((aligned(16))) char hi_lds[];
   HiShared& sh = *reinterpret_cast<HiShared*>(hi_lds);
-  constexpr int PPH = HI_NP / 2;
-  const int t = threadIdx.x, f = t & 127, half = t >> 7;
-  hi_load_spec(sh.sp, spk);
-  __syncthreads();
-  const HiSpec& sp = sh.sp;
-  const int S = uni(sp.S), Lh = d.n_hidden;
-  int n[PPH];
-  bool ok[PPH];
+  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
+  const int Lh = d.n_hidden;
+  int n[HI_PT];
+  bool ok[HI_PT];
 #pragma unroll
-  for (int pp = 0; pp < PPH; ++pp) {
-    const int nn = blockIdx.x * HI_NP + half * PPH + pp;
-    ok[pp] = nn < N;
-    n[pp] = ok[pp] ? nn : N - 1;
+  for (int j = 0; j < HI_PT; ++j) {
+    const int m = blockIdx.x * HI_NP + pg * HI_PT + j;
+    ok[j] = m < N;
+    n[j] = ok[j] ? m : N - 1;
   }
-  f32x8 z[PPH];
-  // ---- layer 0: z = x K0 + b0 (value), K0[var] (first order), 0 (higher) ------------------
-  {
+  float z[HI_PT][S];
+  {  // layer 0: z = x K0 + b0 (value), K0[var] (first order), 0 (higher)
     const int w0 = hw(d, 0);
 #pragma unroll
-    for (int pp = 0; pp < PPH; ++pp) {
-      z[pp] = f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (f < w0) {
-        float a = P[d.d_in * w0 + f];
-        for (int j = 0; j < d.d_in; ++j) a = fmaf(X[(size_t)n[pp] * d.d_in + j], P[j * w0 + f], a);
-        z[pp][0] = a;
+    for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-        for (int s = 1; s < HI_MAXS; ++s)
-          if (s < S && sp.order[s] == 1) z[pp][s] = P[sp.var[s] * w0 + f];
+      for (int s = 0; s < S; ++s) z[j][s] = 0.f;
+    if (f < w0) {
+#pragma unroll
+      for (int j = 0; j < HI_PT; ++j) {
+        float a = P[d.d_in * w0 + f];
+        for (int v = 0; v < d.d_in; ++v) a = fmaf(X[(size_t)n[j] * d.d_in + v], P[v * w0 + f], a);
+        z[j][0] = a;
+#pragma unroll
+        for (int s = 1; s < S; ++s)
+          if (sp.order[s] == 1) z[j][s] = P[sp.var[s] * w0 + f];
       }
     }
   }
+  if (Lh > 1) hi_stage_w(sh, P, d, 1);
   for (int i = 0; i < Lh; ++i) {
     const int wi = hw(d, i);
     if (i >= 1) {  // z_i = h_{i-1} W_i (+ b_i): h_{i-1} in sh.A, W_i staged in sh.W
-      const int win = hw(d, i - 1);
-      const float* bi = P + off_layer(d, i) + win * wi;
+      const int kin = (hw(d, i - 1) + 3) & ~3;
 #pragma unroll
-      for (int pp = 0; pp < PPH; ++pp) z[pp] = f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < HI_PT; ++j)
+#pragma unroll
+        for (int s = 0; s < S; ++s) z[j][s] = 0.f;
+      for (int k = 0; k < kin; k += 4) {
+        const float w0 = sh.W[k][f], w1 = sh.W[k + 1][f], w2 = sh.W[k + 2][f], w3 = sh.W[k + 3][f];
+#pragma unroll
+        for (int j = 0; j < HI_PT; ++j)
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][k]);
+            z[j][s] = fmaf(a[0], w0, fmaf(a[1], w1, fmaf(a[2], w2, fmaf(a[3], w3, z[j][s]))));
+          }
+      }
       if (f < wi) {
-        for (int k = 0; k < win; ++k) {
-          const float w = sh.W[k][f];
+        const float b = P[off_layer(d, i) + hw(d, i - 1) * wi + f];
 #pragma unroll
-          for (int pp = 0; pp < PPH; ++pp)
-#pragma unroll
-            for (int s = 0; s < HI_MAXS; ++s)
-              if (s < S) z[pp][s] = fmaf(sh.A[half * PPH + pp][s][k], w, z[pp][s]);
-        }
-#pragma unroll
-        for (int pp = 0; pp < PPH; ++pp) z[pp][0] += bi[f];
+        for (int j = 0; j < HI_PT; ++j) z[j][0] += b;
       }
       __syncthreads();  // every thread done reading sh.A / sh.W
+      if (i + 1 < Lh) hi_stage_w(sh, P, d, i + 1);
     }
-    // save z, apply the tanh jet, publish h for the next layer's GEMM
 #pragma unroll
-    for (int pp = 0; pp < PPH; ++pp) {
+    for (int j = 0; j < HI_PT; ++j) {
+      float h[S];
       if (f < wi) {
-        if (ok[pp]) {
+        hi_tanh_f<S, CH>(sp, z[j], h);
+      } else {
 #pragma unroll
-          for (int s = 0; s < HI_MAXS; ++s)
-            if (s < S) Z[hi_zoff(i, n[pp], s, f, N)] = z[pp][s];
-        }
-        const f32x8 h = hi_tanh_f(sp, z[pp]);
-#pragma unroll
-        for (int s = 0; s < HI_MAXS; ++s)
-          if (s < S) sh.A[half * PPH + pp][s][f] = h[s];
+        for (int s = 0; s < S; ++s) h[s] = 0.f;
       }
+      if (ok[j]) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          Zb[hi_row(i, n[j], s, S, N) + f] = z[j][s];
+          Hb[hi_row(i, n[j], s, S, N) + f] = h[s];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = h[s];
     }
-    if (i + 1 < Lh) hi_stage_w(sh, P, d, i + 1);
     __syncthreads();
   }
   // ---- output layer: u_s[q] = sum_f h_s[f] Ko[f][q] (+ bo[q] on the value stream) -----------
   const int wl = hw(d, Lh - 1), dout = d.d_out;
   const float* Ko = P + off_layer(d, Lh);
   for (int c = t; c < HI_NP * S * dout; c += blockDim.x) {
-    const int q = c % dout, s = (c / dout) % S, p = c / (dout * S);
-    const int nn = blockIdx.x * HI_NP + p;
-    if (nn >= N || sp.out[s] < 0) continue;
+    const int q = c % dout, s = (c / dout) % S, pp = c / (dout * S);
+    const int m = blockIdx.x * HI_NP + pp;
+    if (m >= N || sp.out[s] < 0) continue;
     float a = s == 0 ? Ko[wl * dout + q] : 0.f;
-    for (int k = 0; k < wl; ++k) a = fmaf(sh.A[p][s][k], Ko[k * dout + q], a);
-    J[((size_t)sp.out[s] * ldJ + j0 + nn) * dout + q] = a;
+    for (int k = 0; k < wl; ++k) a = fmaf(sh.A[pp][s][k], Ko[k * dout + q], a);
+    J[((size_t)sp.out[s] * ldJ + j0 + m) * dout + q] = a;
   }
 }
 
-__global__ void __launch_bounds__(256) jet_hi_bwd_kernel(const float* __restrict__ X, int N, const float* __restrict__ P,
-                                                         NetDims d, HiSpec spk, const float* __restrict__ dJ, int ldJ,
-                                                         int j0, const float* __restrict__ Z, float* __restrict__ slab,
-                                                         int Pst) {
+// adjoint chain: hb of the last hidden layer from dJ, then zb_i = tanh-jet adjoint, hb_{i-1} = W_i zb_i;
+// zb_i -> Bb (the weight gradients are jet_hi_wgrad_kernel's)
+template <int S, bool CH>
+__global__ void __launch_bounds__(HI_THREADS) jet_hi_chain_kernel(int N, const float* __restrict__ P, NetDims d,
+                                                                  HiSpec sp, const float* __restrict__ dJ, int ldJ,
+                                                                  int j0, const float* __restrict__ Zb,
+                                                                  float* __restrict__ Bb) {
   extern __shared__ __attribute__((aligned(16))) char hi_lds[];
   HiShared& sh = *reinterpret_cast<HiShared*>(hi_lds);
-  constexpr int PPH = HI_NP / 2;
-  const int t = threadIdx.x, f = t & 127, half = t >> 7;
-  hi_load_spec(sh.sp, spk);
-  __syncthreads();
-  const HiSpec& sp = sh.sp;
-  const int S = uni(sp.S), Lh = d.n_hidden, dout = d.d_out;
-  float* row = slab + (size_t)blockIdx.x * Pst;
-  int n[PPH];
-  bool ok[PPH];
+  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
+  const int Lh = d.n_hidden, dout = d.d_out;
+  int n[HI_PT];
+  bool ok[HI_PT];
 #pragma unroll
-  for (int pp = 0; pp < PPH; ++pp) {
-    const int nn = blockIdx.x * HI_NP + half * PPH + pp;
-    ok[pp] = nn < N;
-    n[pp] = ok[pp] ? nn : N - 1;
+  for (int j = 0; j < HI_PT; ++j) {
+    const int m = blockIdx.x * HI_NP + pg * HI_PT + j;
+    ok[j] = m < N;
+    n[j] = ok[j] ? m : N - 1;
   }
-  const f32x8 zero8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  // ---- output layer ---------------------------------------------------------------------------
   const int wl = hw(d, Lh - 1);
   const float* Ko = P + off_layer(d, Lh);
-  f32x8 zr[PPH], hb[PPH];
-  {
-    // h of the last hidden layer (from its saved z) -> dKo, and hb = Ko ub
-    float part[TDQ_MAXO] = {0.f, 0.f, 0.f, 0.f};
+  float hb[HI_PT][S];
 #pragma unroll
-    for (int pp = 0; pp < PPH; ++pp) {
-      zr[pp] = zero8;
-      hb[pp] = zero8;
+  for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-      for (int s = 0; s < HI_MAXS; ++s)
-        if (f < wl && s < S) zr[pp][s] = Z[hi_zoff(Lh - 1, n[pp], s, f, N)];
-      if (f < wl) {
-        const f32x8 h = hi_tanh_f(sp, zr[pp]);
-#pragma unroll
-        for (int s = 0; s < HI_MAXS; ++s) {
-          const int orow = sp.out[s];
-          if (s >= S || orow < 0 || !ok[pp]) continue;
-#pragma unroll
-          for (int q = 0; q < TDQ_MAXO; ++q) {
-            if (q >= dout) continue;
-            const float u = dJ[((size_t)orow * ldJ + j0 + n[pp]) * dout + q];
-            part[q] = fmaf(h[s], u, part[q]);
-            hb[pp][s] = fmaf(Ko[f * dout + q], u, hb[pp][s]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < TDQ_MAXO; ++q) sh.red[half][f * TDQ_MAXO + q] = part[q];
-    __syncthreads();
-    if (half == 0 && f < wl)
-      for (int q = 0; q < dout; ++q)
-        row[off_layer(d, Lh) + f * dout + q] = sh.red[0][f * TDQ_MAXO + q] + sh.red[1][f * TDQ_MAXO + q];
-    if (t < dout) {
+    for (int s = 0; s < S; ++s) {
       float a = 0.f;
-      for (int p = 0; p < HI_NP; ++p) {
-        const int nn = blockIdx.x * HI_NP + p;
-        if (nn < N && sp.out[0] >= 0) a += dJ[((size_t)sp.out[0] * ldJ + j0 + nn) * dout + t];
-      }
-      row[off_layer(d, Lh) + wl * dout + t] = a;
+      const int orow = sp.out[s];
+      if (f < wl && orow >= 0 && ok[j])
+        for (int q = 0; q < dout; ++q) a = fmaf(Ko[f * dout + q], dJ[((size_t)orow * ldJ + j0 + n[j]) * dout + q], a);
+      hb[j][s] = a;
     }
-    __syncthreads();
-  }
-  // ---- hidden layers, top down: hb (adjoint of h_i) -> zb_i -> db_i, dK_i, hb_{i-1} ------------
   for (int i = Lh - 1; i >= 0; --i) {
     const int wi = hw(d, i);
-    f32x8 zb[PPH];
-    float bpart = 0.f;
 #pragma unroll
-    for (int pp = 0; pp < PPH; ++pp) {
-      zb[pp] = f < wi ? hi_tanh_b(sp, zr[pp], hb[pp]) : zero8;
-      bpart += zb[pp][0];
+    for (int j = 0; j < HI_PT; ++j) {
+      float z[S], zb[S];
 #pragma unroll
-      for (int s = 0; s < HI_MAXS; ++s)
-        if (s < S) sh.G[half * PPH + pp][s][f] = zb[pp][s];
-    }
-    sh.red[half][f] = bpart;
-    if (i == 0) {
-      // K0[j][f] = sum_p x_j zb_value + sum_{first-order streams of variable j} zb_s
-      for (int j = 0; j < d.d_in; ++j) {
-        float a = 0.f;
+      for (int s = 0; s < S; ++s) z[s] = f < wi ? Zb[hi_row(i, n[j], s, S, N) + f] : 0.f;
+      if (f < wi) {
+        hi_tanh_b<S, CH>(sp, z, hb[j], zb);
+      } else {
 #pragma unroll
-        for (int pp = 0; pp < PPH; ++pp) {
-          float v = X[(size_t)n[pp] * d.d_in + j] * zb[pp][0];
-#pragma unroll
-          for (int s = 1; s < HI_MAXS; ++s)
-            if (s < S && sp.order[s] == 1 && sp.var[s] == j) v += zb[pp][s];
-          a += v;
-        }
-        sh.red[half][HI_W * (1 + j % 3) + f] = a;  // slots 1..3 of the 4 x 128 area (3 variables per pass)
-        if (j % 3 == 2 || j + 1 == d.d_in) {
-          __syncthreads();
-          if (half == 0 && f < wi)
-            for (int jj = j - j % 3; jj <= j; ++jj)
-              row[jj * wi + f] = sh.red[0][HI_W * (1 + jj % 3) + f] + sh.red[1][HI_W * (1 + jj % 3) + f];
-          __syncthreads();
-        }
+        for (int s = 0; s < S; ++s) zb[s] = 0.f;
       }
-      if (half == 0 && f < wi) row[d.d_in * wi + f] = sh.red[0][f] + sh.red[1][f];
-      break;
+      if (ok[j]) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) Bb[hi_row(i, n[j], s, S, N) + f] = zb[s];
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = zb[s];
     }
-    // h_{i-1} from its saved z (thread feature f of layer i-1) into sh.A; W_i into sh.W
-    const int wp = hw(d, i - 1);
-#pragma unroll
-    for (int pp = 0; pp < PPH; ++pp) {
-      zr[pp] = zero8;
-#pragma unroll
-      for (int s = 0; s < HI_MAXS; ++s)
-        if (f < wp && s < S) zr[pp][s] = Z[hi_zoff(i - 1, n[pp], s, f, N)];
-      const f32x8 h = f < wp ? hi_tanh_f(sp, zr[pp]) : zero8;
-#pragma unroll
-      for (int s = 0; s < HI_MAXS; ++s)
-        if (s < S) sh.A[half * PPH + pp][s][f] = h[s];
-    }
+    if (i == 0) break;
+    // hb_{i-1}[k = f] = sum_o zb_i[o] W_i[f][o]
     hi_stage_w(sh, P, d, i);
     __syncthreads();
-    // bias of layer i (both halves' partials landed)
-    if (half == 0 && f < wi) row[off_layer(d, i) + wp * wi + f] = sh.red[0][f] + sh.red[1][f];
-    // dK_i[k][f] = sum over (point, stream) of h_{i-1}[k] zb_i[f]: thread (f, half) owns k in
-    // [64 half, 64 half + 64)
-    if (f < wi) {
-      float acc[64];
+    const int wp = hw(d, i - 1), oin = (wi + 3) & ~3;
 #pragma unroll
-      for (int kk = 0; kk < 64; ++kk) acc[kk] = 0.f;
-      for (int p = 0; p < HI_NP; ++p)
-        for (int s = 0; s < S; ++s) {
-          const float g = sh.G[p][s][f];
-          const f32x4* a4 = reinterpret_cast<const f32x4*>(&sh.A[p][s][64 * half]);
+    for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-          for (int k4 = 0; k4 < 16; ++k4) {
-            const f32x4 hv = a4[k4];
-            acc[4 * k4] = fmaf(hv[0], g, acc[4 * k4]);
-            acc[4 * k4 + 1] = fmaf(hv[1], g, acc[4 * k4 + 1]);
-            acc[4 * k4 + 2] = fmaf(hv[2], g, acc[4 * k4 + 2]);
-            acc[4 * k4 + 3] = fmaf(hv[3], g, acc[4 * k4 + 3]);
-          }
-        }
-      float* dk = row + off_layer(d, i);
-#pragma unroll
-      for (int kk = 0; kk < 64; ++kk) {
-        const int k = 64 * half + kk;
-        if (k < wp) dk[k * wi + f] = acc[kk];
-      }
-    }
-    // hb_{i-1}[k = f] = sum_{o < wi} zb_i[o] W_i[k][o]
-#pragma unroll
-    for (int pp = 0; pp < PPH; ++pp) hb[pp] = zero8;
+      for (int s = 0; s < S; ++s) hb[j][s] = 0.f;
     if (f < wp) {
-      for (int o = 0; o < wi; ++o) {
-        const float w = sh.W[f][o];
+      for (int o = 0; o < oin; o += 4) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(&sh.W[f][o]);
 #pragma unroll
-        for (int pp = 0; pp < PPH; ++pp)
+        for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-          for (int s = 0; s < HI_MAXS; ++s)
-            if (s < S) hb[pp][s] = fmaf(sh.G[half * PPH + pp][s][o], w, hb[pp][s]);
+          for (int s = 0; s < S; ++s) {
+            const f32x4 g = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][o]);
+            hb[j][s] = fmaf(g[0], w[0], fmaf(g[1], w[1], fmaf(g[2], w[2], fmaf(g[3], w[3], hb[j][s]))));
+          }
       }
     }
-    __syncthreads();  // sh.A / sh.G / sh.W / sh.red reused by the next layer
+    __syncthreads();  // sh.A / sh.W reused by the next layer
+  }
+}
+
+// Weight gradients over the point range of split blockIdx.y (one slab row per split, reduced in
+// a fixed order afterwards): blockIdx.x < n_tiles: dK_i = H_{i-1}^T B_i on a 32 x 32 tile
+// (rows = point x stream, staged 64 at a time through LDS); else layer e = blockIdx.x - n_tiles:
+// bias of hidden layer e, plus K0 (e = 0) and the output layer's Ko, bo (e = n_hidden - 1).
+#define HI_TILE 32
+#define HI_CHUNK 64
+__global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(const float* __restrict__ X, int N, NetDims d, HiSpec sp,
+                                                           const float* __restrict__ dJ, int ldJ, int j0,
+                                                           const float* __restrict__ Hb,
+                                                           const float* __restrict__ Bb, float* __restrict__ slab,
+                                                           int Pst, int n_tiles) {
+  __shared__ __attribute__((aligned(16))) float Hc[HI_CHUNK][HI_TILE];
+  __shared__ __attribute__((aligned(16))) float Gc[HI_CHUNK][HI_TILE];
+  __shared__ float red[2][TDQ_MAXD + TDQ_MAXO + 1][HI_W];
+  const int t = threadIdx.x, S = sp.S, Lh = d.n_hidden, dout = d.d_out;
+  const int ks = gridDim.y, y = blockIdx.y;
+  const int n0 = (int)((long long)N * y / ks), n1 = (int)((long long)N * (y + 1) / ks);
+  float* row = slab + (size_t)y * Pst;
+  constexpr int TPL = (HI_W / HI_TILE) * (HI_W / HI_TILE);
+  if ((int)blockIdx.x < n_tiles) {
+    const int i = 1 + blockIdx.x / TPL, tile = blockIdx.x % TPL;
+    const int kt = tile / (HI_W / HI_TILE), ft = tile % (HI_W / HI_TILE);
+    const int win = hw(d, i - 1), wout = hw(d, i);
+    if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
+    const int tk = t >> 4, tf = t & 15;
+    float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    const int r0 = n0 * S, r1 = n1 * S;
+    const float* Hl = Hb + hi_row(i - 1, 0, 0, S, N) + kt * HI_TILE;
+    const float* Bl = Bb + hi_row(i, 0, 0, S, N) + ft * HI_TILE;
+    for (int r = r0; r < r1; r += HI_CHUNK) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // 64 rows x 32 columns = 512 float4 per operand
+        const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
+        f32x4 hv = {0.f, 0.f, 0.f, 0.f}, gv = {0.f, 0.f, 0.f, 0.f};
+        if (r + rr < r1) {
+          hv = *reinterpret_cast<const f32x4*>(Hl + (size_t)(r + rr) * HI_W + c);
+          gv = *reinterpret_cast<const f32x4*>(Bl + (size_t)(r + rr) * HI_W + c);
+        }
+        *reinterpret_cast<f32x4*>(&Hc[rr][c]) = hv;
+        *reinterpret_cast<f32x4*>(&Gc[rr][c]) = gv;
+      }
+      __syncthreads();
+#pragma unroll 8
+      for (int rr = 0; rr < HI_CHUNK; ++rr) {
+        const float2 hv = *reinterpret_cast<const float2*>(&Hc[rr][2 * tk]);
+        const float2 gv = *reinterpret_cast<const float2*>(&Gc[rr][2 * tf]);
+        acc[0][0] = fmaf(hv.x, gv.x, acc[0][0]);
+        acc[0][1] = fmaf(hv.x, gv.y, acc[0][1]);
+        acc[1][0] = fmaf(hv.y, gv.x, acc[1][0]);
+        acc[1][1] = fmaf(hv.y, gv.y, acc[1][1]);
+      }
+      __syncthreads();
+    }
+    float* dk = row + off_layer(d, i);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int k = kt * HI_TILE + 2 * tk + a, f = ft * HI_TILE + 2 * tf + b;
+        if (k < win && f < wout) dk[k * wout + f] = acc[a][b];
+      }
+    return;
+  }
+  // ---- per-layer vectors: thread (f, half); the halves split the point range -----------------
+  const int e = blockIdx.x - n_tiles, f = t & (HI_W - 1), half = t >> 7;
+  const int we = hw(d, e);
+  const int nm = (n0 + n1) / 2, na = half ? nm : n0, nb = half ? n1 : nm;
+  const bool first = e == 0, last = e == Lh - 1;
+  const int nv = 1 + (first ? d.d_in : 0) + (last ? dout : 0);
+  float acc[TDQ_MAXD + TDQ_MAXO + 1];
+#pragma unroll
+  for (int v = 0; v < TDQ_MAXD + TDQ_MAXO + 1; ++v) acc[v] = 0.f;
+  if (f < we) {
+    for (int m = na; m < nb; ++m) {
+      const float zb0 = Bb[hi_row(e, m, 0, S, N) + f];
+      acc[0] += zb0;
+      if (first) {
+        for (int v = 0; v < d.d_in; ++v) acc[1 + v] = fmaf(X[(size_t)m * d.d_in + v], zb0, acc[1 + v]);
+        for (int s = 1; s < S; ++s)
+          if (sp.order[s] == 1) acc[1 + sp.var[s]] += Bb[hi_row(e, m, s, S, N) + f];
+      }
+      if (last) {
+        const int o = 1 + (first ? d.d_in : 0);
+        for (int s = 0; s < S; ++s) {
+          const int orow = sp.out[s];
+          if (orow < 0) continue;
+          const float h = Hb[hi_row(e, m, s, S, N) + f];
+          for (int q = 0; q < dout; ++q) acc[o + q] = fmaf(h, dJ[((size_t)orow * ldJ + j0 + m) * dout + q], acc[o + q]);
+        }
+      }
+    }
+  }
+  for (int v = 0; v < nv; ++v) red[half][v][f] = acc[v];
+  __syncthreads();
+  if (half == 0 && f < we) {
+    const int pin = e == 0 ? d.d_in : hw(d, e - 1);
+    row[off_layer(d, e) + pin * we + f] = red[0][0][f] + red[1][0][f];  // bias of hidden layer e
+    if (first)
+      for (int v = 0; v < d.d_in; ++v) row[v * we + f] = red[0][1 + v][f] + red[1][1 + v][f];
+    if (last) {
+      const int o = 1 + (first ? d.d_in : 0);
+      for (int q = 0; q < dout; ++q) row[off_layer(d, Lh) + f * dout + q] = red[0][o + q][f] + red[1][o + q][f];
+    }
+  }
+  if (last && t < dout) {
+    float a = 0.f;
+    if (sp.out[0] >= 0)
+      for (int m = n0; m < n1; ++m) a += dJ[((size_t)sp.out[0] * ldJ + j0 + m) * dout + t];
+    row[off_layer(d, Lh) + hw(d, Lh - 1) * dout + t] = a;
   }
 }
 
@@ -410,14 +515,9 @@ __global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restr
                                                             float* __restrict__ grad) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= Ptot) return;
-  float a0 = 0.f, a1 = 0.f;
-  int r = 0;
-  for (; r + 1 < nrows; r += 2) {
-    a0 += slab[(size_t)r * Pst + e];
-    a1 += slab[(size_t)(r + 1) * Pst + e];
-  }
-  if (r < nrows) a0 += slab[(size_t)r * Pst + e];
-  grad[e] = a0 + a1;
+  float a = 0.f;
+  for (int r = 0; r < nrows; ++r) a += slab[(size_t)r * Pst + e];
+  grad[e] = a;
 }
 
 namespace {
@@ -456,6 +556,14 @@ bool hi_spec(HiSpec& sp, const int* si, const float* sc) {
       sp.tb[k][b] = v;
     }
   }
+  // the univariate chain (), (v), (v, v), ...: stream k of order k, one variable, in order
+  sp.chain = S >= 2 && S <= 5;
+  for (int s = 1; s < S; ++s) sp.chain = sp.chain && sp.order[s] == s;
+  if (sp.chain) {
+    // every stream's factors are lower streams of the same chain: check via the order-1 variable
+    for (int k = 0; k < nt; ++k)
+      for (int b = 0; b < tt[7 * k + 2]; ++b) sp.chain = sp.chain && sp.order[tt[7 * k + 3 + b]] >= 1;
+  }
   return true;
 }
 
@@ -464,45 +572,101 @@ bool hi_dims(NetDims& d, int d_in, const int* widths, int d_out, int n_hidden) {
   return d.width <= HI_W && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO;
 }
 
+template <typename K>
+void hi_attr(K* kern) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(HiShared));
+}
+
+int hi_splits(int N) { return std::min(HI_KS, std::max(1, (N + 63) / 64)); }
+
+template <int S, bool CH>
+int hi_launch_fwd(const float* X, int N, const float* P, const NetDims& d, const HiSpec& sp, float* J, int ldJ, int j0,
+                  float* Zb, float* Hb, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hi_attr(&jet_hi_fwd_kernel<S, CH>);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_hi_fwd_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS), sizeof(HiShared), st,
+                     X, N, P, d, sp, J, ldJ, j0, Zb, Hb);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int S, bool CH>
+int hi_launch_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const float* dJ, int ldJ, int j0,
+                    const float* Zb, float* Bb, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hi_attr(&jet_hi_chain_kernel<S, CH>);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_hi_chain_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS), sizeof(HiShared),
+                     st, N, P, d, sp, dJ, ldJ, j0, Zb, Bb);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// (S, chain) -> instantiation
+#define HI_CASES(X)                                                                                           \
+  X(2, true) X(3, true) X(4, true) X(5, true) X(2, false) X(3, false) X(4, false) X(5, false) X(6, false) \
+      X(7, false) X(8, false)
+
+int hi_fwd(const float* X, int N, const float* P, const NetDims& d, const HiSpec& sp, float* J, int ldJ, int j0,
+           float* Zb, float* Hb, hipStream_t st) {
+  const bool ch = sp.chain != 0;
+#define HI_F(SS, CC) \
+  if (sp.S == SS && ch == CC) return hi_launch_fwd<SS, CC>(X, N, P, d, sp, J, ldJ, j0, Zb, Hb, st);
+  HI_CASES(HI_F)
+#undef HI_F
+  return (int)hipErrorInvalidValue;
+}
+
+int hi_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const float* dJ, int ldJ, int j0,
+             const float* Zb, float* Bb, hipStream_t st) {
+  const bool ch = sp.chain != 0;
+#define HI_B(SS, CC) \
+  if (sp.S == SS && ch == CC) return hi_launch_chain<SS, CC>(N, P, d, sp, dJ, ldJ, j0, Zb, Bb, st);
+  HI_CASES(HI_B)
+#undef HI_B
+  return (int)hipErrorInvalidValue;
+}
+
+// one activation-sized scratch buffer (Z, H or B), in floats
+size_t hi_act_floats(int N, int n_hidden) { return (size_t)n_hidden * N * HI_MAXS * HI_W; }
+
 }  // namespace
 
 extern "C" {
 
-int64_t tdq_jet_hi_scratch_floats(int N, int n_hidden) { return (int64_t)n_hidden * N * HI_MAXS * HI_W; }
+// Z | H | B: pre-activations, post-activations and pre-activation adjoints of every hidden layer
+int64_t tdq_jet_hi_scratch_floats(int N, int n_hidden) { return 3 * (int64_t)hi_act_floats(N, n_hidden); }
 
-// slab rows + the reduced gradient, in floats
+// slab rows of the weight-gradient pass, in floats
 int64_t tdq_jet_hi_work_floats(int N, int d_in, const int* widths, int d_out, int n_hidden) {
   NetDims d;
   if (!hi_dims(d, d_in, widths, d_out, n_hidden)) return -1;
-  const int nwg = (N + HI_NP - 1) / HI_NP;
-  return (int64_t)nwg * slab_stride(param_count(d));
+  return (int64_t)hi_splits(N) * slab_stride(param_count(d));
 }
 
 // forward over N points X[N][d_in]: stream s with out[s] >= 0 -> J[(out[s] * ldJ + j0 + n) * d_out + q];
-// pre-activations of every hidden layer -> Z (tdq_jet_hi_scratch_floats)
+// hidden-layer activations -> Z (tdq_jet_hi_scratch_floats)
 int tdq_jet_hi_fwd(const float* X, int N, const float* P, int d_in, const int* widths, int d_out, int n_hidden,
                    const int* spec_i, const float* spec_c, float* J, int ldJ, int j0, float* Z, void* stream) {
   if (N <= 0) return 0;
   NetDims d;
   HiSpec sp;
   if (!hi_dims(d, d_in, widths, d_out, n_hidden) || !hi_spec(sp, spec_i, spec_c)) return (int)hipErrorInvalidValue;
-  const size_t lds = sizeof(HiShared);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_hi_fwd_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  hipLaunchKernelGGL(jet_hi_fwd_kernel, dim3((N + HI_NP - 1) / HI_NP), dim3(256), lds,
-                     reinterpret_cast<hipStream_t>(stream), X, N, P, d, sp, J, ldJ, j0, Z);
-  TDQ_CHECK_LAUNCH();
-  return 0;
+  const size_t A = hi_act_floats(N, n_hidden);
+  return hi_fwd(X, N, P, d, sp, J, ldJ, j0, Z, Z + A, reinterpret_cast<hipStream_t>(stream));
 }
 
 // backward: the adjoints dJ of the streams with out[s] >= 0 -> the flat parameter gradient `grad`
-// (slab rows in `work`, reduced in a fixed order)
+// (adjoint chain per point group, then the weight gradients over point splits into slab rows in
+// `work`, reduced in a fixed order: deterministic)
 int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* widths, int d_out, int n_hidden,
-                   const int* spec_i, const float* spec_c, const float* dJ, int ldJ, int j0, const float* Z,
+                   const int* spec_i, const float* spec_c, const float* dJ, int ldJ, int j0, float* Z,
                    float* work, float* grad, void* stream) {
   NetDims d;
   HiSpec sp;
@@ -510,17 +674,15 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d), Pst = slab_stride(Ptot);
   if (N <= 0) return (int)hipMemsetAsync(grad, 0, sizeof(float) * Ptot, st);
-  const int nwg = (N + HI_NP - 1) / HI_NP;
-  const size_t lds = sizeof(HiShared);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_hi_bwd_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  hipLaunchKernelGGL(jet_hi_bwd_kernel, dim3(nwg), dim3(256), lds, st, X, N, P, d, sp, dJ, ldJ, j0, Z, work, Pst);
+  const size_t A = hi_act_floats(N, n_hidden);
+  int rc = hi_chain(N, P, d, sp, dJ, ldJ, j0, Z, Z + 2 * A, st);
+  if (rc) return rc;
+  const int ks = hi_splits(N);
+  const int n_tiles = (n_hidden - 1) * (HI_W / HI_TILE) * (HI_W / HI_TILE);
+  hipLaunchKernelGGL(jet_hi_wgrad_kernel, dim3(n_tiles + n_hidden, ks), dim3(256), 0, st, X, N, d, sp, dJ, ldJ, j0,
+                     Z + A, Z + 2 * A, work, Pst, n_tiles);
   TDQ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((Ptot + 255) / 256), dim3(256), 0, st, work, nwg, Pst, Ptot, grad);
+  hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((Ptot + 255) / 256), dim3(256), 0, st, work, ks, Pst, Ptot, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

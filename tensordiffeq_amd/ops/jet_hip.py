@@ -178,19 +178,6 @@ def backward_range(saved, dJ, work, lo, hi):
     _lib.check(rc, "tdq_jet_bwd_bf3_range")
 
 
-def set_bwd_recompute(on):
-    """Select the recompute backward (csrc/jet_bwdr.h: the forward re-run on chip instead of saved
-    activations) for the geometries it serves; switch only between steps / engines."""
-    _lib.check(_lib.load().tdq_bwdr_set(int(bool(on))), "tdq_bwdr_set")
-
-
-def bwd_recompute_active(cfg):
-    """Whether the recompute backward serves this configuration (precision bf16, instantiated geometry)."""
-    if not is_split_bf16(cfg):
-        return False
-    return bool(_lib.load().tdq_bwdr_active(cfg["d_in"], _warg(cfg), cfg["n_hidden"], cfg["S"], *_lo_args(cfg)))
-
-
 def is_split_bf16(cfg):
     """The fused split-bf16 kernels (csrc/jet_bf3.h) serve this configuration."""
     return cfg["precision"] in ("bf16x3", "bf16") and not is_layered(cfg)

@@ -80,6 +80,21 @@ def test_hi_kernels_match_fp64_jet(sizes, reqs, n):
     # deterministic: a second backward gives the same bits
     g2 = op.backward(dJ, net.flat)
     assert torch.equal(g, g2)
+    # isolated kernel time (the AC-baseline periodic-BC set: 402 points, order 4)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for _ in range(5):
+        op.forward(J, net.flat)
+        op.backward(dJ, net.flat)
+    ev[0].record()
+    for _ in range(50):
+        op.forward(J, net.flat)
+    ev[1].record()
+    for _ in range(50):
+        op.backward(dJ, net.flat)
+    ev[2].record()
+    torch.cuda.synchronize()
+    print(f"HI time {sizes} n={n}: fwd {ev[0].elapsed_time(ev[1]) * 20:.1f} us, "
+          f"bwd {ev[1].elapsed_time(ev[2]) * 20:.1f} us")
 
 
 @pytest.mark.gpu
