@@ -17,27 +17,33 @@
 // The host passes the partition table (term = tanh order k, coefficient, up to 4 factor streams);
 // the backward differentiates each term by product rule, and through tanh^(k)(z) with
 // d/dz tanh^(k) = tanh^(k+1).  The forward saves every hidden layer's PRE-activation streams z
-// (fp32, [layer][point][stream][feature]) - order >= 3 adjoints need z itself, not only h.
+// and post-activation streams h (fp32, [layer][point x stream][feature]); order >= 3 adjoints need
+// z itself, the weight gradients need h.
 //
-// Layout: one workgroup = 1024 threads = 8 points; thread t owns feature f = t & 127 of point
-// p = t >> 7 (GEMM rows = the point's S streams); a layer's weights are staged in LDS (row stride
-// 129 floats: the forward reads W[k][f] along f, the backward W[k][f] along k, both conflict-free),
-// activations / adjoints of the workgroup's points live in LDS for the GEMMs.  dK partials of a
-// workgroup are one slab row (flat Keras order); tdq_jet_hi_bwd reduces the rows in a fixed order
-// (deterministic) into its own gradient vector, which the fused step tail adds to theta's.
-// The stream count is a template parameter, and the common plan - the univariate chain
-// u, u_v, u_vv, u_vvv(, u_vvvv) of the reference's periodic BCs - has its tanh jet and adjoint as
-// straight-line code; other plans interpret the partition table (uniform kernel-argument reads).
-// First build (256 threads, 4 points, interpreted jets, table in LDS): 0.31 + 0.40 ms per AC-baseline
-// step (profiles/r4b_kernel_stats_ac_baseline_slow_hi.txt).
+// Kernels (a few hundred points: latency, not bandwidth, is the budget):
+//   * forward: workgroup = 512 threads = 4 points, thread (f, g) owns feature f of point g; one
+//     layer's weights in LDS (row stride 132: W[k][f] along f and float4 rows W[f][o..o+3] are
+//     conflict-free), the points' activations in LDS as GEMM operand (float4 broadcasts); the next
+//     layer's weights load into registers during this layer's GEMM.
+//   * adjoint chain (same layout): zb_i = tanh-jet adjoint of hb_i, hb_{i-1} = W_i zb_i -> B.
+//   * weight gradients: dK_i = H_{i-1}^T B_i as 32 x 32 tiles over point splits (one slab row per
+//     split), per-layer vectors (biases, K0, Ko, bo) in a second kernel; a fixed-order sum of the
+//     split rows gives the gradient (deterministic), which the fused step tail adds to theta's.
+// Waves of a workgroup share data through LDS only: barriers are lds_sync() (no global-memory
+// wait), and loads are unconditional from clamped addresses (a conditional load is a branch with
+// a wait behind it).  The stream count is a template parameter, and the common plan - the
+// univariate chain u, u_v, u_vv, u_vvv(, u_vvvv) of the reference's periodic BCs - has its tanh jet
+// and adjoint as straight-line code; other plans interpret the partition table.
+// History (AC-baseline, 402 points, order 4; profiles/): interpreted 256-thread first build
+// 0.31 + 0.40 ms per step; this layout 31 + 63 us isolated before lds_sync.
 #include "jet_common.h"
 
 #define HI_MAXS 8
 #define HI_MAXT 48
 #define HI_MAXB 4
 #define HI_W 128
-#define HI_TG 2                      // 128-thread groups per workgroup (one feature per thread)
-#define HI_PT 2                      // points per thread
+#define HI_TG 4                      // 128-thread groups per workgroup (one feature per thread)
+#define HI_PT 1                      // points per thread
 #define HI_NP (HI_TG * HI_PT)        // points per workgroup
 #define HI_THREADS (HI_W * HI_TG)
 #define HI_WS (HI_W + 4)             // LDS row strides (float4 rows, conflict-free)
@@ -207,13 +213,76 @@ struct HiShared {
   float A[HI_NP][HI_MAXS][HI_AS];
 };
 
-// W (in x out) of dense layer `layer` into LDS, zero-padded to HI_W columns and to a multiple of 4 rows
-__device__ __forceinline__ void hi_stage_w(HiShared& sh, const float* __restrict__ P, const NetDims& d, int layer) {
+// Diagnostic build only (tools/hi_stamps.cpp, -DHI_STAMPS): s_memtime at phase boundaries of
+// workgroup 0, printed at the end; compiled out otherwise.
+#ifdef HI_STAMPS
+#define HI_TS_DECL long long hi_ts[24]; int hi_nts = 0;
+#define HI_TS() \
+  if (hi_nts < 24) hi_ts[hi_nts++] = __builtin_amdgcn_s_memtime();
+#define HI_TS_PRINT(name)                                                       \
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                 \
+    printf("%s", name);                                                         \
+    for (int q = 1; q < hi_nts; ++q) printf(" %lld", hi_ts[q] - hi_ts[q - 1]); \
+    printf(" | total %lld\n", hi_ts[hi_nts - 1] - hi_ts[0]);                   \
+  }
+#else
+#define HI_TS_DECL
+#define HI_TS()
+#define HI_TS_PRINT(name)
+#endif
+
+// Loads in these kernels are unconditional, from clamped (valid) addresses, and masked after the
+// fact: a `cond ? load : 0` compiles to a branch around the load with a wait behind it, which
+// serialises a whole batch of loads into one memory latency each.
+__device__ __forceinline__ float ldm(const float* p, bool keep) {
+  const float v = *p;
+  return keep ? v : 0.f;
+}
+
+// W (in x out) of dense layer `layer`, zero-padded to HI_W x HI_W, as float4 pieces in registers:
+// piece u of thread t = row (t + 256 u) >> 5, columns 4 ((t + 256 u) & 31) + [0, 4).  All loads of a
+// layer are issued back to back (one memory latency per layer, not one per element) and overlap
+// the previous layer's GEMM; hi_put_w writes them to LDS after that GEMM's barrier.
+constexpr int HI_WQ = HI_W * HI_W / 4 / HI_THREADS;
+struct HiWRegs {
+  f32x4 q[HI_WQ];
+};
+__device__ __forceinline__ void hi_get_w(HiWRegs& r, const float* __restrict__ P, const NetDims& d, int layer) {
   const float* K = P + off_layer(d, layer);
-  const int win = hw(d, layer - 1), wout = hw(d, layer), rows = (win + 3) & ~3;
-  for (int e = threadIdx.x; e < rows * HI_W; e += blockDim.x) {
-    const int k = e >> 7, f = e & (HI_W - 1);
-    sh.W[k][f] = (k < win && f < wout) ? K[k * wout + f] : 0.f;
+  const int win = hw(d, layer - 1), wout = hw(d, layer);
+  // one uniform branch around each whole batch (a branch per piece makes the compiler wait for
+  // every load at the join)
+  if (((off_layer(d, layer) | wout) & 3) == 0) {
+#pragma unroll
+    for (int u = 0; u < HI_WQ; ++u) {
+      const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
+      const int kc = k < win ? k : win - 1, cc = c < wout ? c : wout - 4;
+      r.q[u] = *reinterpret_cast<const f32x4*>(K + kc * wout + cc);
+    }
+#pragma unroll
+    for (int u = 0; u < HI_WQ; ++u) {
+      const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) r.q[u][x] = (k < win && c < wout) ? r.q[u][x] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < HI_WQ; ++u) {
+      const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
+      const int kc = k < win ? k : win - 1;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int cx = c + x < wout ? c + x : wout - 1;
+        r.q[u][x] = ldm(K + kc * wout + cx, k < win && c + x < wout);
+      }
+    }
+  }
+}
+__device__ __forceinline__ void hi_put_w(HiShared& sh, const HiWRegs& r) {
+#pragma unroll
+  for (int u = 0; u < HI_WQ; ++u) {
+    const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
+    *reinterpret_cast<f32x4*>(&sh.W[k][c]) = r.q[u];
   }
 }
 
@@ -224,13 +293,16 @@ __device__ __forceinline__ size_t hi_row(int layer, int n, int s, int S, int N) 
 }
 
 // thread (f, pg): feature f of points 2 pg, 2 pg + 1 of the workgroup's HI_NP
+// one workgroup per CU (the LDS), two waves per SIMD (full VALU issue rate, 256 registers each)
 template <int S, bool CH>
-__global__ void __launch_bounds__(HI_THREADS) jet_hi_fwd_kernel(const float* __restrict__ X, int N,
+__global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) jet_hi_fwd_kernel(const float* __restrict__ X, int N,
                                                                 const float* __restrict__ P, NetDims d, HiSpec sp,
                                                                 float* __restrict__ J, int ldJ, int j0,
                                                                 float* __restrict__ Zb, float* __restrict__ Hb) {
   extern __shared__ __attribute__((aligned(16))) char hi_lds[];
   HiShared& sh = *reinterpret_cast<HiShared*>(hi_lds);
+  HI_TS_DECL
+  HI_TS()
   const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
   const int Lh = d.n_hidden;
   int n[HI_PT];
@@ -241,6 +313,8 @@ __global__ void __launch_bounds__(HI_THREADS) jet_hi_fwd_kernel(const float* __r
     ok[j] = m < N;
     n[j] = ok[j] ? m : N - 1;
   }
+  HiWRegs wr;
+  if (Lh > 1) hi_get_w(wr, P, d, 1);
   float z[HI_PT][S];
   {  // layer 0: z = x K0 + b0 (value), K0[var] (first order), 0 (higher)
     const int w0 = hw(d, 0);
@@ -248,44 +322,77 @@ __global__ void __launch_bounds__(HI_THREADS) jet_hi_fwd_kernel(const float* __r
     for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
       for (int s = 0; s < S; ++s) z[j][s] = 0.f;
-    if (f < w0) {
+    {
+      const int fc = f < w0 ? f : w0 - 1;
+      float xv[HI_PT][TDQ_MAXD], kv[TDQ_MAXD];
+#pragma unroll
+      for (int v = 0; v < TDQ_MAXD; ++v) {
+        const int vc = v < d.d_in ? v : d.d_in - 1;
+        kv[v] = ldm(P + vc * w0 + fc, v < d.d_in && f < w0);
+#pragma unroll
+        for (int j = 0; j < HI_PT; ++j) xv[j][v] = ldm(X + (size_t)n[j] * d.d_in + vc, v < d.d_in);
+      }
+      const float b0 = ldm(P + d.d_in * w0 + fc, f < w0);
 #pragma unroll
       for (int j = 0; j < HI_PT; ++j) {
-        float a = P[d.d_in * w0 + f];
-        for (int v = 0; v < d.d_in; ++v) a = fmaf(X[(size_t)n[j] * d.d_in + v], P[v * w0 + f], a);
+        float a = b0;
+#pragma unroll
+        for (int v = 0; v < TDQ_MAXD; ++v) a = fmaf(xv[j][v], kv[v], a);
         z[j][0] = a;
 #pragma unroll
-        for (int s = 1; s < S; ++s)
-          if (sp.order[s] == 1) z[j][s] = P[sp.var[s] * w0 + f];
+        for (int s = 1; s < S; ++s) {
+          float k1 = 0.f;
+#pragma unroll
+          for (int v = 0; v < TDQ_MAXD; ++v) k1 = sp.var[s] == v ? kv[v] : k1;
+          if (sp.order[s] == 1) z[j][s] = k1;
+        }
       }
     }
   }
-  if (Lh > 1) hi_stage_w(sh, P, d, 1);
+  if (Lh > 1) hi_put_w(sh, wr);
+  HI_TS()
   for (int i = 0; i < Lh; ++i) {
     const int wi = hw(d, i);
-    if (i >= 1) {  // z_i = h_{i-1} W_i (+ b_i): h_{i-1} in sh.A, W_i staged in sh.W
-      const int kin = (hw(d, i - 1) + 3) & ~3;
+    if (i >= 1) {  // z_i = h_{i-1} W_i (+ b_i): h_{i-1} in sh.A, W_i in sh.W; W_{i+1} loads in flight
+      if (i + 1 < Lh) hi_get_w(wr, P, d, i + 1);
+      const float b = ldm(P + off_layer(d, i) + hw(d, i - 1) * wi + (f < wi ? f : wi - 1), f < wi);
 #pragma unroll
       for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
         for (int s = 0; s < S; ++s) z[j][s] = 0.f;
-      for (int k = 0; k < kin; k += 4) {
-        const float w0 = sh.W[k][f], w1 = sh.W[k + 1][f], w2 = sh.W[k + 2][f], w3 = sh.W[k + 3][f];
+      // software-pipelined over groups of 4 k: the LDS reads of group k + 4 are in flight while
+      // group k's FMAs run (the scheduler alone reuses one register quad and waits after every read)
+      const int kin8 = (hw(d, i - 1) + 7) & ~7;  // sh.A / sh.W are zero past the layer's width
+      f32x4 a0[HI_PT][S], a1[HI_PT][S];
+      float w0[4], w1[4];
+      auto lda = [&](int k, f32x4(&a)[HI_PT][S], float(&w)[4]) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) w[x] = sh.W[k + x][f];
 #pragma unroll
         for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const f32x4 a = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][k]);
-            z[j][s] = fmaf(a[0], w0, fmaf(a[1], w1, fmaf(a[2], w2, fmaf(a[3], w3, z[j][s]))));
-          }
-      }
-      if (f < wi) {
-        const float b = P[off_layer(d, i) + hw(d, i - 1) * wi + f];
+          for (int s = 0; s < S; ++s) a[j][s] = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][k]);
+      };
+      auto fma4 = [&](const f32x4(&a)[HI_PT][S], const float(&w)[4]) {
 #pragma unroll
-        for (int j = 0; j < HI_PT; ++j) z[j][0] += b;
+        for (int j = 0; j < HI_PT; ++j)
+#pragma unroll
+          for (int s = 0; s < S; ++s)
+            z[j][s] = fmaf(a[j][s][0], w[0], fmaf(a[j][s][1], w[1], fmaf(a[j][s][2], w[2], fmaf(a[j][s][3], w[3], z[j][s]))));
+      };
+      lda(0, a0, w0);
+      for (int k = 0; k < kin8; k += 8) {
+        lda(k + 4, a1, w1);
+        fma4(a0, w0);
+        if (k + 8 < kin8) lda(k + 8, a0, w0);
+        fma4(a1, w1);
       }
-      __syncthreads();  // every thread done reading sh.A / sh.W
-      if (i + 1 < Lh) hi_stage_w(sh, P, d, i + 1);
+#pragma unroll
+      for (int j = 0; j < HI_PT; ++j) z[j][0] += b;
+      HI_TS()
+      lds_sync();  // every thread done reading sh.A / sh.W
+      if (i + 1 < Lh) hi_put_w(sh, wr);
+      HI_TS()
     }
 #pragma unroll
     for (int j = 0; j < HI_PT; ++j) {
@@ -306,25 +413,49 @@ __global__ void __launch_bounds__(HI_THREADS) jet_hi_fwd_kernel(const float* __r
 #pragma unroll
       for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = h[s];
     }
-    __syncthreads();
+    HI_TS()
+    lds_sync();
+    HI_TS()
   }
-  // ---- output layer: u_s[q] = sum_f h_s[f] Ko[f][q] (+ bo[q] on the value stream) -----------
+  // ---- output layer: u_s[q] = sum_f h_s[f] Ko[f][q] (+ bo[q] on the value stream): per-feature
+  // products into LDS (the free weight area), then one thread per (point, stream, q) sums them
   const int wl = hw(d, Lh - 1), dout = d.d_out;
   const float* Ko = P + off_layer(d, Lh);
+  float* part = &sh.W[0][0];  // [p][s][q][HI_W]
+  {
+    float ko[TDQ_MAXO];
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q)
+      ko[q] = ldm(Ko + (f < wl ? f : wl - 1) * dout + (q < dout ? q : dout - 1), q < dout && f < wl);
+#pragma unroll
+    for (int j = 0; j < HI_PT; ++j)
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q)
+          if (q < dout) part[(((pg * HI_PT + j) * S + s) * TDQ_MAXO + q) * HI_W + f] = sh.A[pg * HI_PT + j][s][f] * ko[q];
+  }
+  lds_sync();
   for (int c = t; c < HI_NP * S * dout; c += blockDim.x) {
     const int q = c % dout, s = (c / dout) % S, pp = c / (dout * S);
     const int m = blockIdx.x * HI_NP + pp;
     if (m >= N || sp.out[s] < 0) continue;
-    float a = s == 0 ? Ko[wl * dout + q] : 0.f;
-    for (int k = 0; k < wl; ++k) a = fmaf(sh.A[pp][s][k], Ko[k * dout + q], a);
+    const f32x4* r = reinterpret_cast<const f32x4*>(part + ((pp * S + s) * TDQ_MAXO + q) * HI_W);
+    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int k = 0; k < HI_W / 4; ++k) a4 += r[k];
+    float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    if (s == 0) a += Ko[wl * dout + q];
     J[((size_t)sp.out[s] * ldJ + j0 + m) * dout + q] = a;
   }
+  HI_TS()
+  HI_TS_PRINT("fwd")
 }
 
 // adjoint chain: hb of the last hidden layer from dJ, then zb_i = tanh-jet adjoint, hb_{i-1} = W_i zb_i;
 // zb_i -> Bb (the weight gradients are jet_hi_wgrad_kernel's)
 template <int S, bool CH>
-__global__ void __launch_bounds__(HI_THREADS) jet_hi_chain_kernel(int N, const float* __restrict__ P, NetDims d,
+__global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) jet_hi_chain_kernel(int N, const float* __restrict__ P, NetDims d,
                                                                   HiSpec sp, const float* __restrict__ dJ, int ldJ,
                                                                   int j0, const float* __restrict__ Zb,
                                                                   float* __restrict__ Bb) {
@@ -340,28 +471,36 @@ __global__ void __launch_bounds__(HI_THREADS) jet_hi_chain_kernel(int N, const f
     ok[j] = m < N;
     n[j] = ok[j] ? m : N - 1;
   }
+  HiWRegs wr;
+  if (Lh > 1) hi_get_w(wr, P, d, Lh - 1);
   const int wl = hw(d, Lh - 1);
   const float* Ko = P + off_layer(d, Lh);
-  float hb[HI_PT][S];
+  float hb[HI_PT][S], z[HI_PT][S];
+  {
+    float ko[TDQ_MAXO];
 #pragma unroll
-  for (int j = 0; j < HI_PT; ++j)
+    for (int q = 0; q < TDQ_MAXO; ++q)
+      ko[q] = ldm(Ko + (f < wl ? f : wl - 1) * dout + (q < dout ? q : dout - 1), q < dout && f < wl);
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      float a = 0.f;
-      const int orow = sp.out[s];
-      if (f < wl && orow >= 0 && ok[j])
-        for (int q = 0; q < dout; ++q) a = fmaf(Ko[f * dout + q], dJ[((size_t)orow * ldJ + j0 + n[j]) * dout + q], a);
-      hb[j][s] = a;
-    }
+    for (int j = 0; j < HI_PT; ++j)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q)
+          a = fmaf(ko[q], ldm(dJ + ((size_t)orow * ldJ + j0 + n[j]) * dout + (q < dout ? q : 0), sp.out[s] >= 0 && ok[j]), a);
+        hb[j][s] = a;
+        z[j][s] = ldm(Zb + hi_row(Lh - 1, n[j], s, S, N) + f, f < wl);
+      }
+  }
   for (int i = Lh - 1; i >= 0; --i) {
     const int wi = hw(d, i);
 #pragma unroll
     for (int j = 0; j < HI_PT; ++j) {
-      float z[S], zb[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s) z[s] = f < wi ? Zb[hi_row(i, n[j], s, S, N) + f] : 0.f;
+      float zb[S];
       if (f < wi) {
-        hi_tanh_b<S, CH>(sp, z, hb[j], zb);
+        hi_tanh_b<S, CH>(sp, z[j], hb[j], zb);
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) zb[s] = 0.f;
@@ -374,51 +513,65 @@ __global__ void __launch_bounds__(HI_THREADS) jet_hi_chain_kernel(int N, const f
       for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = zb[s];
     }
     if (i == 0) break;
-    // hb_{i-1}[k = f] = sum_o zb_i[o] W_i[f][o]
-    hi_stage_w(sh, P, d, i);
-    __syncthreads();
-    const int wp = hw(d, i - 1), oin = (wi + 3) & ~3;
+    // hb_{i-1}[k = f] = sum_o zb_i[o] W_i[f][o]; the next layer's pre-activations load meanwhile
+    hi_put_w(sh, wr);
+    lds_sync();
+    if (i >= 2) hi_get_w(wr, P, d, i - 1);
+    const int wp = hw(d, i - 1);
 #pragma unroll
     for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-      for (int s = 0; s < S; ++s) hb[j][s] = 0.f;
-    if (f < wp) {
-      for (int o = 0; o < oin; o += 4) {
-        const f32x4 w = *reinterpret_cast<const f32x4*>(&sh.W[f][o]);
+      for (int s = 0; s < S; ++s) {
+        hb[j][s] = 0.f;
+        z[j][s] = ldm(Zb + hi_row(i - 1, n[j], s, S, N) + f, f < wp);
+      }
+    if (f < wp) {  // software-pipelined like the forward's GEMM
+      const int oin8 = (wi + 7) & ~7;
+      f32x4 g0[HI_PT][S], g1[HI_PT][S], w0, w1;
+      auto ldg = [&](int o, f32x4(&g)[HI_PT][S], f32x4& w) {
+        w = *reinterpret_cast<const f32x4*>(&sh.W[f][o]);
 #pragma unroll
         for (int j = 0; j < HI_PT; ++j)
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const f32x4 g = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][o]);
-            hb[j][s] = fmaf(g[0], w[0], fmaf(g[1], w[1], fmaf(g[2], w[2], fmaf(g[3], w[3], hb[j][s]))));
-          }
+          for (int s = 0; s < S; ++s) g[j][s] = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][o]);
+      };
+      auto fma4 = [&](const f32x4(&g)[HI_PT][S], const f32x4& w) {
+#pragma unroll
+        for (int j = 0; j < HI_PT; ++j)
+#pragma unroll
+          for (int s = 0; s < S; ++s)
+            hb[j][s] = fmaf(g[j][s][0], w[0], fmaf(g[j][s][1], w[1], fmaf(g[j][s][2], w[2], fmaf(g[j][s][3], w[3], hb[j][s]))));
+      };
+      ldg(0, g0, w0);
+      for (int o = 0; o < oin8; o += 8) {
+        ldg(o + 4, g1, w1);
+        fma4(g0, w0);
+        if (o + 8 < oin8) ldg(o + 8, g0, w0);
+        fma4(g1, w1);
       }
     }
-    __syncthreads();  // sh.A / sh.W reused by the next layer
+    lds_sync();  // sh.A / sh.W reused by the next layer
   }
 }
 
 // Weight gradients over the point range of split blockIdx.y (one slab row per split, reduced in
-// a fixed order afterwards): blockIdx.x < n_tiles: dK_i = H_{i-1}^T B_i on a 32 x 32 tile
-// (rows = point x stream, staged 64 at a time through LDS); else layer e = blockIdx.x - n_tiles:
-// bias of hidden layer e, plus K0 (e = 0) and the output layer's Ko, bo (e = n_hidden - 1).
+// a fixed order afterwards): dK_i = H_{i-1}^T B_i of the hidden-to-hidden layers on 32 x 32 tiles
+// (rows = point x stream, 64 at a time through LDS, the next 64 loading meanwhile).
 #define HI_TILE 32
 #define HI_CHUNK 64
-__global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(const float* __restrict__ X, int N, NetDims d, HiSpec sp,
-                                                           const float* __restrict__ dJ, int ldJ, int j0,
-                                                           const float* __restrict__ Hb,
+__global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims d, const float* __restrict__ Hb,
                                                            const float* __restrict__ Bb, float* __restrict__ slab,
-                                                           int Pst, int n_tiles) {
+                                                           int Pst) {
   __shared__ __attribute__((aligned(16))) float Hc[HI_CHUNK][HI_TILE];
   __shared__ __attribute__((aligned(16))) float Gc[HI_CHUNK][HI_TILE];
-  __shared__ float red[2][TDQ_MAXD + TDQ_MAXO + 1][HI_W];
-  const int t = threadIdx.x, S = sp.S, Lh = d.n_hidden, dout = d.d_out;
+  const int t = threadIdx.x;
   const int ks = gridDim.y, y = blockIdx.y;
   const int n0 = (int)((long long)N * y / ks), n1 = (int)((long long)N * (y + 1) / ks);
   float* row = slab + (size_t)y * Pst;
   constexpr int TPL = (HI_W / HI_TILE) * (HI_W / HI_TILE);
-  if ((int)blockIdx.x < n_tiles) {
-    const int i = 1 + blockIdx.x / TPL, tile = blockIdx.x % TPL;
+  const int bx = (int)blockIdx.x;
+  {
+    const int i = 1 + bx / TPL, tile = bx % TPL;
     const int kt = tile / (HI_W / HI_TILE), ft = tile % (HI_W / HI_TILE);
     const int win = hw(d, i - 1), wout = hw(d, i);
     if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
@@ -427,29 +580,44 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(const float* __restri
     const int r0 = n0 * S, r1 = n1 * S;
     const float* Hl = Hb + hi_row(i - 1, 0, 0, S, N) + kt * HI_TILE;
     const float* Bl = Bb + hi_row(i, 0, 0, S, N) + ft * HI_TILE;
-    for (int r = r0; r < r1; r += HI_CHUNK) {
+    f32x4 hv[2], gv[2];
+    auto load = [&](int r) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {  // 64 rows x 32 columns = 512 float4 per operand
         const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
-        f32x4 hv = {0.f, 0.f, 0.f, 0.f}, gv = {0.f, 0.f, 0.f, 0.f};
+        hv[u] = gv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (r + rr < r1) {
-          hv = *reinterpret_cast<const f32x4*>(Hl + (size_t)(r + rr) * HI_W + c);
-          gv = *reinterpret_cast<const f32x4*>(Bl + (size_t)(r + rr) * HI_W + c);
+          hv[u] = *reinterpret_cast<const f32x4*>(Hl + (size_t)(r + rr) * HI_W + c);
+          gv[u] = *reinterpret_cast<const f32x4*>(Bl + (size_t)(r + rr) * HI_W + c);
         }
-        *reinterpret_cast<f32x4*>(&Hc[rr][c]) = hv;
-        *reinterpret_cast<f32x4*>(&Gc[rr][c]) = gv;
       }
-      __syncthreads();
-#pragma unroll 8
-      for (int rr = 0; rr < HI_CHUNK; ++rr) {
-        const float2 hv = *reinterpret_cast<const float2*>(&Hc[rr][2 * tk]);
-        const float2 gv = *reinterpret_cast<const float2*>(&Gc[rr][2 * tf]);
-        acc[0][0] = fmaf(hv.x, gv.x, acc[0][0]);
-        acc[0][1] = fmaf(hv.x, gv.y, acc[0][1]);
-        acc[1][0] = fmaf(hv.y, gv.x, acc[1][0]);
-        acc[1][1] = fmaf(hv.y, gv.y, acc[1][1]);
+    };
+    load(r0);
+    for (int r = r0; r < r1; r += HI_CHUNK) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
+        *reinterpret_cast<f32x4*>(&Hc[rr][c]) = hv[u];
+        *reinterpret_cast<f32x4*>(&Gc[rr][c]) = gv[u];
       }
-      __syncthreads();
+      lds_sync();
+      if (r + HI_CHUNK < r1) load(r + HI_CHUNK);
+      for (int rb = 0; rb < HI_CHUNK; rb += 8) {  // 16 LDS reads in flight, then 32 FMAs
+        float2 h2[8], g2[8];
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          h2[rr] = *reinterpret_cast<const float2*>(&Hc[rb + rr][2 * tk]);
+          g2[rr] = *reinterpret_cast<const float2*>(&Gc[rb + rr][2 * tf]);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          acc[0][0] = fmaf(h2[rr].x, g2[rr].x, acc[0][0]);
+          acc[0][1] = fmaf(h2[rr].x, g2[rr].y, acc[0][1]);
+          acc[1][0] = fmaf(h2[rr].y, g2[rr].x, acc[1][0]);
+          acc[1][1] = fmaf(h2[rr].y, g2[rr].y, acc[1][1]);
+        }
+      }
+      lds_sync();
     }
     float* dk = row + off_layer(d, i);
 #pragma unroll
@@ -459,54 +627,124 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(const float* __restri
         const int k = kt * HI_TILE + 2 * tk + a, f = ft * HI_TILE + 2 * tf + b;
         if (k < win && f < wout) dk[k * wout + f] = acc[a][b];
       }
-    return;
   }
-  // ---- per-layer vectors: thread (f, half); the halves split the point range -----------------
-  const int e = blockIdx.x - n_tiles, f = t & (HI_W - 1), half = t >> 7;
-  const int we = hw(d, e);
-  const int nm = (n0 + n1) / 2, na = half ? nm : n0, nb = half ? n1 : nm;
+}
+
+// per-layer vectors of the split blockIdx.y's points, workgroup e = blockIdx.x per hidden layer:
+// bias of hidden layer e, plus K0 (e = 0) and the output layer's Ko, bo (e = n_hidden - 1).
+// Thread (f, g): feature f, point group g of HI_VG; every load unconditional from a clamped
+// address, weighted 0 / 1, so a round of U points is one batch of independent loads.
+#define HI_VG 4
+#define HI_VSLOTS (1 + TDQ_MAXD + 2 * TDQ_MAXO)
+template <int S>
+__global__ void __launch_bounds__(HI_W * HI_VG) jet_hi_wvec_kernel(const float* __restrict__ X, int N, NetDims d,
+                                                                   HiSpec sp, const float* __restrict__ dJ, int ldJ,
+                                                                   int j0, const float* __restrict__ Hb,
+                                                                   const float* __restrict__ Bb,
+                                                                   float* __restrict__ slab, int Pst) {
+  __shared__ float red[HI_VG][HI_VSLOTS][HI_W];
+  const int t = threadIdx.x, Lh = d.n_hidden, dout = d.d_out;
+  const int ks = gridDim.y, y = blockIdx.y;
+  const int n0 = (int)((long long)N * y / ks), n1 = (int)((long long)N * (y + 1) / ks);
+  float* row = slab + (size_t)y * Pst;
+  const int e = blockIdx.x, f = t & (HI_W - 1), g = t >> 7;
+  const int we = hw(d, e), din = d.d_in;
+  const int na = n0 + (int)((long long)(n1 - n0) * g / HI_VG), nb = n0 + (int)((long long)(n1 - n0) * (g + 1) / HI_VG);
   const bool first = e == 0, last = e == Lh - 1;
-  const int nv = 1 + (first ? d.d_in : 0) + (last ? dout : 0);
-  float acc[TDQ_MAXD + TDQ_MAXO + 1];
+  const int fc = f < we ? f : 0;
+  float ab = 0.f, ak[TDQ_MAXD], ao[TDQ_MAXO], abo[TDQ_MAXO];
 #pragma unroll
-  for (int v = 0; v < TDQ_MAXD + TDQ_MAXO + 1; ++v) acc[v] = 0.f;
-  if (f < we) {
-    for (int m = na; m < nb; ++m) {
-      const float zb0 = Bb[hi_row(e, m, 0, S, N) + f];
-      acc[0] += zb0;
-      if (first) {
-        for (int v = 0; v < d.d_in; ++v) acc[1 + v] = fmaf(X[(size_t)m * d.d_in + v], zb0, acc[1 + v]);
-        for (int s = 1; s < S; ++s)
-          if (sp.order[s] == 1) acc[1 + sp.var[s]] += Bb[hi_row(e, m, s, S, N) + f];
+  for (int v = 0; v < TDQ_MAXD; ++v) ak[v] = 0.f;
+#pragma unroll
+  for (int q = 0; q < TDQ_MAXO; ++q) ao[q] = abo[q] = 0.f;
+  constexpr int U = S <= 4 ? 8 : 4;  // points per round (register budget)
+  for (int m0 = na; m0 < nb; m0 += U) {
+    float zb[U][S], w[U];
+    int mc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      w[u] = m0 + u < nb ? 1.f : 0.f;
+      mc[u] = m0 + u < nb ? m0 + u : (na < N ? na : 0);
+    }
+    if (first) {  // uniform branch around a whole batch
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int s = 0; s < S; ++s) zb[u][s] = Bb[hi_row(e, mc[u], s, S, N) + fc];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        zb[u][0] = Bb[hi_row(e, mc[u], 0, S, N) + fc];
+#pragma unroll
+        for (int s = 1; s < S; ++s) zb[u][s] = 0.f;
       }
-      if (last) {
-        const int o = 1 + (first ? d.d_in : 0);
-        for (int s = 0; s < S; ++s) {
-          const int orow = sp.out[s];
-          if (orow < 0) continue;
-          const float h = Hb[hi_row(e, m, s, S, N) + f];
-          for (int q = 0; q < dout; ++q) acc[o + q] = fmaf(h, dJ[((size_t)orow * ldJ + j0 + m) * dout + q], acc[o + q]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) ab = fmaf(w[u], zb[u][0], ab);
+    if (first) {  // K0[v][f]: x_v * zb_value + the first-order streams of variable v
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < TDQ_MAXD; ++v) {
+          float gv = ldm(X + (size_t)mc[u] * din + (v < din ? v : din - 1), v < din) * zb[u][0];
+#pragma unroll
+          for (int s = 1; s < S; ++s) gv += (sp.order[s] == 1 && sp.var[s] == v) ? zb[u][s] : 0.f;
+          ak[v] = fmaf(w[u], gv, ak[v]);
+        }
+    }
+    if (last) {  // Ko[f][q]: sum over the seeded streams of h_s[f] * dJ_s[q]; bo[q]: sum of dJ_value
+      float hv[U][S];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int s = 0; s < S; ++s) hv[u][s] = w[u] * ldm(Hb + hi_row(e, mc[u], s, S, N) + fc, sp.out[s] >= 0);
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) {
+        if (q >= dout) break;
+        float uv[U][S];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
+            uv[u][s] = dJ[((size_t)orow * ldJ + j0 + mc[u]) * dout + q];
+          }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (sp.out[0] >= 0) abo[q] = fmaf(w[u], uv[u][0], abo[q]);
+#pragma unroll
+          for (int s = 0; s < S; ++s) ao[q] = fmaf(hv[u][s], uv[u][s], ao[q]);
         }
       }
     }
   }
-  for (int v = 0; v < nv; ++v) red[half][v][f] = acc[v];
-  __syncthreads();
-  if (half == 0 && f < we) {
-    const int pin = e == 0 ? d.d_in : hw(d, e - 1);
-    row[off_layer(d, e) + pin * we + f] = red[0][0][f] + red[1][0][f];  // bias of hidden layer e
-    if (first)
-      for (int v = 0; v < d.d_in; ++v) row[v * we + f] = red[0][1 + v][f] + red[1][1 + v][f];
-    if (last) {
-      const int o = 1 + (first ? d.d_in : 0);
-      for (int q = 0; q < dout; ++q) row[off_layer(d, Lh) + f * dout + q] = red[0][o + q][f] + red[1][o + q][f];
-    }
+  red[g][0][f] = ab;
+#pragma unroll
+  for (int v = 0; v < TDQ_MAXD; ++v) red[g][1 + v][f] = ak[v];
+#pragma unroll
+  for (int q = 0; q < TDQ_MAXO; ++q) {
+    red[g][1 + TDQ_MAXD + q][f] = ao[q];
+    red[g][1 + TDQ_MAXD + TDQ_MAXO + q][f] = abo[q];
   }
-  if (last && t < dout) {
+  lds_sync();
+  // fixed-order sums over the point groups: thread (f, slot g) of the first HI_VSLOTS / ... slots
+  for (int sl = g; sl < HI_VSLOTS; sl += HI_VG) {
     float a = 0.f;
-    if (sp.out[0] >= 0)
-      for (int m = n0; m < n1; ++m) a += dJ[((size_t)sp.out[0] * ldJ + j0 + m) * dout + t];
-    row[off_layer(d, Lh) + hw(d, Lh - 1) * dout + t] = a;
+#pragma unroll
+    for (int gg = 0; gg < HI_VG; ++gg) a += red[gg][sl][f];
+    if (f >= we) continue;
+    if (sl == 0) {
+      const int pin = e == 0 ? din : hw(d, e - 1);
+      row[off_layer(d, e) + pin * we + f] = a;  // bias of hidden layer e
+    } else if (sl <= TDQ_MAXD) {
+      if (first && sl - 1 < din) row[(sl - 1) * we + f] = a;
+    } else if (sl <= TDQ_MAXD + TDQ_MAXO) {
+      const int q = sl - 1 - TDQ_MAXD;
+      if (last && q < dout) row[off_layer(d, Lh) + f * dout + q] = a;
+    } else {
+      const int q = sl - 1 - TDQ_MAXD - TDQ_MAXO;
+      if (last && q < dout && f == 0) row[off_layer(d, Lh) + hw(d, Lh - 1) * dout + q] = a;
+    }
   }
 }
 
@@ -633,6 +871,25 @@ int hi_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const fl
   return (int)hipErrorInvalidValue;
 }
 
+int hi_wgrad(const float* X, int N, const NetDims& d, const HiSpec& sp, const float* dJ, int ldJ, int j0,
+             const float* Hb, const float* Bb, float* work, int Pst, int ks, hipStream_t st) {
+  const int n_tiles = (d.n_hidden - 1) * (HI_W / HI_TILE) * (HI_W / HI_TILE);
+  if (n_tiles > 0) {
+    hipLaunchKernelGGL(jet_hi_wgrad_kernel, dim3(n_tiles, ks), dim3(256), 0, st, N, sp.S, d, Hb, Bb, work, Pst);
+    TDQ_CHECK_LAUNCH();
+  }
+#define HI_G(SS)                                                                                              \
+  if (sp.S == SS) {                                                                                           \
+    hipLaunchKernelGGL(jet_hi_wvec_kernel<SS>, dim3(d.n_hidden, ks), dim3(HI_W * HI_VG), 0, st, X, N, d, sp, dJ, \
+                       ldJ, j0, Hb, Bb, work, Pst);                                                           \
+    TDQ_CHECK_LAUNCH();                                                                                       \
+    return 0;                                                                                                 \
+  }
+  HI_G(2) HI_G(3) HI_G(4) HI_G(5) HI_G(6) HI_G(7) HI_G(8)
+#undef HI_G
+  return (int)hipErrorInvalidValue;
+}
+
 // one activation-sized scratch buffer (Z, H or B), in floats
 size_t hi_act_floats(int N, int n_hidden) { return (size_t)n_hidden * N * HI_MAXS * HI_W; }
 
@@ -678,10 +935,8 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   int rc = hi_chain(N, P, d, sp, dJ, ldJ, j0, Z, Z + 2 * A, st);
   if (rc) return rc;
   const int ks = hi_splits(N);
-  const int n_tiles = (n_hidden - 1) * (HI_W / HI_TILE) * (HI_W / HI_TILE);
-  hipLaunchKernelGGL(jet_hi_wgrad_kernel, dim3(n_tiles + n_hidden, ks), dim3(256), 0, st, X, N, d, sp, dJ, ldJ, j0,
-                     Z + A, Z + 2 * A, work, Pst, n_tiles);
-  TDQ_CHECK_LAUNCH();
+  rc = hi_wgrad(X, N, d, sp, dJ, ldJ, j0, Z + A, Z + 2 * A, work, Pst, ks, st);
+  if (rc) return rc;
   hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((Ptot + 255) / 256), dim3(256), 0, st, work, ks, Pst, Ptot, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
