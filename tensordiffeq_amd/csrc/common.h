@@ -3,16 +3,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt), not for
-// its outstanding global loads / stores as __syncthreads() does (a workgroup-scope fence covers
-// global memory too, so every barrier would cost a full memory latency).  For kernels whose waves
-// exchange data through LDS only.
-__device__ __forceinline__ void lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define TDQ_WAVE 64

@@ -29,13 +29,12 @@
 //   * weight gradients: dK_i = H_{i-1}^T B_i as 32 x 32 tiles over point splits (one slab row per
 //     split), per-layer vectors (biases, K0, Ko, bo) in a second kernel; a fixed-order sum of the
 //     split rows gives the gradient (deterministic), which the fused step tail adds to theta's.
-// Waves of a workgroup share data through LDS only: barriers are lds_sync() (no global-memory
-// wait), and loads are unconditional from clamped addresses (a conditional load is a branch with
-// a wait behind it).  The stream count is a template parameter, and the common plan - the
+// Loads are unconditional from clamped addresses (a conditional load is a branch with a wait
+// behind it).  The stream count is a template parameter, and the common plan - the
 // univariate chain u, u_v, u_vv, u_vvv(, u_vvvv) of the reference's periodic BCs - has its tanh jet
 // and adjoint as straight-line code; other plans interpret the partition table.
 // History (AC-baseline, 402 points, order 4; profiles/): interpreted 256-thread first build
-// 0.31 + 0.40 ms per step; this layout 31 + 63 us isolated before lds_sync.
+// 0.31 + 0.40 ms per step; this layout 26 + 57 us isolated (profiles/r4g_kernel_stats_hi_isolated.txt).
 #include "jet_common.h"
 
 #define HI_MAXS 8
@@ -390,7 +389,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int j = 0; j < HI_PT; ++j) z[j][0] += b;
       HI_TS()
-      lds_sync();  // every thread done reading sh.A / sh.W
+      __syncthreads();  // every thread done reading sh.A / sh.W
       if (i + 1 < Lh) hi_put_w(sh, wr);
       HI_TS()
     }
@@ -414,7 +413,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = h[s];
     }
     HI_TS()
-    lds_sync();
+    __syncthreads();
     HI_TS()
   }
   // ---- output layer: u_s[q] = sum_f h_s[f] Ko[f][q] (+ bo[q] on the value stream): per-feature
@@ -435,7 +434,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         for (int q = 0; q < TDQ_MAXO; ++q)
           if (q < dout) part[(((pg * HI_PT + j) * S + s) * TDQ_MAXO + q) * HI_W + f] = sh.A[pg * HI_PT + j][s][f] * ko[q];
   }
-  lds_sync();
+  __syncthreads();
   for (int c = t; c < HI_NP * S * dout; c += blockDim.x) {
     const int q = c % dout, s = (c / dout) % S, pp = c / (dout * S);
     const int m = blockIdx.x * HI_NP + pp;
@@ -515,7 +514,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
     if (i == 0) break;
     // hb_{i-1}[k = f] = sum_o zb_i[o] W_i[f][o]; the next layer's pre-activations load meanwhile
     hi_put_w(sh, wr);
-    lds_sync();
+    __syncthreads();
     if (i >= 2) hi_get_w(wr, P, d, i - 1);
     const int wp = hw(d, i - 1);
 #pragma unroll
@@ -550,7 +549,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         fma4(g1, w1);
       }
     }
-    lds_sync();  // sh.A / sh.W reused by the next layer
+    __syncthreads();  // sh.A / sh.W reused by the next layer
   }
 }
 
@@ -600,7 +599,7 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
         *reinterpret_cast<f32x4*>(&Hc[rr][c]) = hv[u];
         *reinterpret_cast<f32x4*>(&Gc[rr][c]) = gv[u];
       }
-      lds_sync();
+      __syncthreads();
       if (r + HI_CHUNK < r1) load(r + HI_CHUNK);
       for (int rb = 0; rb < HI_CHUNK; rb += 8) {  // 16 LDS reads in flight, then 32 FMAs
         float2 h2[8], g2[8];
@@ -617,7 +616,7 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
           acc[1][1] = fmaf(h2[rr].y, g2[rr].y, acc[1][1]);
         }
       }
-      lds_sync();
+      __syncthreads();
     }
     float* dk = row + off_layer(d, i);
 #pragma unroll
@@ -726,7 +725,7 @@ __global__ void __launch_bounds__(HI_W * HI_VG) jet_hi_wvec_kernel(const float* 
     red[g][1 + TDQ_MAXD + q][f] = ao[q];
     red[g][1 + TDQ_MAXD + TDQ_MAXO + q][f] = abo[q];
   }
-  lds_sync();
+  __syncthreads();
   // fixed-order sums over the point groups: thread (f, slot g) of the first HI_VSLOTS / ... slots
   for (int sl = g; sl < HI_VSLOTS; sl += HI_VG) {
     float a = 0.f;
