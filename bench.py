@@ -380,8 +380,8 @@ def main(argv=None):
                          "ac-dist / discovery)")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--layers", default=None,
-                    help="network layer sizes (default: the problem's reference net; widths > 128 run the "
-                         "layer-wise engine)")
+                    help="network layer sizes (default: the problem's reference net; widths 129-256 run "
+                         "the fused kernels in bf16, wider nets / other precisions the layer-wise engine)")
     ap.add_argument("--no-l2", action="store_true", help="skip the accuracy runs")
     ap.add_argument("--acc-seeds", type=int, nargs="*", default=[0, 1, 2],
                     help="seeds of the full-schedule accuracy runs (single GPU only)")

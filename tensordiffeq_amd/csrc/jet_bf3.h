@@ -110,9 +110,12 @@ __device__ __forceinline__ f32x4 mfma_aa(const bf16x8& ah, const bf16x8& al, con
 // wave-private region of global scratch (L2-resident: every wave writes its own lines and reads
 // them back after an s_waitcnt), leaving the LDS to the backward's dK images.
 __host__ __device__ constexpr bool bf3_wide(int WT, int S) { return S * WT > 32; }
-__host__ __device__ constexpr int bf3_wpe(int WT, int S, bool lo) { return (lo || bf3_wide(WT, S)) ? 1 : 2; }
+__host__ __device__ constexpr int bf3_wpe(int WT, int S, bool lo) { return (lo || bf3_wide(WT, S) || WT > 8) ? 1 : 2; }
 __host__ __device__ constexpr bool bf3_gstage(int WT, int S, bool lo) { return lo && bf3_wide(WT, S); }
 // bf16x4 entries of one wave's fragment stage ([s][kb][hl][lane][2 halves])
+// backward [point][feature] image row stride, bf16: 144 (72 words = 8 mod 64) up to 128 features,
+// 16 WT + 16 beyond (WT = 16: 272 = 136 words, again 8 mod 64, so the same conflict-free pattern)
+__host__ __device__ constexpr int bf3_img_rs(int WT) { return WT > 8 ? 16 * WT + 16 : 144; }
 __host__ __device__ constexpr int stage_wave_elems(int WT, int S, bool lo) { return S * (WT / 2) * (lo ? 2 : 1) * 128; }
 
 // the wave's own stage writes have landed before it reads them back (global stage only; an LDS
@@ -863,9 +866,13 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
 #ifndef TDQ_BWD_WIDE
 #define TDQ_BWD_WIDE 1
 #endif
+// WT = 16: dK column tiles per pass (of a wave's 8; -DTDQ_W16_NCP for A/B runs)
+#ifndef TDQ_W16_NCP
+#define TDQ_W16_NCP 2
+#endif
 // (wide plans: 4 waves - an 8-wave workgroup puts two waves on each SIMD, 256 registers each)
 __host__ __device__ constexpr int bwd_waves(int WT, bool lo, int S) {
-  return (TDQ_BWD_WIDE && !lo && WT >= 4 && !bf3_wide(WT, S)) ? 8 : 4;
+  return (TDQ_BWD_WIDE && !lo && WT >= 4 && WT <= 8 && !bf3_wide(WT, S)) ? 8 : 4;
 }
 
 template <int WT, int S, int NSO, bool LO>
@@ -893,13 +900,19 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #endif
   constexpr int NWV = bwd_waves(WT, LO, S), PTS = 16 * NWV;  // waves / points per workgroup
   constexpr bool GST = bf3_gstage(WT, S, LO);                 // zb stage in global scratch
-  constexpr int RS = 144;
+  constexpr int RS = bf3_img_rs(WT);
   constexpr int IMG = PTS * RS;
   // dK tile ownership: the WT x WT output tiles split into (NWV/2) x 2 blocks, wave w owns block
   // (w >> 1, w & 1): NR x NC tiles from NR A and NC B fragments per k-block (4 waves: quadrants;
   // a 2 x 8 strip per wave would need 2 + 8 fragment loads for the same 16 tiles at WT = 8)
   constexpr int NR = WT / (NWV / 2);
   constexpr int NC = WT / 2;
+  // WT = 16: the 8 x 8 tiles of a wave's block take 256 accumulator registers - done in PC column
+  // passes of NCP tiles (the images are rebuilt per pass; a pass's MFMAs read 8 + NCP fragments)
+  constexpr int NCP = NC > 4 ? TDQ_W16_NCP : NC, PC = NC / NCP;
+  // row tiles past the fourth start a second transposed-read base (the immediate offsets 16 r of
+  // one base must stay below the swizzled column bit 6)
+  constexpr int RB = NR > 4 ? 2 : 1, NRB = NR / RB;
   // images: h hi, (h lo,) zb hi, (zb lo) - the lo images only under LO
   constexpr int HL = LO ? 2 : 1;
   constexpr int IH = 0, IHL = IMG, IZ = HL * IMG, IZL = 3 * IMG;
@@ -1068,12 +1081,18 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
     for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT, LO>(Hp, 0, t);
     TDQ_TS(tsb);
 
+#pragma unroll
+    for (int pc = 0; pc < PC; ++pc) {
+    if (pc > 0) {  // next column pass: the images are rebuilt from stream 0
+#pragma unroll
+      for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT, LO>(Hp, 0, t);
+    }
     // (c) dK_i = sum_points sum_streams h_{i-1} zb^T on bf16x3 MFMA, points on the k index
-    f32x4 dw[NR][NC];
+    f32x4 dw[NR][NCP];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) dw[r][c] = zero4();
+      for (int c = 0; c < NCP; ++c) dw[r][c] = zero4();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       // previous users of the region done: the zb stage (s = 0) / the last stream's images (one
@@ -1081,7 +1100,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       // after the MFMAs of s - 1, the last readers of the buffer written here)
       if (s == 0 || !DBUF) __syncthreads();
       __bf16* const im = img + (DBUF ? (s & 1) * IBUF : 0);
-      if (s == 0 && w == 0) {  // bias of layer i: partials of all waves landed before this barrier
+      if (s == 0 && w == 0 && pc == 0) {  // bias of layer i: partials of all waves landed before this barrier
         const float* accBi = accB + (i & 1) * NWV * W;
         const int bo = off_layer(d, i) + hw(d, i - 1) * hw(d, i);
         for (int f = l; f < hw(d, i); f += 64) {
@@ -1113,26 +1132,30 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
         for (int t = 0; t < WT; ++t) hp[t] = hs_load_c<WT, LO>(Hp, s + 1, t);
       }
       __syncthreads();
-      if (s == 0) TDQ_TS(tsb + 1);
+      if (s == 0 && pc == 0) TDQ_TS(tsb + 1);
       // transposed-read bases of this wave's first row / column tile: the other tiles (+16 r / c
-      // columns) and the second k-block (+32 rows) are immediate offsets of these four addresses
-      // (adding 16 r never crosses the swizzled bit 6: the bases' low six bits + 16 (NR - 1) < 64)
-      const int ra1 = tr_row * RS + ((16 * dw_row(w, 0) + tr_col1) ^ swz);
-      const int ra2 = (tr_row + 4) * RS + ((16 * dw_row(w, 0) + tr_col2) ^ swz);
-      const int ca1 = tr_row * RS + ((16 * dw_col(w, 0) + tr_col1) ^ swz);
-      const int ca2 = (tr_row + 4) * RS + ((16 * dw_col(w, 0) + tr_col2) ^ swz);
+      // columns) and the second k-block (+32 rows) are immediate offsets of these addresses (adding
+      // 16 r never crosses the swizzled bit 6: the bases' low six bits + 16 (NRB - 1) < 64)
+      int ra1[RB], ra2[RB];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        ra1[rb] = tr_row * RS + ((16 * (dw_row(w, 0) + NRB * rb) + tr_col1) ^ swz);
+        ra2[rb] = (tr_row + 4) * RS + ((16 * (dw_row(w, 0) + NRB * rb) + tr_col2) ^ swz);
+      }
+      const int ca1 = tr_row * RS + ((16 * (dw_col(w, 0) + NCP * pc) + tr_col1) ^ swz);
+      const int ca2 = (tr_row + 4) * RS + ((16 * (dw_col(w, 0) + NCP * pc) + tr_col2) ^ swz);
 #pragma unroll
       for (int kb = 0; kb < PTS / 32; ++kb) {  // k-blocks of 32 points
         bf16x8 Ah[NR], Al[NR];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-          const int off = ra1 + 32 * kb * RS + 16 * r;
-          const int of2 = ra2 + 32 * kb * RS + 16 * r;
+          const int off = ra1[r / NRB] + 32 * kb * RS + 16 * (r % NRB);
+          const int of2 = ra2[r / NRB] + 32 * kb * RS + 16 * (r % NRB);
           Ah[r] = cat8(tr_read(im + IH + off), tr_read(im + IH + of2));
           if constexpr (LO) Al[r] = cat8(tr_read(im + IHL + off), tr_read(im + IHL + of2));
         }
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
+        for (int c = 0; c < NCP; ++c) {
           const int off = ca1 + 32 * kb * RS + 16 * c;
           const int of2 = ca2 + 32 * kb * RS + 16 * c;
           const bf16x8 Bh = cat8(tr_read(im + IZ + off), tr_read(im + IZ + of2));
@@ -1147,7 +1170,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
       // dK_i rows / columns this wave owns.  Unpadded width: one lane offset + uniform (r, c2, c)
       // offsets through a buffer resource (no per-store address VGPRs, no exec branches);
       // padded width: guarded stores.
-      int in0 = 16 * dw_row(w, 0) + 4 * g, out0 = 16 * dw_col(w, 0) + p;
+      int in0 = 16 * dw_row(w, 0) + 4 * g, out0 = 16 * (dw_col(w, 0) + NCP * pc) + p;
       // opaque per iteration: otherwise LICM hoists the padded path's 64 guarded store addresses
       // (and their exec masks) out of the layer loop, where they stay live and spill
       asm volatile("" : "+v"(in0), "+v"(out0));
@@ -1159,7 +1182,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
-          for (int c2 = 0; c2 < NC; ++c2)
+          for (int c2 = 0; c2 < NCP; ++c2)
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const float v = dw[r][c2][c];
@@ -1173,7 +1196,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
-          for (int c2 = 0; c2 < NC; ++c2)
+          for (int c2 = 0; c2 < NCP; ++c2)
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const int in = in0 + 16 * r + c, out = out0 + 16 * c2;
@@ -1181,6 +1204,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
             }
       }
     }
+    }  // column passes
     TDQ_TS(tsb + 2);
     __syncthreads();  // images consumed: the region becomes the zb fragment stage
     TDQ_TS(tsb + 3);
@@ -1257,7 +1281,7 @@ inline int h0_recompute() {
 
 inline size_t bwd_bf3_lds(int WT, int S, bool lo) {
   const int W = 16 * WT, hl = lo ? 2 : 1, nwv = bwd_waves(WT, lo, S);
-  const size_t u1 = (size_t)(lo ? 1 : 2) * (2 * hl * 16 * nwv * 144) / 2,
+  const size_t u1 = (size_t)(lo ? 1 : 2) * (2 * hl * 16 * nwv * bf3_img_rs(WT)) / 2,
                u2 = bf3_gstage(WT, S, lo) ? 0 : (size_t)nwv * S * WT * hl * 128;
   const size_t u = ((u1 > u2 ? u1 : u2) + 3) / 4 * 4;
   return (u + 3 * nwv * W) * sizeof(float);
@@ -1302,7 +1326,11 @@ int launch_fwd_bf3_lo(const Bf3Args& a) {
 
 template <int WT, int S, int NSO>
 int launch_fwd_bf3(const Bf3Args& a) {
-  return a.lo ? launch_fwd_bf3_lo<WT, S, NSO, true>(a) : launch_fwd_bf3_lo<WT, S, NSO, false>(a);
+  if constexpr (WT > 8) {  // widths 129..256: bf16 only (bf16x3 keeps the layer-wise engine)
+    return a.lo ? (int)hipErrorInvalidValue : launch_fwd_bf3_lo<WT, S, NSO, false>(a);
+  } else {
+    return a.lo ? launch_fwd_bf3_lo<WT, S, NSO, true>(a) : launch_fwd_bf3_lo<WT, S, NSO, false>(a);
+  }
 }
 
 template <int WT, int S, int NSO, bool LO>
@@ -1325,7 +1353,11 @@ int launch_bwd_bf3_lo(const Bf3Args& a) {
 
 template <int WT, int S, int NSO>
 int launch_bwd_bf3(const Bf3Args& a) {
-  return a.lo ? launch_bwd_bf3_lo<WT, S, NSO, true>(a) : launch_bwd_bf3_lo<WT, S, NSO, false>(a);
+  if constexpr (WT > 8) {
+    return a.lo ? (int)hipErrorInvalidValue : launch_bwd_bf3_lo<WT, S, NSO, false>(a);
+  } else {
+    return a.lo ? launch_bwd_bf3_lo<WT, S, NSO, true>(a) : launch_bwd_bf3_lo<WT, S, NSO, false>(a);
+  }
 }
 
 // per-width-class entry points (jet_bf3_w{2,4,8}.hip); return hipErrorInvalidValue when
@@ -1333,6 +1365,8 @@ int launch_bwd_bf3(const Bf3Args& a) {
 int bf3_fwd_w2(int S, int nso, const Bf3Args& a);
 int bf3_fwd_w4(int S, int nso, const Bf3Args& a);
 int bf3_fwd_w8(int S, int nso, const Bf3Args& a);
+int bf3_fwd_w16(int S, int nso, const Bf3Args& a);
 int bf3_bwd_w2(int S, int nso, const Bf3Args& a);
 int bf3_bwd_w4(int S, int nso, const Bf3Args& a);
 int bf3_bwd_w8(int S, int nso, const Bf3Args& a);
+int bf3_bwd_w16(int S, int nso, const Bf3Args& a);

@@ -1,5 +1,5 @@
 // Host ABI + weight-image packing for the split-bf16 (bf16x3) jet kernels (kernels: jet_bf3.h,
-// instantiations: jet_bf3_w{2,4,8}.hip), and the fused step tail of a captured Adam step.
+// instantiations: jet_bf3_w{2,4,8,16}.hip), and the fused step tail of a captured Adam step.
 //
 // Step tail (tdq_step_tail_bf3): the single-GPU Adam step used to end in seven small launches
 // (weight-image pack, loss reduction, two slab-reduction passes, bookkeeping, Adam) of ~4.7 us
@@ -345,8 +345,10 @@ int launch_pack(const float* P, bf16x8* fimg, bf16x8* bimg, float* aux, NetDims 
 // S <= 8 streams at every width class (S * WT <= 32: the 2-waves-per-SIMD kernels; beyond: the
 // "wide" one-wave-per-SIMD kernels of jet_bf3.h)
 bool bf3_ok(int WT, int S, int d_in, int d_out, int n_hidden) {
-  return (WT == 2 || WT == 4 || WT == 8) && S >= 1 && S <= TDQ_MAXS && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO &&
-         n_hidden >= 1;
+  // WT = 16 (widths 129..256, bf16 only): S <= 4 keeps the per-wave stream registers of the wide
+  // WT = 8, S = 8 kernels
+  return (WT == 2 || WT == 4 || WT == 8 || (WT == 16 && S <= 4)) && S >= 1 && S <= TDQ_MAXS &&
+         d_in <= TDQ_MAXD && d_out <= TDQ_MAXO && n_hidden >= 1;
 }
 
 int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
@@ -354,6 +356,7 @@ int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
     case 2: return fwd ? bf3_fwd_w2(S, nso, a) : bf3_bwd_w2(S, nso, a);
     case 4: return fwd ? bf3_fwd_w4(S, nso, a) : bf3_bwd_w4(S, nso, a);
     case 8: return fwd ? bf3_fwd_w8(S, nso, a) : bf3_bwd_w8(S, nso, a);
+    case 16: return fwd ? bf3_fwd_w16(S, nso, a) : bf3_bwd_w16(S, nso, a);
     default: return (int)hipErrorInvalidValue;
   }
 }

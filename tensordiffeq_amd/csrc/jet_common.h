@@ -75,6 +75,7 @@ static inline int width_tiles(int width) {
   if (wt <= 2) return 2;
   if (wt <= 4) return 4;
   if (wt <= 8) return 8;
+  if (wt <= 16) return 16;  // split-bf16 kernels only (bf3_ok)
   return -1;
 }
 

@@ -666,29 +666,37 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
     if hop is not None and ranges[0][1] < program.n_hi:
         raise RuntimeError("point ranges: the first range must hold the high-order points")
     cur = torch.cuda.current_stream(flat.device)
-    # the high-order points' extra streams run on a branch of their own (a hundred workgroups of
-    # long per-layer chains): their forward beside range 0's forward, joined before its loss (they
-    # touch only their own J rows); the gradient of their adjoints after range 0's backward, beside
-    # the longer range 1 (on range 0's stream: a third branch there made hipStreamEndCapture crash
-    # on MI355X / ROCm 7.2)
-    hs = hop.stream if hop is not None else None
-    if hs is not None and os.environ.get("TDQ_HI_BRANCH", "1") == "0":  # all on range 0's stream
-        hs = None
+    # the high-order points' extra streams (a hundred workgroups of long per-layer chains; they
+    # touch only their own J rows): TDQ_HI_PLACE = side_after (default: forward on a side branch
+    # beside range 0's forward, joined before its loss; gradient after range 0's backward, beside
+    # the longer range 1), side_before (gradient between range 0's loss and backward),
+    # serial_after / serial_before (forward on range 0's stream too).  A third branch for the
+    # gradient made hipStreamEndCapture crash on MI355X / ROCm 7.2.
+    place = os.environ.get("TDQ_HI_PLACE", "side_after")
+    hs = hop.stream if (hop is not None and place.startswith("side")) else None
+    bwd_first = place.endswith("before")
     if hs is not None:
         hs.wait_stream(cur)
         with torch.cuda.stream(hs):
             hop.forward(J, flat)
-    if len(ranges) == 1:
-        lo, hi, b0, nb = ranges[0]
-        if hop is not None and hs is None:
+
+    def chain(k, lo, hi, b0, nb, st):
+        if k == 0 and hop is not None and hs is None:
             hop.forward(J, flat)
         jet_hip.forward_range(saved, J, lo, hi)
-        if hs is not None:
-            cur.wait_stream(hs)
+        if k == 0 and hs is not None:
+            st.wait_stream(hs)
         fop.run_range(J, b0, nb)
-        jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
-        if hop is not None:
+        if k == 0 and hop is not None and bwd_first:
             hop.backward(fop.dJ, flat)
+        jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
+        if k == 0 and prereduce:
+            jet_hip.slab_prereduce(saved, work, 0, prereduce)
+        if k == 0 and hop is not None and not bwd_first:
+            hop.backward(fop.dJ, flat)
+
+    if len(ranges) == 1:
+        chain(0, *ranges[0], cur)
         return saved, work
     # (keeping one range on the current stream measured the same: the graph runtime picks the
     # hardware queues of its branches itself, and the join still waits ~9 us across queues)
@@ -696,17 +704,7 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
         st.wait_stream(cur)
     for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
         with torch.cuda.stream(st):
-            if k == 0 and hop is not None and hs is None:
-                hop.forward(J, flat)
-            jet_hip.forward_range(saved, J, lo, hi)
-            if k == 0 and hs is not None:
-                st.wait_stream(hs)
-            fop.run_range(J, b0, nb)
-            jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
-            if k == 0 and prereduce:
-                jet_hip.slab_prereduce(saved, work, 0, prereduce)
-            if k == 0 and hop is not None:  # behind the shorter range: beside range 1's backward
-                hop.backward(fop.dJ, flat)
+            chain(k, lo, hi, b0, nb, st)
     for st in streams[:len(ranges)]:
         cur.wait_stream(st)
     return saved, work

@@ -81,13 +81,21 @@ def hip_config(net, plan, precision=None):
         return {"d_in": d_in, "d_out": d_out, "width": max(hidden), "widths": tuple(hidden), "WT": WT, "S": S,
                 "n_hidden": len(hidden), "precision": precision, "engine": "layered", "why": why}
 
+    if WT > 16:
+        return layered("hidden width > 256")
     if WT > 8:
-        return layered("hidden width > 128")
+        # widths 129..256: the split-bf16 kernels at WT = 16 in bf16 with S <= 4 (csrc/jet_bf3_w16.hip);
+        # fp32 / bf16x3 there keep the layer-wise engine
+        if precision != "bf16":
+            return layered(f"hidden width > 128 in {precision}")
+        if S > 4:
+            return layered("hidden width > 128 with more than 4 streams")
+        WT = 16
     if len(hidden) > 16:
         return layered("more than 16 hidden layers")
     if d_in > 8 or d_out > 4:
         return layered("input width > 8 or output width > 4")
-    if WT not in (1, 2, 4, 8):
+    if WT not in (1, 2, 4, 8, 16):
         WT = 4 if WT == 3 else 8
     if precision in ("bf16x3", "bf16") and WT < 2:
         precision = "fp32"

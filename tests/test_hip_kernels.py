@@ -4,7 +4,7 @@ Jet forward: every derivative stream against the torch jet engine (itself checke
 autograd in test_jet.py) AND directly against nested ``torch.autograd.grad``.
 Jet backward: the flat parameter gradient of a random linear functional of J against autograd
 through the torch jet.  Shapes cover non-multiple-of-64 point counts, every width-tile class
-(WT = 1, 2, 4, 8 incl. padded widths), 1-8 streams, d_in 1-3, d_out 1-2, 1-4 hidden layers.
+(WT = 1, 2, 4, 8 incl. padded widths; WT = 16 in bf16), 1-8 streams, d_in 1-3, d_out 1-2, 1-4 hidden layers.
 """
 import pytest
 import torch
@@ -131,6 +131,52 @@ def test_jet_backward_matches_autograd(sizes, reqs, N, prec):
             a, r = g_hip[off:off + n], g_ref[off:off + n]
             assert ((a - r).norm() / r.norm().clamp_min(1e-30)).item() < 20 * TOL_BWD[prec], (off, n)
             off += n
+
+
+# hidden widths 129..256: the split-bf16 kernels at WT = 16, bf16 only, S <= 4 (csrc/jet_bf3_w16.hip)
+WIDE256_CASES = [
+    ([2, 256, 256, 256, 256, 1], [(0,), (1,), (0, 0)], 1000),      # AC plan at width 256, S = 4
+    ([2, 200, 256, 1], [(0,), (0, 0)], 333),                         # unequal / padded widths, S = 3
+    ([3, 160, 160, 2], [(0,), (1,)], 130),                           # padded, d_out = 2
+    ([2, 256, 1], [(0,)], 70),                                       # one hidden layer, S = 2
+    ([2, 256, 256, 1], [], 65),                                      # value only
+]
+
+
+@pytest.mark.parametrize("sizes,reqs,N", WIDE256_CASES)
+def test_wide256_bf16_kernels_match_fp64(sizes, reqs, N):
+    """Forward streams and the parameter gradient of the width-256 fused kernels vs the fp64 torch
+    jet, at the bf16 bounds of the width-128 kernels."""
+    from tensordiffeq_amd.ops import jet_hip, jet_mlp
+    net, X, plan = _setup(sizes, reqs, N, seed=2)
+    cfg = jet_mlp.hip_config(net, plan, "bf16")
+    assert cfg.get("engine") != "layered" and cfg["WT"] == 16 and cfg["precision"] == "bf16"
+    G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
+    p = net.flat.detach().clone().requires_grad_(True)
+    J = jet_hip.JetMLPFunction.apply(X, p, net, plan, "bf16")
+    (J.double() * G).sum().backward()
+    p64 = net.flat.detach().double().clone().requires_grad_(True)
+    Jr = jet_forward(X.double(), net.weights(p64), plan)
+    (Jr * G).sum().backward()
+    scale = Jr.detach().abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
+    ferr = ((J.detach().double() - Jr.detach()).abs() / scale).max().item()
+    g_hip, g_ref = p.grad.double(), p64.grad
+    gerr = ((g_hip - g_ref).norm() / g_ref.norm()).item()
+    print(f"KERNEL_ERR w256 bf16 {sizes} S={plan.S} fwd {ferr:.3e} bwd {gerr:.3e}")
+    assert ferr < TOL_FWD_BF16_SHALLOW, ferr
+    assert gerr < TOL_BWD["bf16"], gerr
+    off = 0
+    for k, b in net.weights(p64.detach()):
+        for blk in (k, b):
+            n = blk.numel()
+            a, r = g_hip[off:off + n], g_ref[off:off + n]
+            assert ((a - r).norm() / r.norm().clamp_min(1e-30)).item() < 20 * TOL_BWD["bf16"], (off, n)
+            off += n
+    # deterministic
+    p2 = net.flat.detach().clone().requires_grad_(True)
+    J2 = jet_hip.JetMLPFunction.apply(X, p2, net, plan, "bf16")
+    (J2.double() * G).sum().backward()
+    assert torch.equal(J2, J) and torch.equal(p2.grad, p.grad)
 
 
 @pytest.mark.parametrize("prec", PRECS)

@@ -107,14 +107,21 @@ def test_hip_config_unequal_widths():
 
 
 def test_hip_config_wide_hidden_layers_use_layered_engine():
-    """Hidden widths > 128 leave the fused kernels' envelope: the layer-wise engine serves them
-    (library GEMMs in the requested precision + HIP epilogues), never the fused tail / point ranges."""
+    """Hidden widths > 128 leave the fused kernels' envelope except in bf16 with S <= 4 up to
+    width 256 (WT = 16); elsewhere the layer-wise engine serves them (library GEMMs in the
+    requested precision + HIP epilogues), never the fused tail / point ranges."""
     from tensordiffeq_amd.jet import JetPlan
     from tensordiffeq_amd.models.networks import TanhMLP
     from tensordiffeq_amd.ops import jet_hip
     from tensordiffeq_amd.ops.jet_mlp import hip_config
-    cfg = hip_config(TanhMLP([2, 256, 256, 1], device="cpu"), JetPlan([(0,), (1,), (0, 0)], 2), "bf16")
-    assert jet_hip.is_layered(cfg) and cfg["precision"] == "bf16" and not jet_hip.is_split_bf16(cfg)
+    ac = JetPlan([(0,), (1,), (0, 0)], 2)
+    cfg = hip_config(TanhMLP([2, 256, 256, 1], device="cpu"), ac, "bf16")
+    assert not jet_hip.is_layered(cfg) and cfg["WT"] == 16 and jet_hip.is_split_bf16(cfg)
+    for prec in ("bf16x3", "fp32"):
+        cfg = hip_config(TanhMLP([2, 256, 256, 1], device="cpu"), ac, prec)
+        assert jet_hip.is_layered(cfg) and cfg["precision"] == prec
+    assert jet_hip.is_layered(hip_config(TanhMLP([2, 272, 1], device="cpu"), ac, "bf16"))
+    assert jet_hip.is_layered(hip_config(TanhMLP([2, 256, 1], device="cpu"), JetPlan([(0, 0), (1, 1)], 2), "bf16"))
     cfg = hip_config(TanhMLP([2, 64, 200, 1], device="cpu"), JetPlan([(0, 0)], 2), "bf16x3")
     assert jet_hip.is_layered(cfg) and cfg["widths"] == (64, 200)
     assert not jet_hip.is_layered(hip_config(TanhMLP([2, 128, 1], device="cpu"), JetPlan([], 2), "bf16"))
