@@ -27,8 +27,9 @@
 //     layer's weights load into registers during this layer's GEMM.
 //   * adjoint chain (same layout): zb_i = tanh-jet adjoint of hb_i, hb_{i-1} = W_i zb_i -> B.
 //   * weight gradients: dK_i = H_{i-1}^T B_i as 32 x 32 tiles over point splits (one slab row per
-//     split), per-layer vectors (biases, K0, Ko, bo) in a second kernel; a fixed-order sum of the
-//     split rows gives the gradient (deterministic), which the fused step tail adds to theta's.
+//     split); the vector parameters (biases, K0, Ko, bo) summed per workgroup by the chain itself
+//     (one vslab row per workgroup); a fixed-order sum of the rows gives the gradient
+//     (deterministic), which the fused step tail adds to theta's.
 // Loads are unconditional from clamped addresses (a conditional load is a branch with a wait
 // behind it).  The stream count is a template parameter, and the common plan - the
 // univariate chain u, u_v, u_vv, u_vvv(, u_vvvv) of the reference's periodic BCs - has its tanh jet
@@ -451,15 +452,57 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
   HI_TS_PRINT("fwd")
 }
 
+// Per-workgroup partials of the vector parameters (hidden biases, K0, Ko, bo), written by the
+// adjoint chain (one row per workgroup, compact layout below) and summed by jet_hi_reduce_kernel:
+//   [i * HI_W + f]                       bias of hidden layer i
+//   [(Lh + v) * HI_W + f]                K0[v][f]
+//   [(Lh + d_in) * HI_W + f * MAXO + q]   Ko[f][q]
+//   [(Lh + d_in) * HI_W + HI_W * MAXO + q] bo[q]
+#define HI_VSLOTS (1 + TDQ_MAXD + 2 * TDQ_MAXO)
+__host__ __device__ inline int hi_vrow(const NetDims& d) {
+  return (((d.n_hidden + d.d_in) * HI_W + HI_W * TDQ_MAXO + TDQ_MAXO) + 3) & ~3;
+}
+struct HiChainShared {
+  HiShared m;
+  float vred[HI_TG][HI_VSLOTS][HI_W];  // per point group, before the fixed-order sum
+};
+
+// fixed-order sum over the point groups of layer i's vector partials -> the workgroup's vslab row
+// (thread (f, group g) takes slots g, g + HI_TG, ...)
+__device__ __forceinline__ void hi_vsum(const HiChainShared& csh, float* __restrict__ vrow, const NetDims& d, int i,
+                                        int g, int f) {
+  const int Lh = d.n_hidden;
+  for (int sl = g; sl < HI_VSLOTS; sl += HI_TG) {
+    const bool use = sl == 0 || (i == 0 && sl <= d.d_in) ||
+                     (i == Lh - 1 && sl > TDQ_MAXD && (sl - 1 - TDQ_MAXD) % TDQ_MAXO < d.d_out);
+    if (!use) continue;
+    float a = csh.vred[0][sl][f];
+#pragma unroll
+    for (int gg = 1; gg < HI_TG; ++gg) a += csh.vred[gg][sl][f];
+    if (sl == 0) {
+      vrow[i * HI_W + f] = a;
+    } else if (sl <= TDQ_MAXD) {
+      vrow[(Lh + sl - 1) * HI_W + f] = a;
+    } else if (sl <= TDQ_MAXD + TDQ_MAXO) {
+      vrow[(Lh + d.d_in) * HI_W + f * TDQ_MAXO + (sl - 1 - TDQ_MAXD)] = a;
+    } else if (f == 0) {
+      vrow[(Lh + d.d_in) * HI_W + HI_W * TDQ_MAXO + (sl - 1 - TDQ_MAXD - TDQ_MAXO)] = a;
+    }
+  }
+}
+
 // adjoint chain: hb of the last hidden layer from dJ, then zb_i = tanh-jet adjoint, hb_{i-1} = W_i zb_i;
-// zb_i -> Bb (the weight gradients are jet_hi_wgrad_kernel's)
+// zb_i -> Bb (the hidden-to-hidden kernels' gradients are jet_hi_wgrad_kernel's); the vector
+// parameters' gradients are summed over the workgroup's points here -> vslab row blockIdx.x
 template <int S, bool CH>
 __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) jet_hi_chain_kernel(int N, const float* __restrict__ P, NetDims d,
-                                                                  HiSpec sp, const float* __restrict__ dJ, int ldJ,
+                                                                  HiSpec sp, const float* __restrict__ X,
+                                                                  const float* __restrict__ dJ, int ldJ,
                                                                   int j0, const float* __restrict__ Zb,
-                                                                  float* __restrict__ Bb) {
+                                                                  float* __restrict__ Bb, float* __restrict__ vslab) {
   extern __shared__ __attribute__((aligned(16))) char hi_lds[];
-  HiShared& sh = *reinterpret_cast<HiShared*>(hi_lds);
+  HiChainShared& csh = *reinterpret_cast<HiChainShared*>(hi_lds);
+  HiShared& sh = csh.m;
   const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
   const int Lh = d.n_hidden, dout = d.d_out;
   int n[HI_PT];
@@ -472,9 +515,13 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
   }
   HiWRegs wr;
   if (Lh > 1) hi_get_w(wr, P, d, Lh - 1);
-  const int wl = hw(d, Lh - 1);
+  const int wl = hw(d, Lh - 1), din = d.d_in;
   const float* Ko = P + off_layer(d, Lh);
+  float* vrow = vslab + (size_t)blockIdx.x * hi_vrow(d);
   float hb[HI_PT][S], z[HI_PT][S];
+  float vo[TDQ_MAXO], vbo[TDQ_MAXO];  // Ko / bo partials of this thread's point(s)
+#pragma unroll
+  for (int q = 0; q < TDQ_MAXO; ++q) vo[q] = vbo[q] = 0.f;
   {
     float ko[TDQ_MAXO];
 #pragma unroll
@@ -492,6 +539,23 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         hb[j][s] = a;
         z[j][s] = ldm(Zb + hi_row(Lh - 1, n[j], s, S, N) + f, f < wl);
       }
+    // Ko[f][q] = sum over points and seeded streams of h_s[f] dJ_s[q]; bo[q] = sum of dJ_value[q]
+#pragma unroll
+    for (int j = 0; j < HI_PT; ++j) {
+      float h[S];
+      hi_tanh_f<S, CH>(sp, z[j], h);
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
+          const float u = ldm(dJ + ((size_t)orow * ldJ + j0 + n[j]) * dout + (q < dout ? q : 0),
+                              sp.out[s] >= 0 && ok[j] && q < dout);
+          vo[q] = fmaf(f < wl ? h[s] : 0.f, u, vo[q]);
+          if (s == 0) vbo[q] += u;
+        }
+      }
+    }
   }
   for (int i = Lh - 1; i >= 0; --i) {
     const int wi = hw(d, i);
@@ -510,11 +574,36 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       }
 #pragma unroll
       for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = zb[s];
+      // vector-parameter partials of this point (padding points: zero adjoints already)
+      float vb = ok[j] ? zb[0] : 0.f;
+      csh.vred[pg][0][f] = (j == 0 ? 0.f : csh.vred[pg][0][f]) + vb;
+      if (i == 0) {
+#pragma unroll
+        for (int v = 0; v < TDQ_MAXD; ++v) {
+          float g = ldm(X + (size_t)n[j] * din + (v < din ? v : din - 1), v < din) * zb[0];
+#pragma unroll
+          for (int s = 1; s < S; ++s) g += (sp.order[s] == 1 && sp.var[s] == v) ? zb[s] : 0.f;
+          g = ok[j] ? g : 0.f;
+          csh.vred[pg][1 + v][f] = (j == 0 ? 0.f : csh.vred[pg][1 + v][f]) + g;
+        }
+      }
     }
-    if (i == 0) break;
+    if (i == Lh - 1) {
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) {
+        csh.vred[pg][1 + TDQ_MAXD + q][f] = vo[q];
+        csh.vred[pg][1 + TDQ_MAXD + TDQ_MAXO + q][f] = vbo[q];
+      }
+    }
+    if (i == 0) {
+      __syncthreads();
+      hi_vsum(csh, vrow, d, i, pg, f);
+      break;
+    }
     // hb_{i-1}[k = f] = sum_o zb_i[o] W_i[f][o]; the next layer's pre-activations load meanwhile
     hi_put_w(sh, wr);
     __syncthreads();
+    hi_vsum(csh, vrow, d, i, pg, f);
     if (i >= 2) hi_get_w(wr, P, d, i - 1);
     const int wp = hw(d, i - 1);
 #pragma unroll
@@ -554,207 +643,120 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 }
 
 // Weight gradients over the point range of split blockIdx.y (one slab row per split, reduced in
-// a fixed order afterwards): dK_i = H_{i-1}^T B_i of the hidden-to-hidden layers on 32 x 32 tiles
-// (rows = point x stream, 64 at a time through LDS, the next 64 loading meanwhile).
+// a fixed order afterwards): dK_i = H_{i-1}^T B_i of the hidden-to-hidden layers on 32 x 32 tiles.
+// Rows (point x stream) are staged HI_RB at a time through LDS with all loads of a batch in flight
+// at once (a split of the AC-baseline set is one batch: one memory latency per workgroup).
 #define HI_TILE 32
-#define HI_CHUNK 64
+#define HI_RB 256
 __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims d, const float* __restrict__ Hb,
                                                            const float* __restrict__ Bb, float* __restrict__ slab,
                                                            int Pst) {
-  __shared__ __attribute__((aligned(16))) float Hc[HI_CHUNK][HI_TILE];
-  __shared__ __attribute__((aligned(16))) float Gc[HI_CHUNK][HI_TILE];
+  __shared__ __attribute__((aligned(16))) float Hc[HI_RB][HI_TILE];
+  __shared__ __attribute__((aligned(16))) float Gc[HI_RB][HI_TILE];
   const int t = threadIdx.x;
   const int ks = gridDim.y, y = blockIdx.y;
   const int n0 = (int)((long long)N * y / ks), n1 = (int)((long long)N * (y + 1) / ks);
   float* row = slab + (size_t)y * Pst;
   constexpr int TPL = (HI_W / HI_TILE) * (HI_W / HI_TILE);
-  const int bx = (int)blockIdx.x;
-  {
-    const int i = 1 + bx / TPL, tile = bx % TPL;
-    const int kt = tile / (HI_W / HI_TILE), ft = tile % (HI_W / HI_TILE);
-    const int win = hw(d, i - 1), wout = hw(d, i);
-    if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
-    const int tk = t >> 4, tf = t & 15;
-    float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    const int r0 = n0 * S, r1 = n1 * S;
-    const float* Hl = Hb + hi_row(i - 1, 0, 0, S, N) + kt * HI_TILE;
-    const float* Bl = Bb + hi_row(i, 0, 0, S, N) + ft * HI_TILE;
-    f32x4 hv[2], gv[2];
-    auto load = [&](int r) {
+  const int i = 1 + (int)blockIdx.x / TPL, tile = (int)blockIdx.x % TPL;
+  const int kt = tile / (HI_W / HI_TILE), ft = tile % (HI_W / HI_TILE);
+  const int win = hw(d, i - 1), wout = hw(d, i);
+  if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
+  const int tk = t >> 4, tf = t & 15;
+  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  const int r0 = n0 * S, r1 = n1 * S;
+  const float* Hl = Hb + hi_row(i - 1, 0, 0, S, N) + kt * HI_TILE;
+  const float* Bl = Bb + hi_row(i, 0, 0, S, N) + ft * HI_TILE;
+  constexpr int NQ = HI_RB * HI_TILE / 4 / 256;  // float4 pieces per thread per operand
+  for (int r = r0; r < r1; r += HI_RB) {
+    f32x4 hv[NQ], gv[NQ];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {  // 64 rows x 32 columns = 512 float4 per operand
-        const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
-        hv[u] = gv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (r + rr < r1) {
-          hv[u] = *reinterpret_cast<const f32x4*>(Hl + (size_t)(r + rr) * HI_W + c);
-          gv[u] = *reinterpret_cast<const f32x4*>(Bl + (size_t)(r + rr) * HI_W + c);
-        }
-      }
-    };
-    load(r0);
-    for (int r = r0; r < r1; r += HI_CHUNK) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
-        *reinterpret_cast<f32x4*>(&Hc[rr][c]) = hv[u];
-        *reinterpret_cast<f32x4*>(&Gc[rr][c]) = gv[u];
-      }
-      __syncthreads();
-      if (r + HI_CHUNK < r1) load(r + HI_CHUNK);
-      for (int rb = 0; rb < HI_CHUNK; rb += 8) {  // 16 LDS reads in flight, then 32 FMAs
-        float2 h2[8], g2[8];
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
-          h2[rr] = *reinterpret_cast<const float2*>(&Hc[rb + rr][2 * tk]);
-          g2[rr] = *reinterpret_cast<const float2*>(&Gc[rb + rr][2 * tf]);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
-          acc[0][0] = fmaf(h2[rr].x, g2[rr].x, acc[0][0]);
-          acc[0][1] = fmaf(h2[rr].x, g2[rr].y, acc[0][1]);
-          acc[1][0] = fmaf(h2[rr].y, g2[rr].x, acc[1][0]);
-          acc[1][1] = fmaf(h2[rr].y, g2[rr].y, acc[1][1]);
-        }
-      }
-      __syncthreads();
+    for (int u = 0; u < NQ; ++u) {  // every load of the batch first (clamped rows, masked after)
+      const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
+      const int rc = r + rr < r1 ? r + rr : r1 - 1;
+      hv[u] = *reinterpret_cast<const f32x4*>(Hl + (size_t)rc * HI_W + c);
+      gv[u] = *reinterpret_cast<const f32x4*>(Bl + (size_t)rc * HI_W + c);
     }
-    float* dk = row + off_layer(d, i);
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int u = 0; u < NQ; ++u) {
+      const int e = t + 256 * u, rr = e >> 3, c = (e & 7) * 4;
+      const bool in = r + rr < r1;
+      *reinterpret_cast<f32x4*>(&Hc[rr][c]) = in ? hv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(&Gc[rr][c]) = in ? gv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+    const int nb = (min(HI_RB, r1 - r) + 7) & ~7;
+    for (int rb = 0; rb < nb; rb += 8) {  // 16 LDS reads in flight, then 32 FMAs
+      float2 h2[8], g2[8];
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int k = kt * HI_TILE + 2 * tk + a, f = ft * HI_TILE + 2 * tf + b;
-        if (k < win && f < wout) dk[k * wout + f] = acc[a][b];
+      for (int rr = 0; rr < 8; ++rr) {
+        h2[rr] = *reinterpret_cast<const float2*>(&Hc[rb + rr][2 * tk]);
+        g2[rr] = *reinterpret_cast<const float2*>(&Gc[rb + rr][2 * tf]);
       }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        acc[0][0] = fmaf(h2[rr].x, g2[rr].x, acc[0][0]);
+        acc[0][1] = fmaf(h2[rr].x, g2[rr].y, acc[0][1]);
+        acc[1][0] = fmaf(h2[rr].y, g2[rr].x, acc[1][0]);
+        acc[1][1] = fmaf(h2[rr].y, g2[rr].y, acc[1][1]);
+      }
+    }
+    __syncthreads();
   }
+  float* dk = row + off_layer(d, i);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int k = kt * HI_TILE + 2 * tk + a, f = ft * HI_TILE + 2 * tf + b;
+      if (k < win && f < wout) dk[k * wout + f] = acc[a][b];
+    }
 }
 
-// per-layer vectors of the split blockIdx.y's points, workgroup e = blockIdx.x per hidden layer:
-// bias of hidden layer e, plus K0 (e = 0) and the output layer's Ko, bo (e = n_hidden - 1).
-// Thread (f, g): feature f, point group g of HI_VG; every load unconditional from a clamped
-// address, weighted 0 / 1, so a round of U points is one batch of independent loads.
-#define HI_VG 4
-#define HI_VSLOTS (1 + TDQ_MAXD + 2 * TDQ_MAXO)
-template <int S>
-__global__ void __launch_bounds__(HI_W * HI_VG) jet_hi_wvec_kernel(const float* __restrict__ X, int N, NetDims d,
-                                                                   HiSpec sp, const float* __restrict__ dJ, int ldJ,
-                                                                   int j0, const float* __restrict__ Hb,
-                                                                   const float* __restrict__ Bb,
-                                                                   float* __restrict__ slab, int Pst) {
-  __shared__ float red[HI_VG][HI_VSLOTS][HI_W];
-  const int t = threadIdx.x, Lh = d.n_hidden, dout = d.d_out;
-  const int ks = gridDim.y, y = blockIdx.y;
-  const int n0 = (int)((long long)N * y / ks), n1 = (int)((long long)N * (y + 1) / ks);
-  float* row = slab + (size_t)y * Pst;
-  const int e = blockIdx.x, f = t & (HI_W - 1), g = t >> 7;
-  const int we = hw(d, e), din = d.d_in;
-  const int na = n0 + (int)((long long)(n1 - n0) * g / HI_VG), nb = n0 + (int)((long long)(n1 - n0) * (g + 1) / HI_VG);
-  const bool first = e == 0, last = e == Lh - 1;
-  const int fc = f < we ? f : 0;
-  float ab = 0.f, ak[TDQ_MAXD], ao[TDQ_MAXO], abo[TDQ_MAXO];
-#pragma unroll
-  for (int v = 0; v < TDQ_MAXD; ++v) ak[v] = 0.f;
-#pragma unroll
-  for (int q = 0; q < TDQ_MAXO; ++q) ao[q] = abo[q] = 0.f;
-  constexpr int U = S <= 4 ? 8 : 4;  // points per round (register budget)
-  for (int m0 = na; m0 < nb; m0 += U) {
-    float zb[U][S], w[U];
-    int mc[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      w[u] = m0 + u < nb ? 1.f : 0.f;
-      mc[u] = m0 + u < nb ? m0 + u : (na < N ? na : 0);
-    }
-    if (first) {  // uniform branch around a whole batch
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int s = 0; s < S; ++s) zb[u][s] = Bb[hi_row(e, mc[u], s, S, N) + fc];
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        zb[u][0] = Bb[hi_row(e, mc[u], 0, S, N) + fc];
-#pragma unroll
-        for (int s = 1; s < S; ++s) zb[u][s] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) ab = fmaf(w[u], zb[u][0], ab);
-    if (first) {  // K0[v][f]: x_v * zb_value + the first-order streams of variable v
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int v = 0; v < TDQ_MAXD; ++v) {
-          float gv = ldm(X + (size_t)mc[u] * din + (v < din ? v : din - 1), v < din) * zb[u][0];
-#pragma unroll
-          for (int s = 1; s < S; ++s) gv += (sp.order[s] == 1 && sp.var[s] == v) ? zb[u][s] : 0.f;
-          ak[v] = fmaf(w[u], gv, ak[v]);
-        }
-    }
-    if (last) {  // Ko[f][q]: sum over the seeded streams of h_s[f] * dJ_s[q]; bo[q]: sum of dJ_value
-      float hv[U][S];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int s = 0; s < S; ++s) hv[u][s] = w[u] * ldm(Hb + hi_row(e, mc[u], s, S, N) + fc, sp.out[s] >= 0);
-#pragma unroll
-      for (int q = 0; q < TDQ_MAXO; ++q) {
-        if (q >= dout) break;
-        float uv[U][S];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
-            uv[u][s] = dJ[((size_t)orow * ldJ + j0 + mc[u]) * dout + q];
-          }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (sp.out[0] >= 0) abo[q] = fmaf(w[u], uv[u][0], abo[q]);
-#pragma unroll
-          for (int s = 0; s < S; ++s) ao[q] = fmaf(hv[u][s], uv[u][s], ao[q]);
-        }
-      }
-    }
-  }
-  red[g][0][f] = ab;
-#pragma unroll
-  for (int v = 0; v < TDQ_MAXD; ++v) red[g][1 + v][f] = ak[v];
-#pragma unroll
-  for (int q = 0; q < TDQ_MAXO; ++q) {
-    red[g][1 + TDQ_MAXD + q][f] = ao[q];
-    red[g][1 + TDQ_MAXD + TDQ_MAXO + q][f] = abo[q];
-  }
-  __syncthreads();
-  // fixed-order sums over the point groups: thread (f, slot g) of the first HI_VSLOTS / ... slots
-  for (int sl = g; sl < HI_VSLOTS; sl += HI_VG) {
-    float a = 0.f;
-#pragma unroll
-    for (int gg = 0; gg < HI_VG; ++gg) a += red[gg][sl][f];
-    if (f >= we) continue;
-    if (sl == 0) {
-      const int pin = e == 0 ? din : hw(d, e - 1);
-      row[off_layer(d, e) + pin * we + f] = a;  // bias of hidden layer e
-    } else if (sl <= TDQ_MAXD) {
-      if (first && sl - 1 < din) row[(sl - 1) * we + f] = a;
-    } else if (sl <= TDQ_MAXD + TDQ_MAXO) {
-      const int q = sl - 1 - TDQ_MAXD;
-      if (last && q < dout) row[off_layer(d, Lh) + f * dout + q] = a;
-    } else {
-      const int q = sl - 1 - TDQ_MAXD - TDQ_MAXO;
-      if (last && q < dout && f == 0) row[off_layer(d, Lh) + hw(d, Lh - 1) * dout + q] = a;
-    }
-  }
-}
-
-// rows [0, nrows) of the slab -> grad (fixed order: deterministic)
-__global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restrict__ slab, int nrows, int Pst, int Ptot,
-                                                            float* __restrict__ grad) {
+// gradient = fixed-order sums: the hidden-to-hidden kernels over the ks split rows of the tile
+// slab, every other parameter over the nwg workgroup rows of the chain's vslab (deterministic)
+__global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restrict__ slab, int ks, int Pst,
+                                                            const float* __restrict__ vslab, int nwg, int Vst,
+                                                            NetDims d, int Ptot, float* __restrict__ grad) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= Ptot) return;
-  float a = 0.f;
-  for (int r = 0; r < nrows; ++r) a += slab[(size_t)r * Pst + e];
-  grad[e] = a;
+  const int Lh = d.n_hidden;
+  int layer = Lh;
+  for (int i = 1; i <= Lh; ++i)
+    if (e < off_layer(d, i)) {
+      layer = i - 1;
+      break;
+    }
+  const int r = e - off_layer(d, layer);
+  int vi = -1;  // vslab column, or -1: tile slab
+  if (layer < Lh) {
+    const int win = layer == 0 ? d.d_in : hw(d, layer - 1), wout = hw(d, layer);
+    if (r >= win * wout)
+      vi = layer * HI_W + (r - win * wout);                    // bias
+    else if (layer == 0)
+      vi = (Lh + r / wout) * HI_W + r % wout;                  // K0
+  } else {
+    const int wl = hw(d, Lh - 1), dout = d.d_out;
+    vi = r < wl * dout ? (Lh + d.d_in) * HI_W + (r / dout) * TDQ_MAXO + r % dout   // Ko
+                       : (Lh + d.d_in) * HI_W + HI_W * TDQ_MAXO + (r - wl * dout);  // bo
+  }
+  float a0 = 0.f, a1 = 0.f;
+  if (vi < 0) {
+    int q = 0;
+    for (; q + 1 < ks; q += 2) {
+      a0 += slab[(size_t)q * Pst + e];
+      a1 += slab[(size_t)(q + 1) * Pst + e];
+    }
+    if (q < ks) a0 += slab[(size_t)q * Pst + e];
+  } else {
+    int q = 0;
+    for (; q + 1 < nwg; q += 2) {
+      a0 += vslab[(size_t)q * Vst + vi];
+      a1 += vslab[(size_t)(q + 1) * Vst + vi];
+    }
+    if (q < nwg) a0 += vslab[(size_t)q * Vst + vi];
+  }
+  grad[e] = a0 + a1;
 }
 
 namespace {
@@ -810,9 +812,9 @@ bool hi_dims(NetDims& d, int d_in, const int* widths, int d_out, int n_hidden) {
 }
 
 template <typename K>
-void hi_attr(K* kern) {
+void hi_attr(K* kern, size_t bytes = sizeof(HiShared)) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(HiShared));
+                            (int)bytes);
 }
 
 int hi_splits(int N) { return std::min(HI_KS, std::max(1, (N + 63) / 64)); }
@@ -832,15 +834,15 @@ int hi_launch_fwd(const float* X, int N, const float* P, const NetDims& d, const
 }
 
 template <int S, bool CH>
-int hi_launch_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const float* dJ, int ldJ, int j0,
-                    const float* Zb, float* Bb, hipStream_t st) {
+int hi_launch_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const float* X, const float* dJ,
+                    int ldJ, int j0, const float* Zb, float* Bb, float* vslab, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hi_attr(&jet_hi_chain_kernel<S, CH>);
+    hi_attr(&jet_hi_chain_kernel<S, CH>, sizeof(HiChainShared));
     attr = true;
   }
-  hipLaunchKernelGGL((jet_hi_chain_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS), sizeof(HiShared),
-                     st, N, P, d, sp, dJ, ldJ, j0, Zb, Bb);
+  hipLaunchKernelGGL((jet_hi_chain_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS),
+                     sizeof(HiChainShared), st, N, P, d, sp, X, dJ, ldJ, j0, Zb, Bb, vslab);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -860,33 +862,24 @@ int hi_fwd(const float* X, int N, const float* P, const NetDims& d, const HiSpec
   return (int)hipErrorInvalidValue;
 }
 
-int hi_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const float* dJ, int ldJ, int j0,
-             const float* Zb, float* Bb, hipStream_t st) {
+int hi_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, const float* X, const float* dJ, int ldJ,
+             int j0, const float* Zb, float* Bb, float* vslab, hipStream_t st) {
   const bool ch = sp.chain != 0;
 #define HI_B(SS, CC) \
-  if (sp.S == SS && ch == CC) return hi_launch_chain<SS, CC>(N, P, d, sp, dJ, ldJ, j0, Zb, Bb, st);
+  if (sp.S == SS && ch == CC) return hi_launch_chain<SS, CC>(N, P, d, sp, X, dJ, ldJ, j0, Zb, Bb, vslab, st);
   HI_CASES(HI_B)
 #undef HI_B
   return (int)hipErrorInvalidValue;
 }
 
-int hi_wgrad(const float* X, int N, const NetDims& d, const HiSpec& sp, const float* dJ, int ldJ, int j0,
-             const float* Hb, const float* Bb, float* work, int Pst, int ks, hipStream_t st) {
+int hi_wgrad(int N, const NetDims& d, const HiSpec& sp, const float* Hb, const float* Bb, float* work, int Pst,
+             int ks, hipStream_t st) {
   const int n_tiles = (d.n_hidden - 1) * (HI_W / HI_TILE) * (HI_W / HI_TILE);
   if (n_tiles > 0) {
     hipLaunchKernelGGL(jet_hi_wgrad_kernel, dim3(n_tiles, ks), dim3(256), 0, st, N, sp.S, d, Hb, Bb, work, Pst);
     TDQ_CHECK_LAUNCH();
   }
-#define HI_G(SS)                                                                                              \
-  if (sp.S == SS) {                                                                                           \
-    hipLaunchKernelGGL(jet_hi_wvec_kernel<SS>, dim3(d.n_hidden, ks), dim3(HI_W * HI_VG), 0, st, X, N, d, sp, dJ, \
-                       ldJ, j0, Hb, Bb, work, Pst);                                                           \
-    TDQ_CHECK_LAUNCH();                                                                                       \
-    return 0;                                                                                                 \
-  }
-  HI_G(2) HI_G(3) HI_G(4) HI_G(5) HI_G(6) HI_G(7) HI_G(8)
-#undef HI_G
-  return (int)hipErrorInvalidValue;
+  return 0;
 }
 
 // one activation-sized scratch buffer (Z, H or B), in floats
@@ -899,11 +892,12 @@ extern "C" {
 // Z | H | B: pre-activations, post-activations and pre-activation adjoints of every hidden layer
 int64_t tdq_jet_hi_scratch_floats(int N, int n_hidden) { return 3 * (int64_t)hi_act_floats(N, n_hidden); }
 
-// slab rows of the weight-gradient pass, in floats
+// tile slab (split rows) + the chain's vector slab (workgroup rows), in floats
 int64_t tdq_jet_hi_work_floats(int N, int d_in, const int* widths, int d_out, int n_hidden) {
   NetDims d;
   if (!hi_dims(d, d_in, widths, d_out, n_hidden)) return -1;
-  return (int64_t)hi_splits(N) * slab_stride(param_count(d));
+  const int nwg = (N + HI_NP - 1) / HI_NP;
+  return (int64_t)hi_splits(N) * slab_stride(param_count(d)) + (int64_t)nwg * hi_vrow(d);
 }
 
 // forward over N points X[N][d_in]: stream s with out[s] >= 0 -> J[(out[s] * ldJ + j0 + n) * d_out + q];
@@ -931,12 +925,14 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   const int Ptot = param_count(d), Pst = slab_stride(Ptot);
   if (N <= 0) return (int)hipMemsetAsync(grad, 0, sizeof(float) * Ptot, st);
   const size_t A = hi_act_floats(N, n_hidden);
-  int rc = hi_chain(N, P, d, sp, dJ, ldJ, j0, Z, Z + 2 * A, st);
+  const int ks = hi_splits(N), nwg = (N + HI_NP - 1) / HI_NP;
+  float* vslab = work + (size_t)ks * Pst;
+  int rc = hi_chain(N, P, d, sp, X, dJ, ldJ, j0, Z, Z + 2 * A, vslab, st);
   if (rc) return rc;
-  const int ks = hi_splits(N);
-  rc = hi_wgrad(X, N, d, sp, dJ, ldJ, j0, Z + A, Z + 2 * A, work, Pst, ks, st);
+  rc = hi_wgrad(N, d, sp, Z + A, Z + 2 * A, work, Pst, ks, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((Ptot + 255) / 256), dim3(256), 0, st, work, ks, Pst, Ptot, grad);
+  hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((Ptot + 255) / 256), dim3(256), 0, st, work, ks, Pst, vslab, nwg,
+                     hi_vrow(d), d, Ptot, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -6,6 +6,15 @@ cd $R
 export PYTHONPATH=$R
 O=gpurun_out/${TDQ_RUN:-r4m}
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_jet_hi.py -m gpu -v -s --timeout 240 --timeout-method thread > $O/pytest_hi.log 2>&1
+rc=$?
+grep -E "HI time|HI ac|HI grad|passed|failed|FAILED|Error" $O/pytest_hi.log | head -20
+if [ $rc -ne 0 ]; then tail -30 $O/pytest_hi.log; exit $rc; fi
+timeout -k 10 120 python tools/hi_bench.py > $O/hi_bench.json 2> $O/hi_bench.err || { tail -20 $O/hi_bench.err; exit 1; }
+cat $O/hi_bench.json
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/prof_hi -o run --output-format csv -- python3 $R/tools/hi_bench.py > $R/$O/prof_hi.log 2>&1) || { tail -20 $O/prof_hi.log; exit 1; }
+python tools/kernel_stats.py $O/prof_hi/run_kernel_stats.csv --steps 400 > $O/kernel_stats_hi.txt 2>&1
+head -6 $O/kernel_stats_hi.txt | cut -c1-150
 timeout -k 10 300 python -u -m pytest tests/test_hip_kernels.py -m gpu -v -s -k "wide256" --timeout 240 --timeout-method thread > $O/pytest_w256.log 2>&1
 rc=$?
 grep -E "KERNEL_ERR|passed|failed|FAILED|Error" $O/pytest_w256.log | head -30
