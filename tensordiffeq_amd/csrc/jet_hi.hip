@@ -205,13 +205,34 @@ __device__ __forceinline__ void hi_tanh_b(const HiSpec& sp, const float (&z)[S],
     table_b<S>(sp, z, hb, zb);
 }
 
-// LDS of the chain kernels: one layer's weights (row stride 132: the forward reads W[k][f] along f,
-// the backward float4 rows W[f][o..o+3], both conflict-free) + the workgroup's activations /
-// adjoints (read as float4 broadcasts: every lane of a 128-thread group reads the same point)
-struct HiShared {
-  float W[HI_W][HI_WS];
-  float A[HI_NP][HI_MAXS][HI_AS];
+// LDS of the forward / adjoint-chain kernels (floats, dynamic, sized per launch):
+//   W [HI_W][HI_WS]          one layer's weights (row stride 132: float4 rows W[k][4 f4..] and
+//                            W[k][o..o+3] of the k-split GEMMs are conflict-free)
+//   A [HI_NP][S][HI_AS]      the workgroup's activations / adjoints (float4 broadcasts)
+//   R [HI_NP][S][4][HI_AS]   k-split GEMM partials: four k-quarters per output, summed in order
+//   V [HI_TG][nvs][HI_W]     (chain) vector-parameter partials, nvs = 1 + d_in + 2 d_out
+struct HiLds {
+  float* W;
+  float* A;
+  float* R;
+  float* V;
+  int S;
+  __device__ float& w(int k, int f) const { return W[k * HI_WS + f]; }
+  __device__ float& a(int p, int s, int k) const { return A[(p * S + s) * HI_AS + k]; }
+  __device__ float& r(int p, int s, int q, int f) const { return R[((p * S + s) * 4 + q) * HI_AS + f]; }
 };
+__host__ __device__ inline size_t hi_lds_floats(int S, int nvs) {
+  return (size_t)HI_W * HI_WS + (size_t)HI_NP * S * HI_AS * 5 + (size_t)HI_TG * nvs * HI_W;
+}
+__device__ inline HiLds hi_lds_map(float* base, int S) {
+  HiLds L;
+  L.S = S;
+  L.W = base;
+  L.A = L.W + HI_W * HI_WS;
+  L.R = L.A + HI_NP * S * HI_AS;
+  L.V = L.R + HI_NP * S * 4 * HI_AS;
+  return L;
+}
 
 // Diagnostic build only (tools/hi_stamps.cpp, -DHI_STAMPS): s_memtime at phase boundaries of
 // workgroup 0, printed at the end; compiled out otherwise.
@@ -240,7 +261,7 @@ __device__ __forceinline__ float ldm(const float* p, bool keep) {
 }
 
 // W (in x out) of dense layer `layer`, zero-padded to HI_W x HI_W, as float4 pieces in registers:
-// piece u of thread t = row (t + 256 u) >> 5, columns 4 ((t + 256 u) & 31) + [0, 4).  All loads of a
+// piece u of thread t = row (t + HI_THREADS u) >> 5, columns 4 ((t + HI_THREADS u) & 31) + [0, 4).  All loads of a
 // layer are issued back to back (one memory latency per layer, not one per element) and overlap
 // the previous layer's GEMM; hi_put_w writes them to LDS after that GEMM's barrier.
 constexpr int HI_WQ = HI_W * HI_W / 4 / HI_THREADS;
@@ -278,11 +299,11 @@ __device__ __forceinline__ void hi_get_w(HiWRegs& r, const float* __restrict__ P
     }
   }
 }
-__device__ __forceinline__ void hi_put_w(HiShared& sh, const HiWRegs& r) {
+__device__ __forceinline__ void hi_put_w(const HiLds& L, const HiWRegs& r) {
 #pragma unroll
   for (int u = 0; u < HI_WQ; ++u) {
     const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
-    *reinterpret_cast<f32x4*>(&sh.W[k][c]) = r.q[u];
+    *reinterpret_cast<f32x4*>(&L.w(k, c)) = r.q[u];
   }
 }
 
@@ -292,148 +313,128 @@ __device__ __forceinline__ size_t hi_row(int layer, int n, int s, int S, int N) 
   return (((size_t)layer * N + n) * S + s) * HI_W;
 }
 
-// thread (f, pg): feature f of points 2 pg, 2 pg + 1 of the workgroup's HI_NP
-// one workgroup per CU (the LDS), two waves per SIMD (full VALU issue rate, 256 registers each)
+// k-split GEMM step of thread (p, f4, ks): out[s][c] (c < 4) += sum over its k of in[p][s][k] *
+// W[k][4 f4 + c] - the k of quarter ks are 16 j + 4 ks + [0, 4) (interleaved: the float4 W rows
+// of one lane group then fall on 16 distinct bank quads)
+template <int S>
+__device__ __forceinline__ void hi_gemm_fwd(const HiLds& L, int p, int f4, int ks, int kin, f32x4 (&acc)[S]) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nj = (kin + 15) >> 4;
+#pragma unroll 2
+  for (int j = 0; j < nj; ++j) {
+    const int k0 = 16 * j + 4 * ks;
+    f32x4 a[S], w[4];
+#pragma unroll
+    for (int s = 0; s < S; ++s) a[s] = *reinterpret_cast<const f32x4*>(&L.a(p, s, k0));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = *reinterpret_cast<const f32x4*>(&L.w(k0 + c, 4 * f4));
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) acc[s][x] = fmaf(a[s][c], w[c][x], acc[s][x]);
+  }
+}
+
+// thread t: point p = t >> 7 and feature f = t & 127 in the elementwise phases; in the GEMM, feature
+// quad f4 = (t >> 2) & 31 and k-quarter ks = t & 3 (so f = 4 f4 + ks)
 template <int S, bool CH>
 __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) jet_hi_fwd_kernel(const float* __restrict__ X, int N,
                                                                 const float* __restrict__ P, NetDims d, HiSpec sp,
                                                                 float* __restrict__ J, int ldJ, int j0,
                                                                 float* __restrict__ Zb, float* __restrict__ Hb) {
-  extern __shared__ __attribute__((aligned(16))) char hi_lds[];
-  HiShared& sh = *reinterpret_cast<HiShared*>(hi_lds);
+  extern __shared__ __attribute__((aligned(16))) float hi_lds[];
+  const HiLds L = hi_lds_map(hi_lds, S);
   HI_TS_DECL
   HI_TS()
-  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
+  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7, f4 = (t >> 2) & 31, ks = t & 3;
   const int Lh = d.n_hidden;
-  int n[HI_PT];
-  bool ok[HI_PT];
-#pragma unroll
-  for (int j = 0; j < HI_PT; ++j) {
-    const int m = blockIdx.x * HI_NP + pg * HI_PT + j;
-    ok[j] = m < N;
-    n[j] = ok[j] ? m : N - 1;
-  }
+  const int m0 = blockIdx.x * HI_NP + pg;
+  const bool ok = m0 < N;
+  const int n = ok ? m0 : N - 1;
   HiWRegs wr;
   if (Lh > 1) hi_get_w(wr, P, d, 1);
-  float z[HI_PT][S];
+  float z[S];
   {  // layer 0: z = x K0 + b0 (value), K0[var] (first order), 0 (higher)
     const int w0 = hw(d, 0);
+    const int fc = f < w0 ? f : w0 - 1;
+    float xv[TDQ_MAXD], kv[TDQ_MAXD];
 #pragma unroll
-    for (int j = 0; j < HI_PT; ++j)
+    for (int v = 0; v < TDQ_MAXD; ++v) {
+      const int vc = v < d.d_in ? v : d.d_in - 1;
+      kv[v] = ldm(P + vc * w0 + fc, v < d.d_in && f < w0);
+      xv[v] = ldm(X + (size_t)n * d.d_in + vc, v < d.d_in);
+    }
+    float a = ldm(P + d.d_in * w0 + fc, f < w0);
 #pragma unroll
-      for (int s = 0; s < S; ++s) z[j][s] = 0.f;
-    {
-      const int fc = f < w0 ? f : w0 - 1;
-      float xv[HI_PT][TDQ_MAXD], kv[TDQ_MAXD];
+    for (int v = 0; v < TDQ_MAXD; ++v) a = fmaf(xv[v], kv[v], a);
+    z[0] = a;
 #pragma unroll
-      for (int v = 0; v < TDQ_MAXD; ++v) {
-        const int vc = v < d.d_in ? v : d.d_in - 1;
-        kv[v] = ldm(P + vc * w0 + fc, v < d.d_in && f < w0);
+    for (int s = 1; s < S; ++s) {
+      float k1 = 0.f;
 #pragma unroll
-        for (int j = 0; j < HI_PT; ++j) xv[j][v] = ldm(X + (size_t)n[j] * d.d_in + vc, v < d.d_in);
-      }
-      const float b0 = ldm(P + d.d_in * w0 + fc, f < w0);
-#pragma unroll
-      for (int j = 0; j < HI_PT; ++j) {
-        float a = b0;
-#pragma unroll
-        for (int v = 0; v < TDQ_MAXD; ++v) a = fmaf(xv[j][v], kv[v], a);
-        z[j][0] = a;
-#pragma unroll
-        for (int s = 1; s < S; ++s) {
-          float k1 = 0.f;
-#pragma unroll
-          for (int v = 0; v < TDQ_MAXD; ++v) k1 = sp.var[s] == v ? kv[v] : k1;
-          if (sp.order[s] == 1) z[j][s] = k1;
-        }
-      }
+      for (int v = 0; v < TDQ_MAXD; ++v) k1 = sp.var[s] == v ? kv[v] : k1;
+      z[s] = sp.order[s] == 1 ? k1 : 0.f;
     }
   }
-  if (Lh > 1) hi_put_w(sh, wr);
+  if (Lh > 1) hi_put_w(L, wr);
   HI_TS()
   for (int i = 0; i < Lh; ++i) {
     const int wi = hw(d, i);
-    if (i >= 1) {  // z_i = h_{i-1} W_i (+ b_i): h_{i-1} in sh.A, W_i in sh.W; W_{i+1} loads in flight
+    if (i >= 1) {  // z_i = h_{i-1} W_i (+ b_i); W_{i+1} loads in flight meanwhile
       if (i + 1 < Lh) hi_get_w(wr, P, d, i + 1);
       const float b = ldm(P + off_layer(d, i) + hw(d, i - 1) * wi + (f < wi ? f : wi - 1), f < wi);
-#pragma unroll
-      for (int j = 0; j < HI_PT; ++j)
-#pragma unroll
-        for (int s = 0; s < S; ++s) z[j][s] = 0.f;
-      // software-pipelined over groups of 4 k: the LDS reads of group k + 4 are in flight while
-      // group k's FMAs run (the scheduler alone reuses one register quad and waits after every read)
-      const int kin8 = (hw(d, i - 1) + 7) & ~7;  // sh.A / sh.W are zero past the layer's width
-      f32x4 a0[HI_PT][S], a1[HI_PT][S];
-      float w0[4], w1[4];
-      auto lda = [&](int k, f32x4(&a)[HI_PT][S], float(&w)[4]) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) w[x] = sh.W[k + x][f];
-#pragma unroll
-        for (int j = 0; j < HI_PT; ++j)
-#pragma unroll
-          for (int s = 0; s < S; ++s) a[j][s] = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][k]);
-      };
-      auto fma4 = [&](const f32x4(&a)[HI_PT][S], const float(&w)[4]) {
-#pragma unroll
-        for (int j = 0; j < HI_PT; ++j)
-#pragma unroll
-          for (int s = 0; s < S; ++s)
-            z[j][s] = fmaf(a[j][s][0], w[0], fmaf(a[j][s][1], w[1], fmaf(a[j][s][2], w[2], fmaf(a[j][s][3], w[3], z[j][s]))));
-      };
-      lda(0, a0, w0);
-      for (int k = 0; k < kin8; k += 8) {
-        lda(k + 4, a1, w1);
-        fma4(a0, w0);
-        if (k + 8 < kin8) lda(k + 8, a0, w0);
-        fma4(a1, w1);
-      }
-#pragma unroll
-      for (int j = 0; j < HI_PT; ++j) z[j][0] += b;
+      f32x4 acc[S];
+      hi_gemm_fwd<S>(L, pg, f4, ks, hw(d, i - 1), acc);
       HI_TS()
-      __syncthreads();  // every thread done reading sh.A / sh.W
-      if (i + 1 < Lh) hi_put_w(sh, wr);
+#pragma unroll
+      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&L.r(pg, s, ks, 4 * f4)) = acc[s];
+      __syncthreads();  // partials in R; every GEMM read of A / W done
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        z[s] = ((L.r(pg, s, 0, f) + L.r(pg, s, 1, f)) + (L.r(pg, s, 2, f) + L.r(pg, s, 3, f))) + (s == 0 ? b : 0.f);
+      if (i + 1 < Lh) hi_put_w(L, wr);
       HI_TS()
     }
-#pragma unroll
-    for (int j = 0; j < HI_PT; ++j) {
+    {
       float h[S];
       if (f < wi) {
-        hi_tanh_f<S, CH>(sp, z[j], h);
+        hi_tanh_f<S, CH>(sp, z, h);
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) h[s] = 0.f;
       }
-      if (ok[j]) {
+      if (ok) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          Zb[hi_row(i, n[j], s, S, N) + f] = z[j][s];
-          Hb[hi_row(i, n[j], s, S, N) + f] = h[s];
+          Zb[hi_row(i, n, s, S, N) + f] = z[s];
+          Hb[hi_row(i, n, s, S, N) + f] = h[s];
         }
       }
 #pragma unroll
-      for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = h[s];
+      for (int s = 0; s < S; ++s) L.a(pg, s, f) = h[s];
     }
     HI_TS()
-    __syncthreads();
+    __syncthreads();  // A (and W) of the next GEMM written; R read
     HI_TS()
   }
   // ---- output layer: u_s[q] = sum_f h_s[f] Ko[f][q] (+ bo[q] on the value stream): per-feature
   // products into LDS (the free weight area), then one thread per (point, stream, q) sums them
   const int wl = hw(d, Lh - 1), dout = d.d_out;
   const float* Ko = P + off_layer(d, Lh);
-  float* part = &sh.W[0][0];  // [p][s][q][HI_W]
+  float* part = L.W;  // [p][s][q][HI_W]
   {
     float ko[TDQ_MAXO];
 #pragma unroll
     for (int q = 0; q < TDQ_MAXO; ++q)
       ko[q] = ldm(Ko + (f < wl ? f : wl - 1) * dout + (q < dout ? q : dout - 1), q < dout && f < wl);
 #pragma unroll
-    for (int j = 0; j < HI_PT; ++j)
+    for (int s = 0; s < S; ++s)
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-#pragma unroll
-        for (int q = 0; q < TDQ_MAXO; ++q)
-          if (q < dout) part[(((pg * HI_PT + j) * S + s) * TDQ_MAXO + q) * HI_W + f] = sh.A[pg * HI_PT + j][s][f] * ko[q];
+      for (int q = 0; q < TDQ_MAXO; ++q)
+        if (q < dout) part[((pg * S + s) * TDQ_MAXO + q) * HI_W + f] = L.a(pg, s, f) * ko[q];
   }
   __syncthreads();
   for (int c = t; c < HI_NP * S * dout; c += blockDim.x) {
@@ -458,187 +459,181 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 //   [(Lh + v) * HI_W + f]                K0[v][f]
 //   [(Lh + d_in) * HI_W + f * MAXO + q]   Ko[f][q]
 //   [(Lh + d_in) * HI_W + HI_W * MAXO + q] bo[q]
-#define HI_VSLOTS (1 + TDQ_MAXD + 2 * TDQ_MAXO)
 __host__ __device__ inline int hi_vrow(const NetDims& d) {
   return (((d.n_hidden + d.d_in) * HI_W + HI_W * TDQ_MAXO + TDQ_MAXO) + 3) & ~3;
 }
-struct HiChainShared {
-  HiShared m;
-  float vred[HI_TG][HI_VSLOTS][HI_W];  // per point group, before the fixed-order sum
-};
+__host__ __device__ inline int hi_nvs(const NetDims& d) { return 1 + d.d_in + 2 * d.d_out; }
 
-// fixed-order sum over the point groups of layer i's vector partials -> the workgroup's vslab row
-// (thread (f, group g) takes slots g, g + HI_TG, ...)
-__device__ __forceinline__ void hi_vsum(const HiChainShared& csh, float* __restrict__ vrow, const NetDims& d, int i,
-                                        int g, int f) {
-  const int Lh = d.n_hidden;
-  for (int sl = g; sl < HI_VSLOTS; sl += HI_TG) {
-    const bool use = sl == 0 || (i == 0 && sl <= d.d_in) ||
-                     (i == Lh - 1 && sl > TDQ_MAXD && (sl - 1 - TDQ_MAXD) % TDQ_MAXO < d.d_out);
+// fixed-order sum over the point groups of layer i's vector partials (V slots: 0 bias, 1 .. d_in
+// K0, then d_out Ko and d_out bo) -> the workgroup's vslab row; thread (f, group g) takes slots
+// g, g + HI_TG, ...
+__device__ __forceinline__ void hi_vsum(const HiLds& L, float* __restrict__ vrow, const NetDims& d, int i, int g,
+                                        int f) {
+  const int Lh = d.n_hidden, din = d.d_in, dout = d.d_out, nvs = hi_nvs(d);
+  for (int sl = g; sl < nvs; sl += HI_TG) {
+    const bool use = sl == 0 || (i == 0 && sl <= din) || (i == Lh - 1 && sl > din);
     if (!use) continue;
-    float a = csh.vred[0][sl][f];
+    float a = L.V[sl * HI_W + f];
 #pragma unroll
-    for (int gg = 1; gg < HI_TG; ++gg) a += csh.vred[gg][sl][f];
+    for (int gg = 1; gg < HI_TG; ++gg) a += L.V[(gg * nvs + sl) * HI_W + f];
     if (sl == 0) {
       vrow[i * HI_W + f] = a;
-    } else if (sl <= TDQ_MAXD) {
+    } else if (sl <= din) {
       vrow[(Lh + sl - 1) * HI_W + f] = a;
-    } else if (sl <= TDQ_MAXD + TDQ_MAXO) {
-      vrow[(Lh + d.d_in) * HI_W + f * TDQ_MAXO + (sl - 1 - TDQ_MAXD)] = a;
+    } else if (sl <= din + dout) {
+      vrow[(Lh + din) * HI_W + f * TDQ_MAXO + (sl - 1 - din)] = a;
     } else if (f == 0) {
-      vrow[(Lh + d.d_in) * HI_W + HI_W * TDQ_MAXO + (sl - 1 - TDQ_MAXD - TDQ_MAXO)] = a;
+      vrow[(Lh + din) * HI_W + HI_W * TDQ_MAXO + (sl - 1 - din - dout)] = a;
     }
   }
 }
 
 // adjoint chain: hb of the last hidden layer from dJ, then zb_i = tanh-jet adjoint, hb_{i-1} = W_i zb_i;
 // zb_i -> Bb (the hidden-to-hidden kernels' gradients are jet_hi_wgrad_kernel's); the vector
-// parameters' gradients are summed over the workgroup's points here -> vslab row blockIdx.x
+// parameters' gradients are summed over the workgroup's points here -> vslab row blockIdx.x.
+// Thread t: point p = t >> 7; GEMM role: output quad k4 = (t >> 2) & 31 (outputs k4 + 32 c) over
+// o-quarter ks = t & 3 (o = 64 m + 16 ks + [0, 16)); elementwise role: feature f = k4 + 32 ks.
 template <int S, bool CH>
 __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) jet_hi_chain_kernel(int N, const float* __restrict__ P, NetDims d,
                                                                   HiSpec sp, const float* __restrict__ X,
                                                                   const float* __restrict__ dJ, int ldJ,
                                                                   int j0, const float* __restrict__ Zb,
                                                                   float* __restrict__ Bb, float* __restrict__ vslab) {
-  extern __shared__ __attribute__((aligned(16))) char hi_lds[];
-  HiChainShared& csh = *reinterpret_cast<HiChainShared*>(hi_lds);
-  HiShared& sh = csh.m;
-  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
-  const int Lh = d.n_hidden, dout = d.d_out;
-  int n[HI_PT];
-  bool ok[HI_PT];
-#pragma unroll
-  for (int j = 0; j < HI_PT; ++j) {
-    const int m = blockIdx.x * HI_NP + pg * HI_PT + j;
-    ok[j] = m < N;
-    n[j] = ok[j] ? m : N - 1;
-  }
+  extern __shared__ __attribute__((aligned(16))) float hi_lds[];
+  const HiLds L = hi_lds_map(hi_lds, S);
+  const int t = threadIdx.x, pg = t >> 7, k4 = (t >> 2) & 31, ks = t & 3, f = k4 + 32 * ks;
+  const int Lh = d.n_hidden, dout = d.d_out, din = d.d_in, nvs = hi_nvs(d);
+  const int m0 = blockIdx.x * HI_NP + pg;
+  const bool ok = m0 < N;
+  const int n = ok ? m0 : N - 1;
   HiWRegs wr;
   if (Lh > 1) hi_get_w(wr, P, d, Lh - 1);
-  const int wl = hw(d, Lh - 1), din = d.d_in;
+  const int wl = hw(d, Lh - 1);
   const float* Ko = P + off_layer(d, Lh);
   float* vrow = vslab + (size_t)blockIdx.x * hi_vrow(d);
-  float hb[HI_PT][S], z[HI_PT][S];
-  float vo[TDQ_MAXO], vbo[TDQ_MAXO];  // Ko / bo partials of this thread's point(s)
-#pragma unroll
-  for (int q = 0; q < TDQ_MAXO; ++q) vo[q] = vbo[q] = 0.f;
+  float hb[S], z[S];
+  float vo[TDQ_MAXO], vbo[TDQ_MAXO];  // Ko / bo partials of this thread's point
   {
     float ko[TDQ_MAXO];
 #pragma unroll
     for (int q = 0; q < TDQ_MAXO; ++q)
       ko[q] = ldm(Ko + (f < wl ? f : wl - 1) * dout + (q < dout ? q : dout - 1), q < dout && f < wl);
+    float u[S][TDQ_MAXO];
 #pragma unroll
-    for (int j = 0; j < HI_PT; ++j)
+    for (int s = 0; s < S; ++s) {
+      const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
-        float a = 0.f;
+      for (int q = 0; q < TDQ_MAXO; ++q)
+        u[s][q] = ldm(dJ + ((size_t)orow * ldJ + j0 + n) * dout + (q < dout ? q : 0), sp.out[s] >= 0 && ok && q < dout);
+      z[s] = ldm(Zb + hi_row(Lh - 1, n, s, S, N) + f, f < wl);
+    }
 #pragma unroll
-        for (int q = 0; q < TDQ_MAXO; ++q)
-          a = fmaf(ko[q], ldm(dJ + ((size_t)orow * ldJ + j0 + n[j]) * dout + (q < dout ? q : 0), sp.out[s] >= 0 && ok[j]), a);
-        hb[j][s] = a;
-        z[j][s] = ldm(Zb + hi_row(Lh - 1, n[j], s, S, N) + f, f < wl);
-      }
+    for (int s = 0; s < S; ++s) {
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) a = fmaf(ko[q], u[s][q], a);
+      hb[s] = a;
+    }
     // Ko[f][q] = sum over points and seeded streams of h_s[f] dJ_s[q]; bo[q] = sum of dJ_value[q]
+    float h[S];
+    hi_tanh_f<S, CH>(sp, z, h);
 #pragma unroll
-    for (int j = 0; j < HI_PT; ++j) {
-      float h[S];
-      hi_tanh_f<S, CH>(sp, z[j], h);
+    for (int q = 0; q < TDQ_MAXO; ++q) {
+      float a = 0.f;
 #pragma unroll
-      for (int q = 0; q < TDQ_MAXO; ++q) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
-          const float u = ldm(dJ + ((size_t)orow * ldJ + j0 + n[j]) * dout + (q < dout ? q : 0),
-                              sp.out[s] >= 0 && ok[j] && q < dout);
-          vo[q] = fmaf(f < wl ? h[s] : 0.f, u, vo[q]);
-          if (s == 0) vbo[q] += u;
-        }
-      }
+      for (int s = 0; s < S; ++s) a = fmaf(f < wl ? h[s] : 0.f, u[s][q], a);
+      vo[q] = a;
+      vbo[q] = u[0][q];
     }
   }
   for (int i = Lh - 1; i >= 0; --i) {
     const int wi = hw(d, i);
-#pragma unroll
-    for (int j = 0; j < HI_PT; ++j) {
+    {
       float zb[S];
       if (f < wi) {
-        hi_tanh_b<S, CH>(sp, z[j], hb[j], zb);
+        hi_tanh_b<S, CH>(sp, z, hb, zb);
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) zb[s] = 0.f;
       }
-      if (ok[j]) {
+      if (ok) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) Bb[hi_row(i, n[j], s, S, N) + f] = zb[s];
+        for (int s = 0; s < S; ++s) Bb[hi_row(i, n, s, S, N) + f] = zb[s];
       }
 #pragma unroll
-      for (int s = 0; s < S; ++s) sh.A[pg * HI_PT + j][s][f] = zb[s];
+      for (int s = 0; s < S; ++s) L.a(pg, s, f) = zb[s];
       // vector-parameter partials of this point (padding points: zero adjoints already)
-      float vb = ok[j] ? zb[0] : 0.f;
-      csh.vred[pg][0][f] = (j == 0 ? 0.f : csh.vred[pg][0][f]) + vb;
+      float* V = L.V + pg * nvs * HI_W;
+      V[f] = ok ? zb[0] : 0.f;
       if (i == 0) {
 #pragma unroll
         for (int v = 0; v < TDQ_MAXD; ++v) {
-          float g = ldm(X + (size_t)n[j] * din + (v < din ? v : din - 1), v < din) * zb[0];
+          if (v >= din) break;
+          float g = ldm(X + (size_t)n * din + v, true) * zb[0];
 #pragma unroll
           for (int s = 1; s < S; ++s) g += (sp.order[s] == 1 && sp.var[s] == v) ? zb[s] : 0.f;
-          g = ok[j] ? g : 0.f;
-          csh.vred[pg][1 + v][f] = (j == 0 ? 0.f : csh.vred[pg][1 + v][f]) + g;
+          V[(1 + v) * HI_W + f] = ok ? g : 0.f;
         }
       }
-    }
-    if (i == Lh - 1) {
+      if (i == Lh - 1) {
 #pragma unroll
-      for (int q = 0; q < TDQ_MAXO; ++q) {
-        csh.vred[pg][1 + TDQ_MAXD + q][f] = vo[q];
-        csh.vred[pg][1 + TDQ_MAXD + TDQ_MAXO + q][f] = vbo[q];
+        for (int q = 0; q < TDQ_MAXO; ++q) {
+          if (q >= dout) break;
+          V[(1 + din + q) * HI_W + f] = vo[q];
+          V[(1 + din + dout + q) * HI_W + f] = vbo[q];
+        }
       }
     }
     if (i == 0) {
       __syncthreads();
-      hi_vsum(csh, vrow, d, i, pg, f);
+      hi_vsum(L, vrow, d, i, pg, f);
       break;
     }
-    // hb_{i-1}[k = f] = sum_o zb_i[o] W_i[f][o]; the next layer's pre-activations load meanwhile
-    hi_put_w(sh, wr);
+    // hb_{i-1}[k] = sum_o zb_i[o] W_i[k][o] (k-split over o); the next pre-activations load meanwhile
+    hi_put_w(L, wr);
     __syncthreads();
-    hi_vsum(csh, vrow, d, i, pg, f);
+    hi_vsum(L, vrow, d, i, pg, f);
     if (i >= 2) hi_get_w(wr, P, d, i - 1);
     const int wp = hw(d, i - 1);
 #pragma unroll
-    for (int j = 0; j < HI_PT; ++j)
+    for (int s = 0; s < S; ++s) z[s] = ldm(Zb + hi_row(i - 1, n, s, S, N) + f, f < wp);
+    {
+      f32x4 acc[S];  // acc[s][c]: output k4 + 32 c
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        hb[j][s] = 0.f;
-        z[j][s] = ldm(Zb + hi_row(i - 1, n[j], s, S, N) + f, f < wp);
+      for (int s = 0; s < S; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int jj = 0; jj < 8; ++jj) {
+        const int o = 64 * (jj >> 2) + 16 * ks + 4 * (jj & 3);
+        f32x4 g[S], w[4];
+#pragma unroll
+        for (int s = 0; s < S; ++s) g[s] = *reinterpret_cast<const f32x4*>(&L.a(pg, s, o));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[c] = *reinterpret_cast<const f32x4*>(&L.w(k4 + 32 * c, o));
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            acc[s][c] = fmaf(g[s][0], w[c][0], fmaf(g[s][1], w[c][1], fmaf(g[s][2], w[c][2], fmaf(g[s][3], w[c][3], acc[s][c]))));
       }
-    if (f < wp) {  // software-pipelined like the forward's GEMM
-      const int oin8 = (wi + 7) & ~7;
-      f32x4 g0[HI_PT][S], g1[HI_PT][S], w0, w1;
-      auto ldg = [&](int o, f32x4(&g)[HI_PT][S], f32x4& w) {
-        w = *reinterpret_cast<const f32x4*>(&sh.W[f][o]);
+      // partial of output k = k4 + 32 c -> R at column k + (k >> 5) (the four quarters' lanes of one
+      // output on distinct banks when summed)
 #pragma unroll
-        for (int j = 0; j < HI_PT; ++j)
+      for (int s = 0; s < S; ++s)
 #pragma unroll
-          for (int s = 0; s < S; ++s) g[j][s] = *reinterpret_cast<const f32x4*>(&sh.A[pg * HI_PT + j][s][o]);
-      };
-      auto fma4 = [&](const f32x4(&g)[HI_PT][S], const f32x4& w) {
+        for (int c = 0; c < 4; ++c) L.r(pg, s, ks, k4 + 33 * c) = acc[s][c];
+    }
+    __syncthreads();  // partials in R; GEMM reads of A / W done
+    {
+      const int fr = f + (f >> 5);
 #pragma unroll
-        for (int j = 0; j < HI_PT; ++j)
+      for (int s = 0; s < S; ++s)
+        hb[s] = (L.r(pg, s, 0, fr) + L.r(pg, s, 1, fr)) + (L.r(pg, s, 2, fr) + L.r(pg, s, 3, fr));
+      if (f >= wp) {
 #pragma unroll
-          for (int s = 0; s < S; ++s)
-            hb[j][s] = fmaf(g[j][s][0], w[0], fmaf(g[j][s][1], w[1], fmaf(g[j][s][2], w[2], fmaf(g[j][s][3], w[3], hb[j][s]))));
-      };
-      ldg(0, g0, w0);
-      for (int o = 0; o < oin8; o += 8) {
-        ldg(o + 4, g1, w1);
-        fma4(g0, w0);
-        if (o + 8 < oin8) ldg(o + 8, g0, w0);
-        fma4(g1, w1);
+        for (int s = 0; s < S; ++s) hb[s] = 0.f;
       }
     }
-    __syncthreads();  // sh.A / sh.W reused by the next layer
+    __syncthreads();  // R, A, V reused by the next layer
   }
 }
 
@@ -811,11 +806,13 @@ bool hi_dims(NetDims& d, int d_in, const int* widths, int d_out, int n_hidden) {
   return d.width <= HI_W && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO;
 }
 
+constexpr size_t HI_LDS_MAX = 160 * 1024;
 template <typename K>
-void hi_attr(K* kern, size_t bytes = sizeof(HiShared)) {
+void hi_attr(K* kern) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)bytes);
+                            (int)HI_LDS_MAX);
 }
+bool hi_lds_fits(int S, const NetDims& d) { return hi_lds_floats(S, hi_nvs(d)) * sizeof(float) <= HI_LDS_MAX; }
 
 int hi_splits(int N) { return std::min(HI_KS, std::max(1, (N + 63) / 64)); }
 
@@ -827,7 +824,8 @@ int hi_launch_fwd(const float* X, int N, const float* P, const NetDims& d, const
     hi_attr(&jet_hi_fwd_kernel<S, CH>);
     attr = true;
   }
-  hipLaunchKernelGGL((jet_hi_fwd_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS), sizeof(HiShared), st,
+  hipLaunchKernelGGL((jet_hi_fwd_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS),
+                     hi_lds_floats(S, 0) * sizeof(float), st,
                      X, N, P, d, sp, J, ldJ, j0, Zb, Hb);
   TDQ_CHECK_LAUNCH();
   return 0;
@@ -838,11 +836,11 @@ int hi_launch_chain(int N, const float* P, const NetDims& d, const HiSpec& sp, c
                     int ldJ, int j0, const float* Zb, float* Bb, float* vslab, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hi_attr(&jet_hi_chain_kernel<S, CH>, sizeof(HiChainShared));
+    hi_attr(&jet_hi_chain_kernel<S, CH>);
     attr = true;
   }
   hipLaunchKernelGGL((jet_hi_chain_kernel<S, CH>), dim3((N + HI_NP - 1) / HI_NP), dim3(HI_THREADS),
-                     sizeof(HiChainShared), st, N, P, d, sp, X, dJ, ldJ, j0, Zb, Bb, vslab);
+                     hi_lds_floats(S, hi_nvs(d)) * sizeof(float), st, N, P, d, sp, X, dJ, ldJ, j0, Zb, Bb, vslab);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -907,7 +905,8 @@ int tdq_jet_hi_fwd(const float* X, int N, const float* P, int d_in, const int* w
   if (N <= 0) return 0;
   NetDims d;
   HiSpec sp;
-  if (!hi_dims(d, d_in, widths, d_out, n_hidden) || !hi_spec(sp, spec_i, spec_c)) return (int)hipErrorInvalidValue;
+  if (!hi_dims(d, d_in, widths, d_out, n_hidden) || !hi_spec(sp, spec_i, spec_c) || !hi_lds_fits(sp.S, d))
+    return (int)hipErrorInvalidValue;
   const size_t A = hi_act_floats(N, n_hidden);
   return hi_fwd(X, N, P, d, sp, J, ldJ, j0, Z, Z + A, reinterpret_cast<hipStream_t>(stream));
 }
@@ -920,7 +919,8 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
                    float* work, float* grad, void* stream) {
   NetDims d;
   HiSpec sp;
-  if (!hi_dims(d, d_in, widths, d_out, n_hidden) || !hi_spec(sp, spec_i, spec_c)) return (int)hipErrorInvalidValue;
+  if (!hi_dims(d, d_in, widths, d_out, n_hidden) || !hi_spec(sp, spec_i, spec_c) || !hi_lds_fits(sp.S, d))
+    return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d), Pst = slab_stride(Ptot);
   if (N <= 0) return (int)hipMemsetAsync(grad, 0, sizeof(float) * Ptot, st);
@@ -935,6 +935,14 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
                      hi_vrow(d), d, Ptot, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
+}
+
+// whether the kernels' LDS takes S streams with this input / output width (1) or not (0)
+int tdq_jet_hi_lds_ok(int S, int d_in, int d_out) {
+  NetDims d;
+  d.d_in = d_in;
+  d.d_out = d_out;
+  return S >= 1 && S <= HI_MAXS && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO && hi_lds_fits(S, d) ? 1 : 0;
 }
 
 int tdq_jet_hi_limits(int* out) {

@@ -62,6 +62,12 @@ def eligible(net, plan_hi):
         build_spec(plan_hi, {})
     except ValueError as e:
         return False, str(e)
+    try:
+        lib = _lib.load()
+    except _lib.NativeUnavailable:
+        lib = None
+    if lib is not None and not lib.tdq_jet_hi_lds_ok(len(plan_hi.streams), sizes[0], sizes[-1]):
+        return False, "streams x input / output width beyond the high-order kernels' LDS"
     return True, ""
 
 
