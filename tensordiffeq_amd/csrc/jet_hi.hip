@@ -210,7 +210,7 @@ __device__ __forceinline__ void hi_tanh_b(const HiSpec& sp, const float (&z)[S],
 //                            W[k][o..o+3] of the k-split GEMMs are conflict-free)
 //   A [HI_NP][S][HI_AS]      the workgroup's activations / adjoints (float4 broadcasts)
 //   R [HI_NP][S][4][HI_AS]   k-split GEMM partials: four k-quarters per output, summed in order
-//   V [HI_TG][nvs][HI_W]     (chain) vector-parameter partials, nvs = 1 + d_in + 2 d_out
+//   V [HI_TG][nvs][HI_W]     (chain) vector-parameter partials (nvs slots, hi_nvs)
 struct HiLds {
   float* W;
   float* A;
@@ -462,29 +462,34 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 __host__ __device__ inline int hi_vrow(const NetDims& d) {
   return (((d.n_hidden + d.d_in) * HI_W + HI_W * TDQ_MAXO + TDQ_MAXO) + 3) & ~3;
 }
-__host__ __device__ inline int hi_nvs(const NetDims& d) { return 1 + d.d_in + 2 * d.d_out; }
+// V slots: 0 bias; 1 .. d_in K0 (layer 0); from hi_vko: d_out Ko then d_out bo (last layer) - with
+// two or more hidden layers the first and the last layer share slots 1.. (never both live)
+__host__ __device__ inline int hi_vko(const NetDims& d) { return d.n_hidden == 1 ? 1 + d.d_in : 1; }
+__host__ __device__ inline int hi_nvs(const NetDims& d) {
+  return d.n_hidden == 1 ? 1 + d.d_in + 2 * d.d_out : 1 + (d.d_in > 2 * d.d_out ? d.d_in : 2 * d.d_out);
+}
 
-// fixed-order sum over the point groups of layer i's vector partials (V slots: 0 bias, 1 .. d_in
-// K0, then d_out Ko and d_out bo) -> the workgroup's vslab row; thread (f, group g) takes slots
-// g, g + HI_TG, ...
+// fixed-order sum over the point groups of layer i's vector partials (slots: hi_nvs) -> the
+// workgroup's vslab row; thread (f, group g) takes slots g, g + HI_TG, ...
 __device__ __forceinline__ void hi_vsum(const HiLds& L, float* __restrict__ vrow, const NetDims& d, int i, int g,
                                         int f) {
-  const int Lh = d.n_hidden, din = d.d_in, dout = d.d_out, nvs = hi_nvs(d);
+  const int Lh = d.n_hidden, din = d.d_in, dout = d.d_out, nvs = hi_nvs(d), vko = hi_vko(d);
   for (int sl = g; sl < nvs; sl += HI_TG) {
-    const bool use = sl == 0 || (i == 0 && sl <= din) || (i == Lh - 1 && sl > din);
-    if (!use) continue;
+    const bool k0 = i == 0 && sl >= 1 && sl <= din;
+    const bool ko = i == Lh - 1 && sl >= vko && sl < vko + dout;
+    const bool bo = i == Lh - 1 && sl >= vko + dout && sl < vko + 2 * dout;
+    if (!(sl == 0 || k0 || ko || (bo && f == 0))) continue;
     float a = L.V[sl * HI_W + f];
 #pragma unroll
     for (int gg = 1; gg < HI_TG; ++gg) a += L.V[(gg * nvs + sl) * HI_W + f];
-    if (sl == 0) {
+    if (sl == 0)
       vrow[i * HI_W + f] = a;
-    } else if (sl <= din) {
+    else if (k0)
       vrow[(Lh + sl - 1) * HI_W + f] = a;
-    } else if (sl <= din + dout) {
-      vrow[(Lh + din) * HI_W + f * TDQ_MAXO + (sl - 1 - din)] = a;
-    } else if (f == 0) {
-      vrow[(Lh + din) * HI_W + HI_W * TDQ_MAXO + (sl - 1 - din - dout)] = a;
-    }
+    else if (ko)
+      vrow[(Lh + din) * HI_W + f * TDQ_MAXO + (sl - vko)] = a;
+    else
+      vrow[(Lh + din) * HI_W + HI_W * TDQ_MAXO + (sl - vko - dout)] = a;
   }
 }
 
@@ -576,11 +581,12 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         }
       }
       if (i == Lh - 1) {
+        const int vko = hi_vko(d);
 #pragma unroll
         for (int q = 0; q < TDQ_MAXO; ++q) {
           if (q >= dout) break;
-          V[(1 + din + q) * HI_W + f] = vo[q];
-          V[(1 + din + dout + q) * HI_W + f] = vbo[q];
+          V[(vko + q) * HI_W + f] = vo[q];
+          V[(vko + dout + q) * HI_W + f] = vbo[q];
         }
       }
     }
@@ -937,11 +943,12 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   return 0;
 }
 
-// whether the kernels' LDS takes S streams with this input / output width (1) or not (0)
-int tdq_jet_hi_lds_ok(int S, int d_in, int d_out) {
+// whether the kernels' LDS takes S streams with this input / output width and depth (1) or not (0)
+int tdq_jet_hi_lds_ok(int S, int d_in, int d_out, int n_hidden) {
   NetDims d;
   d.d_in = d_in;
   d.d_out = d_out;
+  d.n_hidden = n_hidden;
   return S >= 1 && S <= HI_MAXS && d_in <= TDQ_MAXD && d_out <= TDQ_MAXO && hi_lds_fits(S, d) ? 1 : 0;
 }
 

@@ -73,7 +73,7 @@ def _declare(lib):
         "tdq_jet_hi_fwd": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P]),
         "tdq_jet_hi_bwd": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P, P, P]),
         "tdq_jet_hi_limits": (I, [P]),
-        "tdq_jet_hi_lds_ok": (I, [I, I, I]),
+        "tdq_jet_hi_lds_ok": (I, [I, I, I, I]),
         # one-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py)
         "tdq_peer_maxw": (I, []),
         "tdq_peer_chunk": (I, []),

@@ -66,7 +66,7 @@ def eligible(net, plan_hi):
         lib = _lib.load()
     except _lib.NativeUnavailable:
         lib = None
-    if lib is not None and not lib.tdq_jet_hi_lds_ok(len(plan_hi.streams), sizes[0], sizes[-1]):
+    if lib is not None and not lib.tdq_jet_hi_lds_ok(len(plan_hi.streams), sizes[0], sizes[-1], len(sizes) - 2):
         return False, "streams x input / output width beyond the high-order kernels' LDS"
     return True, ""
 
