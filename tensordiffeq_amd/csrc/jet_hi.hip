@@ -714,50 +714,54 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
     }
 }
 
-// gradient = fixed-order sums: the hidden-to-hidden kernels over the ks split rows of the tile
-// slab, every other parameter over the nwg workgroup rows of the chain's vslab (deterministic)
-__global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restrict__ slab, int ks, int Pst,
-                                                            const float* __restrict__ vslab, int nwg, int Vst,
-                                                            NetDims d, int Ptot, float* __restrict__ grad) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= Ptot) return;
+// gradient of the hidden-to-hidden kernels: fixed-order sums over the ks split rows of the tile slab
+__global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restrict__ slab, int ks, int Pst, NetDims d,
+                                                            float* __restrict__ grad) {
   const int Lh = d.n_hidden;
-  int layer = Lh;
-  for (int i = 1; i <= Lh; ++i)
-    if (e < off_layer(d, i)) {
-      layer = i - 1;
-      break;
-    }
+  const int e = off_layer(d, 1) + blockIdx.x * 256 + threadIdx.x;
+  if (e >= off_layer(d, Lh)) return;
+  int layer = 1;
+  while (layer + 1 < Lh && e >= off_layer(d, layer + 1)) ++layer;
   const int r = e - off_layer(d, layer);
-  int vi = -1;  // vslab column, or -1: tile slab
-  if (layer < Lh) {
-    const int win = layer == 0 ? d.d_in : hw(d, layer - 1), wout = hw(d, layer);
-    if (r >= win * wout)
-      vi = layer * HI_W + (r - win * wout);                    // bias
-    else if (layer == 0)
-      vi = (Lh + r / wout) * HI_W + r % wout;                  // K0
+  if (r >= hw(d, layer - 1) * hw(d, layer)) return;  // bias: the vector reduction's
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int q = 0;
+  for (; q + 3 < ks; q += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += slab[(size_t)(q + u) * Pst + e];
+  for (; q < ks; ++q) a[0] += slab[(size_t)q * Pst + e];
+  grad[e] = (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+// gradient of the vector parameters (hidden biases, K0, Ko, bo): one wave per vslab column; lane l
+// sums the workgroup rows l, l + 64, ... in order, then a fixed butterfly across the wave
+// (deterministic, and ~nwg / 64 dependent loads per lane instead of nwg)
+__global__ void __launch_bounds__(256) jet_hi_vreduce_kernel(const float* __restrict__ vslab, int nwg, int Vst,
+                                                             NetDims d, float* __restrict__ grad) {
+  const int Lh = d.n_hidden, din = d.d_in, dout = d.d_out, wl = hw(d, Lh - 1);
+  const int vi = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  int e = -1;  // parameter index of vslab column vi (-1: padding column)
+  if (vi < Lh * HI_W) {
+    const int i = vi / HI_W, f = vi % HI_W;
+    if (f < hw(d, i)) e = off_layer(d, i) + (i == 0 ? din : hw(d, i - 1)) * hw(d, i) + f;
+  } else if (vi < (Lh + din) * HI_W) {
+    const int v = vi / HI_W - Lh, f = vi % HI_W;
+    if (f < hw(d, 0)) e = v * hw(d, 0) + f;
+  } else if (vi < (Lh + din) * HI_W + HI_W * TDQ_MAXO) {
+    const int r = vi - (Lh + din) * HI_W, f = r / TDQ_MAXO, q = r % TDQ_MAXO;
+    if (f < wl && q < dout) e = off_layer(d, Lh) + f * dout + q;
   } else {
-    const int wl = hw(d, Lh - 1), dout = d.d_out;
-    vi = r < wl * dout ? (Lh + d.d_in) * HI_W + (r / dout) * TDQ_MAXO + r % dout   // Ko
-                       : (Lh + d.d_in) * HI_W + HI_W * TDQ_MAXO + (r - wl * dout);  // bo
+    const int q = vi - (Lh + din) * HI_W - HI_W * TDQ_MAXO;
+    if (q < dout) e = off_layer(d, Lh) + wl * dout + q;
   }
-  float a0 = 0.f, a1 = 0.f;
-  if (vi < 0) {
-    int q = 0;
-    for (; q + 1 < ks; q += 2) {
-      a0 += slab[(size_t)q * Pst + e];
-      a1 += slab[(size_t)(q + 1) * Pst + e];
-    }
-    if (q < ks) a0 += slab[(size_t)q * Pst + e];
-  } else {
-    int q = 0;
-    for (; q + 1 < nwg; q += 2) {
-      a0 += vslab[(size_t)q * Vst + vi];
-      a1 += vslab[(size_t)(q + 1) * Vst + vi];
-    }
-    if (q < nwg) a0 += vslab[(size_t)q * Vst + vi];
-  }
-  grad[e] = a0 + a1;
+  if (e < 0) return;  // wave-uniform
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = l, u = 0;
+  for (; r < nwg; r += 64, u = (u + 1) & 3) a[u] += vslab[(size_t)r * Vst + vi];
+  float v = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  if (l == 0) grad[e] = v;
 }
 
 namespace {
@@ -937,8 +941,13 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   if (rc) return rc;
   rc = hi_wgrad(N, d, sp, Z + A, Z + 2 * A, work, Pst, ks, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((Ptot + 255) / 256), dim3(256), 0, st, work, ks, Pst, vslab, nwg,
-                     hi_vrow(d), d, Ptot, grad);
+  const int ntile = off_layer(d, n_hidden) - off_layer(d, 1);
+  if (ntile > 0) {
+    hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((ntile + 255) / 256), dim3(256), 0, st, work, ks, Pst, d, grad);
+    TDQ_CHECK_LAUNCH();
+  }
+  const int ncol = (n_hidden + d_in) * HI_W + HI_W * TDQ_MAXO + TDQ_MAXO;
+  hipLaunchKernelGGL(jet_hi_vreduce_kernel, dim3((ncol + 3) / 4), dim3(256), 0, st, vslab, nwg, hi_vrow(d), d, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

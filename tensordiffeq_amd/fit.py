@@ -667,12 +667,14 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
         raise RuntimeError("point ranges: the first range must hold the high-order points")
     cur = torch.cuda.current_stream(flat.device)
     # the high-order points' extra streams (a hundred workgroups of long per-layer chains; they
-    # touch only their own J rows): TDQ_HI_PLACE = side_after (default: forward on a side branch
-    # beside range 0's forward, joined before its loss; gradient after range 0's backward, beside
-    # the longer range 1), side_before (gradient between range 0's loss and backward),
-    # serial_after / serial_before (forward on range 0's stream too).  A third branch for the
-    # gradient made hipStreamEndCapture crash on MI355X / ROCm 7.2.
-    place = os.environ.get("TDQ_HI_PLACE", "side_after")
+    # touch only their own J rows) run on range 0's stream: TDQ_HI_PLACE = serial_after (default:
+    # forward before range 0's forward, gradient after its backward - beside the longer range 1),
+    # serial_before (gradient between range 0's loss and backward), side_after / side_before
+    # (forward on a third graph branch beside range 0's forward, joined before its loss).  AC-baseline
+    # step, MI355X: serial 0.275 ms, side branch 0.302-0.307 ms (three branches contend for the CUs;
+    # profiles/r4l_place.jsonl).  A third branch for the gradient made hipStreamEndCapture crash on
+    # MI355X / ROCm 7.2.
+    place = os.environ.get("TDQ_HI_PLACE", "serial_after")
     hs = hop.stream if (hop is not None and place.startswith("side")) else None
     bwd_first = place.endswith("before")
     if hs is not None:

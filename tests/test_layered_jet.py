@@ -79,6 +79,9 @@ def test_layered_engine_hip(sizes, reqs, N, prec):
     from tensordiffeq_amd.ops import jet_hip, jet_mlp
     net, X, plan = _setup(sizes, reqs, N, "cuda", torch.float32, seed=1)
     cfg = jet_mlp.hip_config(net, plan, prec)
+    if prec == "bf16" and not jet_hip.is_layered(cfg):
+        assert cfg["WT"] == 16   # widths <= 256, S <= 4: the fused kernels (tests/test_hip_kernels.py::test_wide256_*)
+        pytest.skip("served by the fused WT = 16 kernels")
     assert jet_hip.is_layered(cfg) and not jet_hip.is_split_bf16(cfg) and cfg["precision"] == prec
     p = net.flat.detach().clone().requires_grad_(True)
     J = jet_hip.JetMLPFunction.apply(X, p, net, plan, prec)
