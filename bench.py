@@ -387,7 +387,7 @@ def main(argv=None):
                     help="seeds of the full-schedule accuracy runs (single GPU only)")
     ap.add_argument("--acc-iters", type=int, default=10000)
     ap.add_argument("--acc-newton", type=int, default=None,
-                    help="L-BFGS iterations of the accuracy runs (default 10000; discovery 5000)")
+                    help="L-BFGS iterations of the accuracy runs (default 10000; discovery 15000)")
     ap.add_argument("--newton-precision", default="bf16x3")
     ap.add_argument("--newton-schedule", default=None,
                     help="leading L-BFGS phases of the accuracy runs, 'prec:iters,...' (e.g. bf16:7000)")
