@@ -506,6 +506,8 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
                                                                   float* __restrict__ Bb, float* __restrict__ vslab) {
   extern __shared__ __attribute__((aligned(16))) float hi_lds[];
   const HiLds L = hi_lds_map(hi_lds, S);
+  HI_TS_DECL
+  HI_TS()
   const int t = threadIdx.x, pg = t >> 7, k4 = (t >> 2) & 31, ks = t & 3, f = k4 + 32 * ks;
   const int Lh = d.n_hidden, dout = d.d_out, din = d.d_in, nvs = hi_nvs(d);
   const int m0 = blockIdx.x * HI_NP + pg;
@@ -551,6 +553,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       vbo[q] = u[0][q];
     }
   }
+  HI_TS()
   for (int i = Lh - 1; i >= 0; --i) {
     const int wi = hw(d, i);
     {
@@ -590,14 +593,17 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         }
       }
     }
+    HI_TS()
     if (i == 0) {
       __syncthreads();
       hi_vsum(L, vrow, d, i, pg, f);
+      HI_TS()
       break;
     }
     // hb_{i-1}[k] = sum_o zb_i[o] W_i[k][o] (k-split over o); the next pre-activations load meanwhile
     hi_put_w(L, wr);
     __syncthreads();
+    HI_TS()
     hi_vsum(L, vrow, d, i, pg, f);
     if (i >= 2) hi_get_w(wr, P, d, i - 1);
     const int wp = hw(d, i - 1);
@@ -628,6 +634,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
         for (int c = 0; c < 4; ++c) L.r(pg, s, ks, k4 + 33 * c) = acc[s][c];
     }
+    HI_TS()
     __syncthreads();  // partials in R; GEMM reads of A / W done
     {
       const int fr = f + (f >> 5);
@@ -640,7 +647,9 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       }
     }
     __syncthreads();  // R, A, V reused by the next layer
+    HI_TS()
   }
+  HI_TS_PRINT("chain")
 }
 
 // Weight gradients over the point range of split blockIdx.y (one slab row per split, reduced in
@@ -663,6 +672,8 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
   const int kt = tile / (HI_W / HI_TILE), ft = tile % (HI_W / HI_TILE);
   const int win = hw(d, i - 1), wout = hw(d, i);
   if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
+  HI_TS_DECL
+  HI_TS()
   const int tk = t >> 4, tf = t & 15;
   float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
   const int r0 = n0 * S, r1 = n1 * S;
@@ -686,6 +697,7 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
       *reinterpret_cast<f32x4*>(&Gc[rr][c]) = in ? gv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
+    HI_TS()
     const int nb = (min(HI_RB, r1 - r) + 7) & ~7;
     for (int rb = 0; rb < nb; rb += 8) {  // 16 LDS reads in flight, then 32 FMAs
       float2 h2[8], g2[8];
@@ -712,6 +724,8 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
       const int k = kt * HI_TILE + 2 * tk + a, f = ft * HI_TILE + 2 * tf + b;
       if (k < win && f < wout) dk[k * wout + f] = acc[a][b];
     }
+  HI_TS()
+  HI_TS_PRINT("wgrad")
 }
 
 // gradient of the hidden-to-hidden kernels: fixed-order sums over the ks split rows of the tile slab
