@@ -674,8 +674,12 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
   if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
   HI_TS_DECL
   HI_TS()
-  const int tk = t >> 4, tf = t & 15;
-  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  const int wv = t >> 6, tk4 = (t & 63) >> 3, tf4 = t & 7;
+  float acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
   const int r0 = n0 * S, r1 = n1 * S;
   const float* Hl = Hb + hi_row(i - 1, 0, 0, S, N) + kt * HI_TILE;
   const float* Bl = Bb + hi_row(i, 0, 0, S, N) + ft * HI_TILE;
@@ -698,32 +702,44 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
     }
     __syncthreads();
     HI_TS()
-    const int nb = (min(HI_RB, r1 - r) + 7) & ~7;
-    for (int rb = 0; rb < nb; rb += 8) {  // 16 LDS reads in flight, then 32 FMAs
-      float2 h2[8], g2[8];
+    // wave w takes rows w, w + 4, ...; lane (tk4, tf4) a 4 x 4 block: two float4 LDS reads per row
+    // for 16 FMAs (rows four at a time: eight reads in flight)
+    const int nb = min(HI_RB, r1 - r);
+    for (int rb = wv; rb < nb; rb += 16) {
+      f32x4 h4[4], g4[4];
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        h2[rr] = *reinterpret_cast<const float2*>(&Hc[rb + rr][2 * tk]);
-        g2[rr] = *reinterpret_cast<const float2*>(&Gc[rb + rr][2 * tf]);
+      for (int u = 0; u < 4; ++u) {
+        const int rr = min(rb + 4 * u, HI_RB - 1);  // rows past nb are zero-filled (or finite: masked below)
+        h4[u] = *reinterpret_cast<const f32x4*>(&Hc[rr][4 * tk4]);
+        g4[u] = *reinterpret_cast<const f32x4*>(&Gc[rr][4 * tf4]);
       }
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        acc[0][0] = fmaf(h2[rr].x, g2[rr].x, acc[0][0]);
-        acc[0][1] = fmaf(h2[rr].x, g2[rr].y, acc[0][1]);
-        acc[1][0] = fmaf(h2[rr].y, g2[rr].x, acc[1][0]);
-        acc[1][1] = fmaf(h2[rr].y, g2[rr].y, acc[1][1]);
+      for (int u = 0; u < 4; ++u) {
+        const float m = rb + 4 * u < nb ? 1.f : 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = fmaf(m * h4[u][a], g4[u][b], acc[a][b]);
       }
     }
     __syncthreads();
   }
+  // the four waves' partials -> fixed-order sum (the staging area is free now)
+  float* red = &Hc[0][0];  // [wave][32][32]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+    *reinterpret_cast<f32x4*>(&red[(wv * HI_TILE + 4 * tk4 + a) * HI_TILE + 4 * tf4]) =
+        f32x4{acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
+  __syncthreads();
   float* dk = row + off_layer(d, i);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int k = kt * HI_TILE + 2 * tk + a, f = ft * HI_TILE + 2 * tf + b;
-      if (k < win && f < wout) dk[k * wout + f] = acc[a][b];
-    }
+  for (int q = 0; q < 4; ++q) {
+    const int o = t + 256 * q, kk = o / HI_TILE, ff = o % HI_TILE;
+    const float v = (red[(0 * HI_TILE + kk) * HI_TILE + ff] + red[(1 * HI_TILE + kk) * HI_TILE + ff]) +
+                    (red[(2 * HI_TILE + kk) * HI_TILE + ff] + red[(3 * HI_TILE + kk) * HI_TILE + ff]);
+    const int k = kt * HI_TILE + kk, f = ft * HI_TILE + ff;
+    if (k < win && f < wout) dk[k * wout + f] = v;
+  }
   HI_TS()
   HI_TS_PRINT("wgrad")
 }

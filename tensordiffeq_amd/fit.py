@@ -587,8 +587,14 @@ def point_ranges(program, fop):
         return None
     if spec == "auto":
         # sweeps on MI355X with the specialized loss kernel: bf16 0.38 (0.2018 ms vs 0.2035 at 0.45,
-        # 3 passes, profiles/r3_yz_split_sweep_jit.jsonl), bf16x3 0.30-0.40 equal within noise
-        fracs = [0.35] if cfg["precision"] == "bf16x3" else [0.38]
+        # 3 passes, profiles/r3_yz_split_sweep_jit.jsonl), bf16x3 0.30-0.40 equal within noise.
+        # Mixed programs (high-order kernels on the first range's stream): the first range the
+        # LONGER one, 0.62 (AC-baseline 0.231-0.232 ms vs 0.251-0.261 at 0.30-0.55,
+        # profiles/r4s_place.jsonl) - its high-order gradient then overlaps the other range's backward
+        if getattr(program, "hi_op", None) is not None:
+            fracs = [0.62]
+        else:
+            fracs = [0.35] if cfg["precision"] == "bf16x3" else [0.38]
     else:
         fracs = sorted(float(v) for v in spec.split(","))
     if len(fracs) > 1:
@@ -667,14 +673,16 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
         raise RuntimeError("point ranges: the first range must hold the high-order points")
     cur = torch.cuda.current_stream(flat.device)
     # the high-order points' extra streams (a hundred workgroups of long per-layer chains; they
-    # touch only their own J rows) run on range 0's stream: TDQ_HI_PLACE = serial_after (default:
-    # forward before range 0's forward, gradient after its backward - beside the longer range 1),
-    # serial_before (gradient between range 0's loss and backward), side_after / side_before
-    # (forward on a third graph branch beside range 0's forward, joined before its loss).  AC-baseline
-    # step, MI355X: serial 0.275 ms, side branch 0.302-0.307 ms (three branches contend for the CUs;
-    # profiles/r4l_place.jsonl).  A third branch for the gradient made hipStreamEndCapture crash on
-    # MI355X / ROCm 7.2.
-    place = os.environ.get("TDQ_HI_PLACE", "serial_after")
+    # touch only their own J rows) run on range 0's stream: TDQ_HI_PLACE = serial_before (default:
+    # forward before range 0's forward, gradient between its loss and its backward - with range 0
+    # the longer range (point_ranges) that gradient runs beside range 1's backward), serial_after
+    # (gradient after range 0's backward), side_after / side_before (forward on a third graph branch
+    # beside range 0's forward, joined before its loss).  AC-baseline step on MI355X: serial_before
+    # at cut 0.62 0.231-0.237 ms; at cut 0.38 serial 0.275 ms, side branch 0.302-0.307 ms (three
+    # branches contend for the CUs) - profiles/r4l_place.jsonl, r4q_place_cut_sweep.jsonl,
+    # r4s_place.jsonl.  A third branch for the gradient made hipStreamEndCapture crash on MI355X /
+    # ROCm 7.2.
+    place = os.environ.get("TDQ_HI_PLACE", "serial_before")
     hs = hop.stream if (hop is not None and place.startswith("side")) else None
     bwd_first = place.endswith("before")
     if hs is not None:
