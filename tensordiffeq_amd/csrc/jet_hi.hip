@@ -364,10 +364,17 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int v = 0; v < TDQ_MAXD; ++v) {
       const int vc = v < d.d_in ? v : d.d_in - 1;
-      kv[v] = ldm(P + vc * w0 + fc, v < d.d_in && f < w0);
-      xv[v] = ldm(X + (size_t)n * d.d_in + vc, v < d.d_in);
+      kv[v] = P[vc * w0 + fc];
+      xv[v] = X[(size_t)n * d.d_in + vc];
     }
-    float a = ldm(P + d.d_in * w0 + fc, f < w0);
+    float a = P[d.d_in * w0 + fc];
+    __builtin_amdgcn_sched_barrier(0);  // all loads in flight first
+#pragma unroll
+    for (int v = 0; v < TDQ_MAXD; ++v) {
+      kv[v] = (v < d.d_in && f < w0) ? kv[v] : 0.f;
+      xv[v] = v < d.d_in ? xv[v] : 0.f;
+    }
+    a = f < w0 ? a : 0.f;
 #pragma unroll
     for (int v = 0; v < TDQ_MAXD; ++v) a = fmaf(xv[v], kv[v], a);
     z[0] = a;
@@ -530,9 +537,17 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
     for (int s = 0; s < S; ++s) {
       const int orow = sp.out[s] >= 0 ? sp.out[s] : 0;
 #pragma unroll
-      for (int q = 0; q < TDQ_MAXO; ++q)
-        u[s][q] = ldm(dJ + ((size_t)orow * ldJ + j0 + n) * dout + (q < dout ? q : 0), sp.out[s] >= 0 && ok && q < dout);
-      z[s] = ldm(Zb + hi_row(Lh - 1, n, s, S, N) + f, f < wl);
+      for (int q = 0; q < TDQ_MAXO; ++q) u[s][q] = dJ[((size_t)orow * ldJ + j0 + n) * dout + (q < dout ? q : 0)];
+      z[s] = Zb[hi_row(Lh - 1, n, s, S, N) + f];
+    }
+    // every load above in flight before the first use (the scheduler otherwise interleaves each load
+    // with its use: one memory latency per load); masks applied after
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int q = 0; q < TDQ_MAXO; ++q) u[s][q] = (sp.out[s] >= 0 && ok && q < dout) ? u[s][q] : 0.f;
+      z[s] = f < wl ? z[s] : 0.f;
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -574,13 +589,16 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       float* V = L.V + pg * nvs * HI_W;
       V[f] = ok ? zb[0] : 0.f;
       if (i == 0) {
+        float xv[TDQ_MAXD];
+#pragma unroll
+        for (int v = 0; v < TDQ_MAXD; ++v) xv[v] = X[(size_t)n * din + (v < din ? v : din - 1)];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int v = 0; v < TDQ_MAXD; ++v) {
-          if (v >= din) break;
-          float g = ldm(X + (size_t)n * din + v, true) * zb[0];
+          float g = xv[v] * zb[0];
 #pragma unroll
           for (int s = 1; s < S; ++s) g += (sp.order[s] == 1 && sp.var[s] == v) ? zb[s] : 0.f;
-          V[(1 + v) * HI_W + f] = ok ? g : 0.f;
+          if (v < din) V[(1 + v) * HI_W + f] = ok ? g : 0.f;
         }
       }
       if (i == Lh - 1) {
@@ -608,7 +626,8 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
     if (i >= 2) hi_get_w(wr, P, d, i - 1);
     const int wp = hw(d, i - 1);
 #pragma unroll
-    for (int s = 0; s < S; ++s) z[s] = ldm(Zb + hi_row(i - 1, n, s, S, N) + f, f < wp);
+    for (int s = 0; s < S; ++s) z[s] = Zb[hi_row(i - 1, n, s, S, N) + f];  // used (masked) after the GEMM
+    __builtin_amdgcn_sched_barrier(0);
     {
       f32x4 acc[S];  // acc[s][c]: output k4 + 32 c
 #pragma unroll
@@ -643,7 +662,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         hb[s] = (L.r(pg, s, 0, fr) + L.r(pg, s, 1, fr)) + (L.r(pg, s, 2, fr) + L.r(pg, s, 3, fr));
       if (f >= wp) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) hb[s] = 0.f;
+        for (int s = 0; s < S; ++s) hb[s] = z[s] = 0.f;
       }
     }
     __syncthreads();  // R, A, V reused by the next layer
