@@ -189,7 +189,8 @@ def test_forced_dp_rccl_multistep_graph():
 
 
 @pytest.mark.timeout(300)
-def test_bench_self_launch_two_ranks_share_gpu():
+@pytest.mark.parametrize("problem", ["ac-sa", "ac-baseline"])
+def test_bench_self_launch_two_ranks_share_gpu(problem):
     """``python bench.py --gpus 2`` with no launcher on the one-GPU box: bench.py starts the two ranks
     itself (children under torch.distributed.run); they share cuda:0 over gloo + the peer all-reduce
     (TDQ_DIST_BACKEND=gloo: RCCL refuses two ranks on one device) and rank 0 prints one JSON line
@@ -202,13 +203,13 @@ def test_bench_self_launch_two_ranks_share_gpu():
     env.pop("WORLD_SIZE", None)
     env.update(TDQ_DIST_BACKEND="gloo", PYTHONPATH=root + os.pathsep + env.get("PYTHONPATH", ""))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "4",
-           "--npts", "8192", "--no-l2", "--min-warmup-s", "0.2"]
+           "--npts", "8192", "--no-l2", "--min-warmup-s", "0.2", "--problem", problem]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     rec = json.loads(lines[0])
-    print("SELF_LAUNCH", json.dumps({k: rec[k] for k in ("n_gpus", "ms_per_step", "rank_ms_per_step", "allreduce")}))
+    print("SELF_LAUNCH", problem, json.dumps({k: rec[k] for k in ("n_gpus", "ms_per_step", "rank_ms_per_step", "allreduce")}))
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["backend"] == "hip"
     assert rec["rank_ms_per_step"]["min"] <= rec["rank_ms_per_step"]["max"]
     assert rec["allreduce"]["replay"]["us_per_call"] > 0
