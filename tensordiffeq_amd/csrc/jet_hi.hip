@@ -38,6 +38,8 @@
 // 0.31 + 0.40 ms per step; this layout 26 + 57 us isolated (profiles/r4g_kernel_stats_hi_isolated.txt).
 #include "jet_common.h"
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 #define HI_MAXS 8
 #define HI_MAXT 48
 #define HI_MAXB 4
@@ -693,12 +695,10 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
   if (kt * HI_TILE >= win || ft * HI_TILE >= wout) return;  // uniform: the whole workgroup leaves
   HI_TS_DECL
   HI_TS()
-  const int wv = t >> 6, tk4 = (t & 63) >> 3, tf4 = t & 7;
-  float acc[4][4];
+  const int wv = t >> 6, l = t & 63;
+  f32x16 acc;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
   const int r0 = n0 * S, r1 = n1 * S;
   const float* Hl = Hb + hi_row(i - 1, 0, 0, S, N) + kt * HI_TILE;
   const float* Bl = Bb + hi_row(i, 0, 0, S, N) + ft * HI_TILE;
@@ -721,34 +721,21 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
     }
     __syncthreads();
     HI_TS()
-    // wave w takes rows w, w + 4, ...; lane (tk4, tf4) a 4 x 4 block: two float4 LDS reads per row
-    // for 16 FMAs (rows four at a time: eight reads in flight)
+    // fp32 MFMA 32x32x2: wave w takes the row pairs 2 (w + 4 m); lane l supplies A[k = l & 31][row
+    // l >> 5] = H[row][k] and B[row l >> 5][f = l & 31] = G[row][f] - one conflict-free LDS read each
     const int nb = min(HI_RB, r1 - r);
-    for (int rb = wv; rb < nb; rb += 16) {
-      f32x4 h4[4], g4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int rr = min(rb + 4 * u, HI_RB - 1);  // rows past nb are zero-filled (or finite: masked below)
-        h4[u] = *reinterpret_cast<const f32x4*>(&Hc[rr][4 * tk4]);
-        g4[u] = *reinterpret_cast<const f32x4*>(&Gc[rr][4 * tf4]);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float m = rb + 4 * u < nb ? 1.f : 0.f;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = fmaf(m * h4[u][a], g4[u][b], acc[a][b]);
-      }
+    for (int rb = 2 * wv; rb < nb; rb += 8) {
+      const int rr = min(rb + (l >> 5), HI_RB - 1);  // rows past nb are zero-filled
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Hc[rr][l & 31], Gc[rr][l & 31], acc, 0, 0, 0);
     }
     __syncthreads();
   }
-  // the four waves' partials -> fixed-order sum (the staging area is free now)
+  // the four waves' partials -> fixed-order sum (the staging area is free now); lane l, register q
+  // of the 32x32 accumulator holds D[8 (q >> 2) + 4 (l >> 5) + (q & 3)][l & 31]
   float* red = &Hc[0][0];  // [wave][32][32]
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-    *reinterpret_cast<f32x4*>(&red[(wv * HI_TILE + 4 * tk4 + a) * HI_TILE + 4 * tf4]) =
-        f32x4{acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
+  for (int q = 0; q < 16; ++q)
+    red[(wv * HI_TILE + 8 * (q >> 2) + 4 * (l >> 5) + (q & 3)) * HI_TILE + (l & 31)] = acc[q];
   __syncthreads();
   float* dk = row + off_layer(d, i);
 #pragma unroll
