@@ -751,10 +751,10 @@ __global__ void __launch_bounds__(256) jet_hi_wgrad_kernel(int N, int S, NetDims
 }
 
 // gradient of the hidden-to-hidden kernels: fixed-order sums over the ks split rows of the tile slab
-__global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restrict__ slab, int ks, int Pst, NetDims d,
-                                                            float* __restrict__ grad) {
+__device__ __forceinline__ void hi_tile_reduce(int bx, const float* __restrict__ slab, int ks, int Pst, const NetDims& d,
+                                               float* __restrict__ grad) {
   const int Lh = d.n_hidden;
-  const int e = off_layer(d, 1) + blockIdx.x * 256 + threadIdx.x;
+  const int e = off_layer(d, 1) + bx * 256 + threadIdx.x;
   if (e >= off_layer(d, Lh)) return;
   int layer = 1;
   while (layer + 1 < Lh && e >= off_layer(d, layer + 1)) ++layer;
@@ -772,10 +772,10 @@ __global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restr
 // gradient of the vector parameters (hidden biases, K0, Ko, bo): one wave per vslab column; lane l
 // sums the workgroup rows l, l + 64, ... in order, then a fixed butterfly across the wave
 // (deterministic, and ~nwg / 64 dependent loads per lane instead of nwg)
-__global__ void __launch_bounds__(256) jet_hi_vreduce_kernel(const float* __restrict__ vslab, int nwg, int Vst,
-                                                             NetDims d, float* __restrict__ grad) {
+__device__ __forceinline__ void hi_vec_reduce(int bx, const float* __restrict__ vslab, int nwg, int Vst, const NetDims& d,
+                                              float* __restrict__ grad) {
   const int Lh = d.n_hidden, din = d.d_in, dout = d.d_out, wl = hw(d, Lh - 1);
-  const int vi = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int vi = bx * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   int e = -1;  // parameter index of vslab column vi (-1: padding column)
   if (vi < Lh * HI_W) {
     const int i = vi / HI_W, f = vi % HI_W;
@@ -798,6 +798,16 @@ __global__ void __launch_bounds__(256) jet_hi_vreduce_kernel(const float* __rest
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
   if (l == 0) grad[e] = v;
+}
+
+// both reductions in one launch: blocks [0, ntb) the tile slab, the rest the vector slab
+__global__ void __launch_bounds__(256) jet_hi_reduce_kernel(const float* __restrict__ slab, int ks, int Pst,
+                                                            const float* __restrict__ vslab, int nwg, int Vst, int ntb,
+                                                            NetDims d, float* __restrict__ grad) {
+  if ((int)blockIdx.x < ntb)
+    hi_tile_reduce(blockIdx.x, slab, ks, Pst, d, grad);
+  else
+    hi_vec_reduce(blockIdx.x - ntb, vslab, nwg, Vst, d, grad);
 }
 
 namespace {
@@ -978,12 +988,10 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   rc = hi_wgrad(N, d, sp, Z + A, Z + 2 * A, work, Pst, ks, st);
   if (rc) return rc;
   const int ntile = off_layer(d, n_hidden) - off_layer(d, 1);
-  if (ntile > 0) {
-    hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3((ntile + 255) / 256), dim3(256), 0, st, work, ks, Pst, d, grad);
-    TDQ_CHECK_LAUNCH();
-  }
+  const int ntb = (ntile + 255) / 256;
   const int ncol = (n_hidden + d_in) * HI_W + HI_W * TDQ_MAXO + TDQ_MAXO;
-  hipLaunchKernelGGL(jet_hi_vreduce_kernel, dim3((ncol + 3) / 4), dim3(256), 0, st, vslab, nwg, hi_vrow(d), d, grad);
+  hipLaunchKernelGGL(jet_hi_reduce_kernel, dim3(ntb + (ncol + 3) / 4), dim3(256), 0, st, work, ks, Pst, vslab, nwg,
+                     hi_vrow(d), ntb, d, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
