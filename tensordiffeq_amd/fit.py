@@ -684,6 +684,8 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
     # ROCm 7.2.
     place = os.environ.get("TDQ_HI_PLACE", "serial_before")
     hs = hop.stream if (hop is not None and place.startswith("side")) else None
+    if place == "cross" and len(ranges) != 2:
+        place = "serial_before"
     bwd_first = place.endswith("before")
     if hs is not None:
         hs.wait_stream(cur)
@@ -712,9 +714,31 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
     # hardware queues of its branches itself, and the join still waits ~9 us across queues)
     for st in streams[:len(ranges)]:
         st.wait_stream(cur)
-    for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
-        with torch.cuda.stream(st):
-            chain(k, lo, hi, b0, nb, st)
+    if place == "cross" and hop is not None and len(ranges) == 2:
+        # high-order forward at the head of range 1's branch (range 0 waits for it before its loss),
+        # their gradient on range 0's branch between its loss and its backward: the two pieces on
+        # the two branches, still two branches (captured in dependency order)
+        (lo0, hi0, b00, nb0), (lo1, hi1, b01, nb1) = ranges
+        st0, st1 = streams[0], streams[1]
+        with torch.cuda.stream(st1):
+            hop.forward(J, flat)
+        with torch.cuda.stream(st0):
+            jet_hip.forward_range(saved, J, lo0, hi0)
+        st0.wait_stream(st1)   # (st1 holds only the high-order forward so far)
+        with torch.cuda.stream(st0):
+            fop.run_range(J, b00, nb0)
+            hop.backward(fop.dJ, flat)
+            jet_hip.backward_range(saved, fop.dJ, work, lo0, hi0)
+            if prereduce:
+                jet_hip.slab_prereduce(saved, work, 0, prereduce)
+        with torch.cuda.stream(st1):
+            jet_hip.forward_range(saved, J, lo1, hi1)
+            fop.run_range(J, b01, nb1)
+            jet_hip.backward_range(saved, fop.dJ, work, lo1, hi1)
+    else:
+        for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
+            with torch.cuda.stream(st):
+                chain(k, lo, hi, b0, nb, st)
     for st in streams[:len(ranges)]:
         cur.wait_stream(st)
     return saved, work
