@@ -866,9 +866,10 @@ __device__ __forceinline__ void bwd_hidden_d(const bf16x8 (&zh)[S][WT / 2], cons
 #ifndef TDQ_BWD_WIDE
 #define TDQ_BWD_WIDE 1
 #endif
-// WT = 16: dK column tiles per pass (of a wave's 8; -DTDQ_W16_NCP for A/B runs)
+// WT = 16: dK column tiles per pass (of a wave's 8): 4 (two passes) 0.945 ms vs 2 (four passes) 1.035 ms per
+// width-256 AC step (profiles/r4v_w256_ncp_ab.jsonl); -DTDQ_W16_NCP for A/B runs
 #ifndef TDQ_W16_NCP
-#define TDQ_W16_NCP 2
+#define TDQ_W16_NCP 4
 #endif
 // (wide plans: 4 waves - an 8-wave workgroup puts two waves on each SIMD, 256 registers each)
 __host__ __device__ constexpr int bwd_waves(int WT, bool lo, int S) {
