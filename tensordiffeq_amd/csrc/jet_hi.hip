@@ -1,4 +1,5 @@
-// High-order Taylor jets (any multi-index up to order 4) of a tanh MLP on SMALL point sets, fp32.
+// High-order Taylor jets (any multi-index up to order 4) of a tanh MLP on SMALL point sets: fp32
+// elementwise work, split-bf16 (bf16x3) MFMA layer GEMMs, fp32 MFMA weight gradients.
 //
 // Why a separate kernel: the fused jet kernels (jet_bf3.h) carry value, first- and second-order
 // streams only, with the post-activation identities of the order-2 tanh jet.  The reference's
@@ -22,9 +23,10 @@
 //
 // Kernels (a few hundred points: latency, not bandwidth, is the budget):
 //   * forward: workgroup = 512 threads = 4 points, thread (f, g) owns feature f of point g; one
-//     layer's weights in LDS (row stride 132: W[k][f] along f and float4 rows W[f][o..o+3] are
-//     conflict-free), the points' activations in LDS as GEMM operand (float4 broadcasts); the next
-//     layer's weights load into registers during this layer's GEMM.
+//     layer's weights and the points' activations in LDS, the layer GEMM on bf16x3 MFMA tiles
+//     (hi_mma: rows point x stream, wave w = 16 output columns); the next layer's weights load
+//     into registers during this layer's GEMM (zero padding applied at the LDS store, so nothing
+//     waits for them before it).
 //   * adjoint chain (same layout): zb_i = tanh-jet adjoint of hb_i, hb_{i-1} = W_i zb_i -> B.
 //   * weight gradients: dK_i = H_{i-1}^T B_i as 32 x 32 tiles over point splits (one slab row per
 //     split); the vector parameters (biases, K0, Ko, bo) summed per workgroup by the chain itself
@@ -35,7 +37,8 @@
 // univariate chain u, u_v, u_vv, u_vvv(, u_vvvv) of the reference's periodic BCs - has its tanh jet
 // and adjoint as straight-line code; other plans interpret the partition table.
 // History (AC-baseline, 402 points, order 4; profiles/): interpreted 256-thread first build
-// 0.31 + 0.40 ms per step; this layout 26 + 57 us isolated (profiles/r4g_kernel_stats_hi_isolated.txt).
+// 0.31 + 0.40 ms per step; this layout 26 + 57 us isolated (profiles/r4g_kernel_stats_hi_isolated.txt);
+// MFMA layer GEMMs: chain -16 %, forward -7 % of workgroup cycles (profiles/r4x_hi_phase_stamps_mfma.txt).
 #include "jet_common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -208,11 +211,13 @@ __device__ __forceinline__ void hi_tanh_b(const HiSpec& sp, const float (&z)[S],
 }
 
 // LDS of the forward / adjoint-chain kernels (floats, dynamic, sized per launch):
-//   W [HI_W][HI_WS]          one layer's weights (row stride 132: float4 rows W[k][4 f4..] and
-//                            W[k][o..o+3] of the k-split GEMMs are conflict-free)
-//   A [HI_NP][S][HI_AS]      the workgroup's activations / adjoints (float4 broadcasts)
-//   R [HI_NP][S][4][HI_AS]   k-split GEMM partials: four k-quarters per output, summed in order
+//   W [HI_W][HI_WS]          one layer's weights (row stride 132: the 8-float MFMA fragment rows
+//                            of 16 lanes land on distinct banks)
+//   A [HI_NP][S][HI_AS]      the workgroup's activations / adjoints (MFMA A rows)
+//   R [HI_MR][HI_AS]         GEMM product (rows point * S + stream; both 16-row MFMA tiles)
 //   V [HI_TG][nvs][HI_W]     (chain) vector-parameter partials (nvs slots, hi_nvs)
+constexpr int HI_MR = 32;  // GEMM rows: HI_NP points x at most HI_MAXS streams
+static_assert(HI_NP * HI_MAXS <= HI_MR, "two 16-row MFMA tiles cover the workgroup's rows");
 struct HiLds {
   float* W;
   float* A;
@@ -221,10 +226,9 @@ struct HiLds {
   int S;
   __device__ float& w(int k, int f) const { return W[k * HI_WS + f]; }
   __device__ float& a(int p, int s, int k) const { return A[(p * S + s) * HI_AS + k]; }
-  __device__ float& r(int p, int s, int q, int f) const { return R[((p * S + s) * 4 + q) * HI_AS + f]; }
 };
 __host__ __device__ inline size_t hi_lds_floats(int S, int nvs) {
-  return (size_t)HI_W * HI_WS + (size_t)HI_NP * S * HI_AS * 5 + (size_t)HI_TG * nvs * HI_W;
+  return (size_t)HI_W * HI_WS + (size_t)(HI_NP * S + HI_MR) * HI_AS + (size_t)HI_TG * nvs * HI_W;
 }
 __device__ inline HiLds hi_lds_map(float* base, int S) {
   HiLds L;
@@ -232,7 +236,7 @@ __device__ inline HiLds hi_lds_map(float* base, int S) {
   L.W = base;
   L.A = L.W + HI_W * HI_WS;
   L.R = L.A + HI_NP * S * HI_AS;
-  L.V = L.R + HI_NP * S * 4 * HI_AS;
+  L.V = L.R + HI_MR * HI_AS;
   return L;
 }
 
@@ -274,7 +278,8 @@ __device__ __forceinline__ void hi_get_w(HiWRegs& r, const float* __restrict__ P
   const float* K = P + off_layer(d, layer);
   const int win = hw(d, layer - 1), wout = hw(d, layer);
   // one uniform branch around each whole batch (a branch per piece makes the compiler wait for
-  // every load at the join)
+  // every load at the join); clamped addresses, the zero padding is hi_put_w's (a select here would
+  // wait for the loads before the GEMM they are meant to overlap)
   if (((off_layer(d, layer) | wout) & 3) == 0) {
 #pragma unroll
     for (int u = 0; u < HI_WQ; ++u) {
@@ -282,30 +287,25 @@ __device__ __forceinline__ void hi_get_w(HiWRegs& r, const float* __restrict__ P
       const int kc = k < win ? k : win - 1, cc = c < wout ? c : wout - 4;
       r.q[u] = *reinterpret_cast<const f32x4*>(K + kc * wout + cc);
     }
-#pragma unroll
-    for (int u = 0; u < HI_WQ; ++u) {
-      const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) r.q[u][x] = (k < win && c < wout) ? r.q[u][x] : 0.f;
-    }
   } else {
 #pragma unroll
     for (int u = 0; u < HI_WQ; ++u) {
       const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
       const int kc = k < win ? k : win - 1;
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int cx = c + x < wout ? c + x : wout - 1;
-        r.q[u][x] = ldm(K + kc * wout + cx, k < win && c + x < wout);
-      }
+      for (int x = 0; x < 4; ++x) r.q[u][x] = K[kc * wout + (c + x < wout ? c + x : wout - 1)];
     }
   }
 }
-__device__ __forceinline__ void hi_put_w(const HiLds& L, const HiWRegs& r) {
+__device__ __forceinline__ void hi_put_w(const HiLds& L, const HiWRegs& r, const NetDims& d, int layer) {
+  const int win = hw(d, layer - 1), wout = hw(d, layer);
 #pragma unroll
   for (int u = 0; u < HI_WQ; ++u) {
     const int e = threadIdx.x + HI_THREADS * u, k = e >> 5, c = (e & 31) * 4;
-    *reinterpret_cast<f32x4*>(&L.w(k, c)) = r.q[u];
+    f32x4 v;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) v[x] = (k < win && c + x < wout) ? r.q[u][x] : 0.f;
+    *reinterpret_cast<f32x4*>(&L.w(k, c)) = v;
   }
 }
 
@@ -315,28 +315,72 @@ __device__ __forceinline__ size_t hi_row(int layer, int n, int s, int S, int N) 
   return (((size_t)layer * N + n) * S + s) * HI_W;
 }
 
-// k-split GEMM step of thread (p, f4, ks): out[s][c] (c < 4) += sum over its k of in[p][s][k] *
-// W[k][4 f4 + c] - the k of quarter ks are 16 j + 4 ks + [0, 4) (interleaved: the float4 W rows
-// of one lane group then fall on 16 distinct bank quads)
-template <int S>
-__device__ __forceinline__ void hi_gemm_fwd(const HiLds& L, int p, int f4, int ks, int kin, f32x4 (&acc)[S]) {
+// Layer GEMMs on bf16x3 MFMA (v_mfma_f32_16x16x32_bf16; fp32 operands split into bf16 hi + lo,
+// products hi*hi + hi*lo + lo*hi, fp32 accumulation - the split-bf16 family of the fused kernels,
+// ~1e-5 relative).  Rows m = point * S + stream (at most 32: two 16-row tiles, rows >= 4 S zero);
+// wave w owns the 16 output columns [16 w, 16 w + 16).  Lane l: A[row l & 15][k = 8 (l >> 4) + j],
+// B[k][col l & 15], C[4 (l >> 4) + r][l & 15].  The product lands in R as [m][HI_AS].
+typedef __bf16 hbf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void hi_split(const float (&x)[8], hbf16x8& h, hbf16x8& lo) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nj = (kin + 15) >> 4;
-#pragma unroll 2
-  for (int j = 0; j < nj; ++j) {
-    const int k0 = 16 * j + 4 * ks;
-    f32x4 a[S], w[4];
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 hx = (__bf16)x[j];
+    h[j] = hx;
+    lo[j] = (__bf16)(x[j] - (float)hx);
+  }
+}
+__device__ __forceinline__ f32x4 hi_mma3(const hbf16x8& ah, const hbf16x8& al, const hbf16x8& bh, const hbf16x8& bl,
+                                         f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+}
+// A rows of the workgroup (L.A is [m][HI_AS]); rows past 4 S read as zero
+__device__ __forceinline__ void hi_arow(const HiLds& L, int m, int k0, int S, float (&x)[8]) {
+  const bool in = m < HI_NP * S;
+  const float* a = L.A + (in ? m : 0) * HI_AS + k0;
+  const f32x4 u = *reinterpret_cast<const f32x4*>(a), v = *reinterpret_cast<const f32x4*>(a + 4);
 #pragma unroll
-    for (int s = 0; s < S; ++s) a[s] = *reinterpret_cast<const f32x4*>(&L.a(p, s, k0));
+  for (int j = 0; j < 4; ++j) {
+    x[j] = in ? u[j] : 0.f;
+    x[4 + j] = in ? v[j] : 0.f;
+  }
+}
+// TRANS = false (forward): out[m][c] = sum_k A[m][k] W[k][c]; true (adjoint chain): out[m][c] =
+// sum_o A[m][o] W[c][o]
+template <bool TRANS>
+__device__ __forceinline__ void hi_mma(const HiLds& L, int S, int kin) {
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, p = l & 15, g = l >> 4, col = 16 * wv + p;
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+  const int nk = (kin + 31) >> 5;
+  for (int kk = 0; kk < nk; ++kk) {
+    const int k0 = 32 * kk + 8 * g;
+    float a0[8], a1[8], w[8];
+    hi_arow(L, p, k0, S, a0);
+    hi_arow(L, 16 + p, k0, S, a1);
+    if constexpr (TRANS) {
+      const float* r = &L.w(col, k0);
+      const f32x4 u = *reinterpret_cast<const f32x4*>(r), v = *reinterpret_cast<const f32x4*>(r + 4);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[c] = *reinterpret_cast<const f32x4*>(&L.w(k0 + c, 4 * f4));
+      for (int j = 0; j < 4; ++j) {
+        w[j] = u[j];
+        w[4 + j] = v[j];
+      }
+    } else {
 #pragma unroll
-    for (int s = 0; s < S; ++s)
+      for (int j = 0; j < 8; ++j) w[j] = L.w(k0 + j, col);
+    }
+    hbf16x8 a0h, a0l, a1h, a1l, wh, wl;
+    hi_split(a0, a0h, a0l);
+    hi_split(a1, a1h, a1l);
+    hi_split(w, wh, wl);
+    c0 = hi_mma3(a0h, a0l, wh, wl, c0);
+    c1 = hi_mma3(a1h, a1l, wh, wl, c1);
+  }
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) acc[s][x] = fmaf(a[s][c], w[c][x], acc[s][x]);
+  for (int r = 0; r < 4; ++r) {
+    L.R[(4 * g + r) * HI_AS + col] = c0[r];
+    L.R[(16 + 4 * g + r) * HI_AS + col] = c1[r];
   }
 }
 
@@ -351,7 +395,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
   const HiLds L = hi_lds_map(hi_lds, S);
   HI_TS_DECL
   HI_TS()
-  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7, f4 = (t >> 2) & 31, ks = t & 3;
+  const int t = threadIdx.x, f = t & (HI_W - 1), pg = t >> 7;
   const int Lh = d.n_hidden;
   const int m0 = blockIdx.x * HI_NP + pg;
   const bool ok = m0 < N;
@@ -388,23 +432,20 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       z[s] = sp.order[s] == 1 ? k1 : 0.f;
     }
   }
-  if (Lh > 1) hi_put_w(L, wr);
+  if (Lh > 1) hi_put_w(L, wr, d, 1);
   HI_TS()
   for (int i = 0; i < Lh; ++i) {
     const int wi = hw(d, i);
     if (i >= 1) {  // z_i = h_{i-1} W_i (+ b_i); W_{i+1} loads in flight meanwhile
       if (i + 1 < Lh) hi_get_w(wr, P, d, i + 1);
-      const float b = ldm(P + off_layer(d, i) + hw(d, i - 1) * wi + (f < wi ? f : wi - 1), f < wi);
-      f32x4 acc[S];
-      hi_gemm_fwd<S>(L, pg, f4, ks, hw(d, i - 1), acc);
+      float b = P[off_layer(d, i) + hw(d, i - 1) * wi + (f < wi ? f : wi - 1)];  // masked after the GEMM
+      hi_mma<false>(L, S, hw(d, i - 1));
       HI_TS()
+      __syncthreads();  // z in R; every GEMM read of A / W done
+      b = f < wi ? b : 0.f;
 #pragma unroll
-      for (int s = 0; s < S; ++s) *reinterpret_cast<f32x4*>(&L.r(pg, s, ks, 4 * f4)) = acc[s];
-      __syncthreads();  // partials in R; every GEMM read of A / W done
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        z[s] = ((L.r(pg, s, 0, f) + L.r(pg, s, 1, f)) + (L.r(pg, s, 2, f) + L.r(pg, s, 3, f))) + (s == 0 ? b : 0.f);
-      if (i + 1 < Lh) hi_put_w(L, wr);
+      for (int s = 0; s < S; ++s) z[s] = L.R[(pg * S + s) * HI_AS + f] + (s == 0 ? b : 0.f);
+      if (i + 1 < Lh) hi_put_w(L, wr, d, i + 1);
       HI_TS()
     }
     {
@@ -505,8 +546,7 @@ __device__ __forceinline__ void hi_vsum(const HiLds& L, float* __restrict__ vrow
 // adjoint chain: hb of the last hidden layer from dJ, then zb_i = tanh-jet adjoint, hb_{i-1} = W_i zb_i;
 // zb_i -> Bb (the hidden-to-hidden kernels' gradients are jet_hi_wgrad_kernel's); the vector
 // parameters' gradients are summed over the workgroup's points here -> vslab row blockIdx.x.
-// Thread t: point p = t >> 7; GEMM role: output quad k4 = (t >> 2) & 31 (outputs k4 + 32 c) over
-// o-quarter ks = t & 3 (o = 64 m + 16 ks + [0, 16)); elementwise role: feature f = k4 + 32 ks.
+// Thread t: point p = t >> 7, feature f = t & 127; the GEMM is hi_mma's (wave w: columns 16 w ..).
 template <int S, bool CH>
 __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) jet_hi_chain_kernel(int N, const float* __restrict__ P, NetDims d,
                                                                   HiSpec sp, const float* __restrict__ X,
@@ -517,7 +557,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
   const HiLds L = hi_lds_map(hi_lds, S);
   HI_TS_DECL
   HI_TS()
-  const int t = threadIdx.x, pg = t >> 7, k4 = (t >> 2) & 31, ks = t & 3, f = k4 + 32 * ks;
+  const int t = threadIdx.x, pg = t >> 7, f = t & (HI_W - 1);
   const int Lh = d.n_hidden, dout = d.d_out, din = d.d_in, nvs = hi_nvs(d);
   const int m0 = blockIdx.x * HI_NP + pg;
   const bool ok = m0 < N;
@@ -529,6 +569,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
   float* vrow = vslab + (size_t)blockIdx.x * hi_vrow(d);
   float hb[S], z[S];
   float vo[TDQ_MAXO], vbo[TDQ_MAXO];  // Ko / bo partials of this thread's point
+  float xv[TDQ_MAXD];
   {
     float ko[TDQ_MAXO];
 #pragma unroll
@@ -542,6 +583,10 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       for (int q = 0; q < TDQ_MAXO; ++q) u[s][q] = dJ[((size_t)orow * ldJ + j0 + n) * dout + (q < dout ? q : 0)];
       z[s] = Zb[hi_row(Lh - 1, n, s, S, N) + f];
     }
+    // the input point (K0 partials of the last step; loaded here: a load inside the loop's exit
+    // branch makes the waitcnt pass wait for it on every iteration's GEMM)
+#pragma unroll
+    for (int v = 0; v < TDQ_MAXD; ++v) xv[v] = X[(size_t)n * din + (v < din ? v : din - 1)];
     // every load above in flight before the first use (the scheduler otherwise interleaves each load
     // with its use: one memory latency per load); masks applied after
     __builtin_amdgcn_sched_barrier(0);
@@ -591,10 +636,6 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       float* V = L.V + pg * nvs * HI_W;
       V[f] = ok ? zb[0] : 0.f;
       if (i == 0) {
-        float xv[TDQ_MAXD];
-#pragma unroll
-        for (int v = 0; v < TDQ_MAXD; ++v) xv[v] = X[(size_t)n * din + (v < din ? v : din - 1)];
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int v = 0; v < TDQ_MAXD; ++v) {
           float g = xv[v] * zb[0];
@@ -620,8 +661,8 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
       HI_TS()
       break;
     }
-    // hb_{i-1}[k] = sum_o zb_i[o] W_i[k][o] (k-split over o); the next pre-activations load meanwhile
-    hi_put_w(L, wr);
+    // hb_{i-1}[k] = sum_o zb_i[o] W_i[k][o]; the next pre-activations load meanwhile
+    hi_put_w(L, wr, d, i);
     __syncthreads();
     HI_TS()
     hi_vsum(L, vrow, d, i, pg, f);
@@ -630,38 +671,12 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int s = 0; s < S; ++s) z[s] = Zb[hi_row(i - 1, n, s, S, N) + f];  // used (masked) after the GEMM
     __builtin_amdgcn_sched_barrier(0);
-    {
-      f32x4 acc[S];  // acc[s][c]: output k4 + 32 c
-#pragma unroll
-      for (int s = 0; s < S; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int jj = 0; jj < 8; ++jj) {
-        const int o = 64 * (jj >> 2) + 16 * ks + 4 * (jj & 3);
-        f32x4 g[S], w[4];
-#pragma unroll
-        for (int s = 0; s < S; ++s) g[s] = *reinterpret_cast<const f32x4*>(&L.a(pg, s, o));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) w[c] = *reinterpret_cast<const f32x4*>(&L.w(k4 + 32 * c, o));
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            acc[s][c] = fmaf(g[s][0], w[c][0], fmaf(g[s][1], w[c][1], fmaf(g[s][2], w[c][2], fmaf(g[s][3], w[c][3], acc[s][c]))));
-      }
-      // partial of output k = k4 + 32 c -> R at column k + (k >> 5) (the four quarters' lanes of one
-      // output on distinct banks when summed)
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) L.r(pg, s, ks, k4 + 33 * c) = acc[s][c];
-    }
+    hi_mma<true>(L, S, wi);
     HI_TS()
-    __syncthreads();  // partials in R; GEMM reads of A / W done
+    __syncthreads();  // hb in R; GEMM reads of A / W done
     {
-      const int fr = f + (f >> 5);
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        hb[s] = (L.r(pg, s, 0, fr) + L.r(pg, s, 1, fr)) + (L.r(pg, s, 2, fr) + L.r(pg, s, 3, fr));
+      for (int s = 0; s < S; ++s) hb[s] = L.R[(pg * S + s) * HI_AS + f];
       if (f >= wp) {
 #pragma unroll
         for (int s = 0; s < S; ++s) hb[s] = z[s] = 0.f;

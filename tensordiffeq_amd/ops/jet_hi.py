@@ -51,7 +51,7 @@ def build_spec(plan_hi, out_rows):
 
 
 def eligible(net, plan_hi):
-    """Whether the kernels take this network / high-order plan (fp32 VALU, widths <= 128)."""
+    """Whether the kernels take this network / high-order plan (split-bf16 MFMA layer GEMMs, widths <= 128)."""
     from ..models.networks import TanhMLP
     if not isinstance(net, TanhMLP):
         return False, "network is not a TanhMLP"

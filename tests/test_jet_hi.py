@@ -54,7 +54,9 @@ def _ref_fp64(net, X, plan, dJ):
 ])
 def test_hi_kernels_match_fp64_jet(sizes, reqs, n):
     """Every stream row of the forward and the parameter gradient of <dJ, J> vs the fp64 torch jet
-    (relative error per stream < 2e-5 forward, < 1e-4 gradient; fp32 VALU kernels)."""
+    (relative error per stream < 1e-4 forward and gradient: the layer GEMMs are split-bf16 (bf16x3)
+    MFMA, the precision of the main kernels this path runs beside; ~1e-5 typical, mixed-variable
+    streams with cancellation up to ~5e-5)."""
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     net = TanhMLP(sizes, device=dev)
@@ -73,7 +75,7 @@ def test_hi_kernels_match_fp64_jet(sizes, reqs, n):
     for s, mi in enumerate(plan.streams):
         err = ((J[s].double() - Jr[s]).norm() / Jr[s].norm().clamp_min(1e-30)).item()
         print(f"HI fwd {sizes} stream {mi}: {err:.2e}")
-        assert err < 2e-5, (mi, err)
+        assert err < 1e-4, (mi, err)
     gerr = ((g.double() - gr).norm() / gr.norm()).item()
     print(f"HI grad {sizes}: {gerr:.2e}")
     assert gerr < 1e-4
