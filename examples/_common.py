@@ -76,6 +76,12 @@ def report(name, res, quiet=False, model=None):
     if model is not None:
         prog = model.program()
         res["backend"] = prog.backend
+        fi = getattr(model, "fit_info", None) or {}
+        adam = fi.get("adam") or {}
+        if adam.get("steps"):   # wall time of the Adam phase per step (graph capture included)
+            res["adam_ms_per_step"] = 1e3 * float(adam["wall_s"]) / int(adam["steps"])
+        if fi.get("lbfgs"):
+            res["lbfgs_iters"] = int(fi["lbfgs"].get("n_iter", 0))
     if not quiet:
         print(f"[{name}] " + ", ".join(f"{k}={v:.4e}" if isinstance(v, float) else f"{k}={v}"
                                        for k, v in res.items()))
