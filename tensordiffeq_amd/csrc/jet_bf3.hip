@@ -213,12 +213,8 @@ __device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti)
   }
 }
 
-#ifndef TDQ_TAIL_ELEM
-#define TDQ_TAIL_ELEM 1
-#endif
-
-#if TDQ_TAIL_ELEM
-// Adam over every group, one ELEMENT per thread (args.start in elements); group 0 = theta, whose
+// Adam over every group, one ELEMENT per thread (args.start in elements; float4 slots per thread
+// measured ~2 us slower per step, profiles/r2_v10_ab_tail_elem.jsonl); group 0 = theta, whose
 // gradient is the second slab pass of its column (the f32x4 pass's summation order, so the
 // result is bit-identical) plus gx[e] when given (the high-order points' gradient, jet_hi.hip),
 // written to args.grp[0].g as well
@@ -257,73 +253,6 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
     if (th && ti.fimg != nullptr) scatter_param(p, (int)e, ti);
   }
 }
-#else
-// (TDQ_TAIL_ELEM=0: float4 slots per thread, measured ~2 us slower per step: profiles/r2_v10_ab_tail_elem.jsonl)
-// Adam over every group; group 0 = theta, whose gradient is the second slab pass of its float4
-// column (slot == column), written to args.grp[0].g as well
-__global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const float* __restrict__ part, int Pst,
-                                                        int chunks, const int* __restrict__ improved,
-                                                        float* __restrict__ snap, TailImg ti,
-                                                        const float* __restrict__ gx) {
-  const bool do_snap = snap != nullptr && *improved != 0;
-  const int64_t total = args.start[args.ngroups];
-  for (int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x; slot < total; slot += (int64_t)gridDim.x * 256) {
-    const int gi = adam_group_of(args, slot);
-    const AdamGroup gr = args.grp[gi];
-    const int64_t e0 = (slot - args.start[gi]) * 4;
-    const float sg = gr.sign, b1 = gr.b1, b2 = gr.b2, eps = gr.eps;
-    const float lr_t = adam_lr_t(gr);
-    const bool th = gi == 0;
-    float* gout = const_cast<float*>(gr.g);
-    const bool red = th && part != nullptr;  // theta gradient from the slab partials (else: gr.g)
-    f32x4 g = zero4();
-    if (red) {
-      g = slab_reduce2_sum(part, Pst, chunks, (int)slot);
-      if (gx != nullptr)
-        for (int c = 0; c < 4; ++c)
-          if (e0 + c < gr.n) g[c] += gx[e0 + c];
-    }
-    const bool aligned = ((((uintptr_t)gr.p) | ((uintptr_t)gr.g) | ((uintptr_t)gr.m) | ((uintptr_t)gr.v)) & 15) == 0;
-    if (aligned && e0 + 4 <= gr.n) {
-      f32x4 p = *reinterpret_cast<const f32x4*>(gr.p + e0);
-      if (do_snap && th) *reinterpret_cast<f32x4*>(snap + e0) = p;
-      if (red) *reinterpret_cast<f32x4*>(gout + e0) = g;
-      else g = *reinterpret_cast<const f32x4*>(gr.g + e0);
-      f32x4 m = *reinterpret_cast<const f32x4*>(gr.m + e0);
-      f32x4 v = *reinterpret_cast<const f32x4*>(gr.v + e0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float pc = p[c], mc = m[c], vc = v[c];
-        adam_elem(pc, sg * g[c], mc, vc, b1, b2, eps, lr_t);
-        p[c] = pc; m[c] = mc; v[c] = vc;
-      }
-      *reinterpret_cast<f32x4*>(gr.p + e0) = p;
-      *reinterpret_cast<f32x4*>(gr.m + e0) = m;
-      *reinterpret_cast<f32x4*>(gr.v + e0) = v;
-      if (th && ti.fimg != nullptr) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) scatter_param(p[c], (int)(e0 + c), ti);
-      }
-    } else {
-      for (int c = 0; c < 4; ++c) {
-        const int64_t e = e0 + c;
-        if (e < gr.n) {
-          if (do_snap && th) snap[e] = gr.p[e];
-          float gc;
-          if (red) {
-            gc = g[c];
-            gout[e] = gc;
-          } else {
-            gc = gr.g[e];
-          }
-          adam_elem(gr.p[e], sg * gc, gr.m[e], gr.v[e], b1, b2, eps, lr_t);
-          if (th && ti.fimg != nullptr) scatter_param(gr.p[e], (int)e, ti);
-        }
-      }
-    }
-  }
-}
-#endif
 
 namespace {
 
@@ -528,7 +457,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
       n_terms < 0 || n_scal < 0)
     return (int)hipErrorInvalidValue;
   AdamArgs args;
-  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, TDQ_TAIL_ELEM != 0))
+  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, true))
     return (int)hipErrorInvalidValue;
   const int Ptot = param_count(d);
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
@@ -663,7 +592,7 @@ int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   AdamArgs args;
-  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, TDQ_TAIL_ELEM != 0))
+  if (!adam_args_fill(args, reinterpret_cast<const AdamGroup*>(groups), ngroups, true))
     return (int)hipErrorInvalidValue;
   if (args.grp[0].n != param_count(d)) return (int)hipErrorInvalidValue;
   TailImg ti{nullptr, nullptr, nullptr, d, WT};
