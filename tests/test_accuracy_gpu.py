@@ -72,19 +72,21 @@ def test_helmholtz_steady_state_reference_schedule_l2():
 def test_ac_discovery_recovers_coefficients():
     """AC-discovery (examples/AC-discovery.py) on the full AC.mat field: Adam 10k (the reference
     schedule, SA collocation weights) + 15k L-BFGS over network and coefficients (truth c1 = 1e-4,
-    c2 = 5; the reference marks its Adam-only version "doesnt work quite yet", so parity is unpinned).
+    c2 = 5; the reference marks its Adam-only version "doesnt work quite yet", so parity is unpinned),
+    with c1 = exp(v) from v = -6 (Raissi et al.'s parametrization of a small positive coefficient;
+    the reference's raw c1 = v ends 5-11x too large: 6.1e-4, profiles/r4o_discovery_variants.txt).
 
-    c2 comes out within 2 % (measured 4.9986, 0.03 %).  c1 does not: every variant measured stays
-    5-11x too large (6.1e-4 here; fp32 kernels 8.0e-4, Adam 20k 1.2e-3 - profiles/r4o_discovery_variants.txt).
-    The data's x-grid (512 points, spacing 3.9e-3) is coarser than the interface width
-    sqrt(c1 / c2) = 4.5e-3, so the network's u_xx at the fronts is not pinned by the data and c1
-    absorbs the smoothing; the bound below only guards against regressions of that state."""
+    c2 comes out within 1 % on every seed.  c1 with the log parametrization, seeds 0-4: 4.9e-5,
+    1.31e-4, 4.2e-5, 4.5e-5, 9.1e-5 (median 51 % off, profiles/r4disc_c1_param_ab.jsonl) - the
+    data's x-grid (512 points, spacing 3.9e-3) is coarser than the interface width
+    sqrt(c1 / c2) = 4.5e-3, so u_xx at the fronts is weakly pinned by the data; the bound below is
+    the measured spread (a factor 3), a regression guard rather than the 30 % target."""
     import time
     t0 = time.perf_counter()
-    res = _example("AC-discovery").main(["--device", "cuda", "--quiet", "--newton", "15000"])
+    res = _example("AC-discovery").main(["--device", "cuda", "--quiet", "--newton", "15000", "--c1-param", "log"])
     dt = time.perf_counter() - t0
     print(f"ACCURACY discovery c1 {res['c1']:.4e} ({res['c1_rel_err']:.3f}) c2 {res['c2']:.4f} "
           f"({res['c2_rel_err']:.4f}) wall {dt:.1f} s {res.get('wall_s')} lbfgs {res.get('lbfgs')}")
     assert res["backend"] == "hip"
     assert res["c2_rel_err"] < 0.02, res
-    assert 0 < res["c1"] < 1e-3, res   # known gap: order of magnitude only (see docstring)
+    assert 3.3e-5 < res["c1"] < 3e-4, res   # factor 3 around the truth (see docstring)
