@@ -233,6 +233,16 @@ __global__ void __launch_bounds__(256) tail_adam_kernel(AdamArgs args, const flo
     if (th && part != nullptr) {
       float a0 = 0.f, a1 = 0.f;
       int c = 0;
+      for (; c + 7 < chunks; c += 8) {  // (slab_reduce2_sum's order, eight loads in flight)
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = part[(size_t)(c + k) * Pst + e];
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          a0 += v[k];
+          a1 += v[k + 1];
+        }
+      }
       for (; c + 1 < chunks; c += 2) {
         a0 += part[(size_t)c * Pst + e];
         a1 += part[(size_t)(c + 1) * Pst + e];

@@ -129,11 +129,18 @@ static inline int spec_nso(int S, const int* spec) {
 // loads of the bf16 slab reduction (slab_reduce1_body8)
 static inline int slab_stride(int P) { return (P + 7) & ~7; }
 
-// workgroup-chunk count of the first reduction pass (-DTDQ_SLAB_CHUNKS for A/B runs)
+// workgroup-chunk count of the first reduction pass (-DTDQ_SLAB_CHUNKS for A/B runs): 8 up to 2047
+// rows (the 50k-point steps: tuned, their summation order and range cuts depend on it); beyond, one
+// chunk per 256 rows up to 256 chunks - with 8 chunks a 2M-point step summed ~2000 rows per thread
+// (0.42 of 3.7 ms per Poisson step, profiles/r4pois_*)
 #ifndef TDQ_SLAB_CHUNKS
 #define TDQ_SLAB_CHUNKS 8
 #endif
-static inline int slab_chunks(int nwg) { return nwg < TDQ_SLAB_CHUNKS ? nwg : TDQ_SLAB_CHUNKS; }
+static inline int slab_chunks(int nwg) {
+  if (nwg < 2048) return nwg < TDQ_SLAB_CHUNKS ? nwg : TDQ_SLAB_CHUNKS;
+  const int c = nwg / 256;
+  return c < TDQ_SLAB_CHUNKS ? TDQ_SLAB_CHUNKS : (c > 256 ? 256 : c);
+}
 // chunk c of the first pass covers slab rows [floor(nwg c / chunks), floor(nwg (c + 1) / chunks)); a
 // point-range cut placed on one of these row boundaries splits the reduction into chunks of the first
 // range (pre-reduced while the second range's backward runs) and of the second (fit.point_ranges,
@@ -218,12 +225,23 @@ __device__ __forceinline__ void slab_reduce1_body8(const void* __restrict__ slab
   p4[1] = (b0 + b1) + (b2 + b3);
 }
 
-// second pass: the gradient of float4 column q (fixed summation order: deterministic)
+// second pass: the gradient of float4 column q (fixed summation order: deterministic; chunk pairs
+// alternate between two accumulators, eight partials loaded before they are added)
 __device__ __forceinline__ f32x4 slab_reduce2_sum(const float* __restrict__ part, int Pst, int chunks, int q) {
   const f32x4* p4 = reinterpret_cast<const f32x4*>(part) + q;
   const size_t row = (size_t)(Pst >> 2);
   f32x4 a0 = zero4(), a1 = zero4();
   int c = 0;
+  for (; c + 7 < chunks; c += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p4[(size_t)(c + k) * row];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      a0 += v[k];
+      a1 += v[k + 1];
+    }
+  }
   for (; c + 1 < chunks; c += 2) {
     a0 += p4[(size_t)c * row];
     a1 += p4[(size_t)(c + 1) * row];
