@@ -108,6 +108,8 @@ class AdamEngine:
         captured step (it writes its row through the buffer's address), so the history grows
         geometrically: repeated short ``fit`` / ``run`` calls re-capture O(log steps) times."""
         st = self.state
+        if "improved" not in st:  # allocated here, outside any graph capture
+            st["improved"] = torch.zeros((), dtype=torch.int32, device=self.device)
         need = int(st["epoch_host"]) + int(n) + 1
         if st["hist"] is None or st["hist"].shape[0] < need:
             old = 0 if st["hist"] is None else st["hist"].shape[0]
