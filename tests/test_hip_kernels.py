@@ -496,6 +496,30 @@ def test_fused_step_tail_matches_unfused(prec, problem, sizes, monkeypatch):
     assert (u1 == u2).all()
 
 
+def test_fused_step_tail_large_set_matches_unfused(monkeypatch):
+    """300k points (bf16 backward: 2344 slab rows): the slab reduction's chunk count grows past the
+    8 of the 50k-point steps (jet_common.h slab_chunks), range cuts land on the new chunk
+    boundaries - the fused step still reproduces the unfused one bit for bit, and the loss falls."""
+    from tensordiffeq_amd.ops import jet_hip
+    from tensordiffeq_amd.ops.jet_mlp import hip_config
+
+    def run(fused_tail):
+        monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
+        m = _poisson_model("bf16", n_f=300_000, sizes=(2, 50, 50, 50, 50, 1))
+        m.fit(tf_iter=20)
+        return m
+
+    a = run(True)
+    prog = a.program()
+    _, nwg, chunks, _ = jet_hip.slab_geometry(hip_config(prog.net, prog.plan, prog.precision), prog.X_all.shape[0])
+    assert nwg >= 2048 and chunks > 8, (nwg, chunks)
+    b = run(False)
+    assert torch.equal(a.u_model.flat, b.u_model.flat)
+    la = [r["Total Loss"] for r in a.losses]
+    assert la == [r["Total Loss"] for r in b.losses]
+    assert la[-1] < la[0]
+
+
 @pytest.mark.parametrize("prec", ["bf16", "bf16x3"])
 def test_fused_step_tail_discovery_matches_unfused(prec, monkeypatch):
     """DiscoveryModel (PDE coefficients as extra scalars through dscal, SA collocation weights)
