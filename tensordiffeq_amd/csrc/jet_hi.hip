@@ -985,9 +985,11 @@ int tdq_jet_hi_fwd(const float* X, int N, const float* P, int d_in, const int* w
 // backward: the adjoints dJ of the streams with out[s] >= 0 -> the flat parameter gradient `grad`
 // (adjoint chain per point group, then the weight gradients over point splits into slab rows in
 // `work`, reduced in a fixed order: deterministic)
-int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* widths, int d_out, int n_hidden,
-                   const int* spec_i, const float* spec_c, const float* dJ, int ldJ, int j0, float* Z,
-                   float* work, float* grad, void* stream) {
+// part: 0 = all, 1 = the adjoint chain only, 2 = the weight-gradient tiles + reduction only (after a
+// part-1 call on the same buffers; the two halves may run on different streams, fit.run_ranges)
+int tdq_jet_hi_bwd_part(const float* X, int N, const float* P, int d_in, const int* widths, int d_out, int n_hidden,
+                        const int* spec_i, const float* spec_c, const float* dJ, int ldJ, int j0, float* Z,
+                        float* work, float* grad, int part, void* stream) {
   NetDims d;
   HiSpec sp;
   if (!hi_dims(d, d_in, widths, d_out, n_hidden) || !hi_spec(sp, spec_i, spec_c) || !hi_lds_fits(sp.S, d))
@@ -998,9 +1000,11 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
   const size_t A = hi_act_floats(N, n_hidden);
   const int ks = hi_splits(N), nwg = (N + HI_NP - 1) / HI_NP;
   float* vslab = work + (size_t)ks * Pst;
-  int rc = hi_chain(N, P, d, sp, X, dJ, ldJ, j0, Z, Z + 2 * A, vslab, st);
-  if (rc) return rc;
-  rc = hi_wgrad(N, d, sp, Z + A, Z + 2 * A, work, Pst, ks, st);
+  if (part != 2) {
+    const int rc = hi_chain(N, P, d, sp, X, dJ, ldJ, j0, Z, Z + 2 * A, vslab, st);
+    if (rc || part == 1) return rc;
+  }
+  const int rc = hi_wgrad(N, d, sp, Z + A, Z + 2 * A, work, Pst, ks, st);
   if (rc) return rc;
   const int ntile = off_layer(d, n_hidden) - off_layer(d, 1);
   const int ntb = (ntile + 255) / 256;
@@ -1009,6 +1013,13 @@ int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* w
                      hi_vrow(d), ntb, d, grad);
   TDQ_CHECK_LAUNCH();
   return 0;
+}
+
+int tdq_jet_hi_bwd(const float* X, int N, const float* P, int d_in, const int* widths, int d_out, int n_hidden,
+                   const int* spec_i, const float* spec_c, const float* dJ, int ldJ, int j0, float* Z,
+                   float* work, float* grad, void* stream) {
+  return tdq_jet_hi_bwd_part(X, N, P, d_in, widths, d_out, n_hidden, spec_i, spec_c, dJ, ldJ, j0, Z, work, grad, 0,
+                             stream);
 }
 
 // whether the kernels' LDS takes S streams with this input / output width and depth (1) or not (0)

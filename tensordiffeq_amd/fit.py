@@ -686,8 +686,15 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
     # ROCm 7.2.
     place = os.environ.get("TDQ_HI_PLACE", "serial_before")
     hs = hop.stream if (hop is not None and place.startswith("side")) else None
-    if place == "cross" and len(ranges) != 2:
+    if place in ("cross", "split") and len(ranges) != 2:
         place = "serial_before"
+    # split: the adjoint chain between range 0's loss and backward (it needs that loss's adjoints),
+    # the weight-gradient tiles + reduction at the end of range 1's branch (which idles while the
+    # longer range 0 finishes), joined there by an event edge.  Bitwise the same step; measured
+    # 0.2196-0.2205 vs 0.2198-0.2215 ms (noise level: the tiles then steal whole CUs from range 0's
+    # backward, whose 159 KB LDS leaves no room beside it) - profiles/r4split_*; not the default
+    split = place == "split" and hop is not None
+    ev_chain = torch.cuda.Event() if split else None
     bwd_first = place.endswith("before")
     if hs is not None:
         hs.wait_stream(cur)
@@ -701,13 +708,19 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
         if k == 0 and hs is not None:
             st.wait_stream(hs)
         fop.run_range(J, b0, nb)
-        if k == 0 and hop is not None and bwd_first:
+        if k == 0 and split:
+            hop.backward(fop.dJ, flat, part=1)
+            ev_chain.record(st)
+        elif k == 0 and hop is not None and bwd_first:
             hop.backward(fop.dJ, flat)
         jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
         if k == 0 and prereduce:
             jet_hip.slab_prereduce(saved, work, 0, prereduce)
-        if k == 0 and hop is not None and not bwd_first:
+        if k == 0 and hop is not None and not bwd_first and not split:
             hop.backward(fop.dJ, flat)
+        if k == 1 and split:
+            st.wait_event(ev_chain)
+            hop.backward(fop.dJ, flat, part=2)
 
     if len(ranges) == 1:
         chain(0, *ranges[0], cur)

@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 _lock = threading.Lock()
 _lib = None
@@ -72,6 +72,7 @@ def _declare(lib):
         "tdq_jet_hi_work_floats": (L, [I, I, P, I, I]),
         "tdq_jet_hi_fwd": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P]),
         "tdq_jet_hi_bwd": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P, P, P]),
+        "tdq_jet_hi_bwd_part": (I, [P, I, P, I, P, I, I, P, P, P, I, I, P, P, P, I, P]),
         "tdq_jet_hi_limits": (I, [P]),
         "tdq_jet_hi_lds_ok": (I, [I, I, I, I]),
         # one-shot peer-memory all-reduce (csrc/peer.hip, parallel/peer.py)

@@ -110,10 +110,12 @@ class HiJetOp:
                                      _lib.ptr(self.Z), _lib.stream_ptr(self.X.device))
         _lib.check(rc, "tdq_jet_hi_fwd")
 
-    def backward(self, dJ, P):
-        """Parameter gradient of the adjoints in the extra rows of ``dJ`` -> :attr:`grad`."""
-        rc = self.lib.tdq_jet_hi_bwd(_lib.ptr(self.X), self.n_hi, _lib.ptr(P), *self._args(), _lib.ptr(dJ), self.ldJ, 0,
-                                     _lib.ptr(self.Z), _lib.ptr(self.work), _lib.ptr(self.grad),
-                                     _lib.stream_ptr(self.X.device))
-        _lib.check(rc, "tdq_jet_hi_bwd")
+    def backward(self, dJ, P, part=0):
+        """Parameter gradient of the adjoints in the extra rows of ``dJ`` -> :attr:`grad`.  ``part``:
+        0 everything; 1 the adjoint chain only; 2 the weight-gradient tiles + reduction only (after a
+        part-1 call; ``dJ`` unused) - the halves may run on different graph branches."""
+        rc = self.lib.tdq_jet_hi_bwd_part(_lib.ptr(self.X), self.n_hi, _lib.ptr(P), *self._args(), _lib.ptr(dJ),
+                                          self.ldJ, 0, _lib.ptr(self.Z), _lib.ptr(self.work), _lib.ptr(self.grad),
+                                          int(part), _lib.stream_ptr(self.X.device))
+        _lib.check(rc, "tdq_jet_hi_bwd_part")
         return self.grad
