@@ -120,13 +120,25 @@ def force_dp_requested():
     return os.environ.get("TDQ_FORCE_DP", "0") == "1"
 
 
-def _free_port():
+def free_port(lo=20000, hi=32000):
+    """A bindable 127.0.0.1 port for a rendezvous, drawn from [lo, hi) - below Linux's ephemeral
+    range (32768+), so the other ranks' outgoing connections cannot be handed the same port before
+    rank 0's store binds it (a port from bind(0) is an ephemeral one: EADDRINUSE races)."""
+    import random
     import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    rng = random.Random()
+    for _ in range(200):
+        port = rng.randrange(lo, hi)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+        return port
+    raise RuntimeError(f"no free port in [{lo}, {hi})")
+
+
+_free_port = free_port
 
 
 def launcher_env():

@@ -4,7 +4,6 @@ includes the collective warm-up stop (a rank-local clock once let ranks run diff
 DP steps)."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -17,11 +16,8 @@ SMALL = ["--steps", "3", "--warmup", "1", "--npts", "512", "--no-l2", "--min-war
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from tensordiffeq_amd.parallel.dist import free_port
+    return free_port()
 
 
 def _env():

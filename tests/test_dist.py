@@ -5,7 +5,6 @@ scaled by 1/world, one flat all-reduce) reproduces the single-process full-batch
 gradients and Adam trajectory, and that L-BFGS runs under DP.
 """
 import os
-import socket
 
 import pytest
 import torch
@@ -15,11 +14,8 @@ import tensordiffeq_amd as tdq
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from tensordiffeq_amd.parallel.dist import free_port
+    return free_port()
 
 
 def _build(dist):

@@ -6,7 +6,6 @@ loss on per-rank shards, SA weights sharded with the points, the HIP-graph captu
 flat-bucket all-reduce, and L-BFGS under DP.  Compared against a single-process full-batch run.
 """
 import os
-import socket
 
 import pytest
 import torch
@@ -19,11 +18,8 @@ N_F = 4096
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from tensordiffeq_amd.parallel.dist import free_port
+    return free_port()
 
 
 def _build(dist, world=1, precision=None, n_f=N_F):

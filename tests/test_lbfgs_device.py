@@ -8,7 +8,6 @@ the solver on the HIP path against the host-driven optimizer.
 """
 import math
 import os
-import socket
 
 import pytest
 import torch
@@ -161,11 +160,8 @@ def test_solver_device_lbfgs_matches_host(monkeypatch):
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from tensordiffeq_amd.parallel.dist import free_port
+    return free_port()
 
 
 def _dp_worker(rank, world, port, q):

@@ -6,7 +6,6 @@ kernel, the self-test and selection at start-up, graph capture of the kernel, an
 parities.  The control plane (IPC handle exchange) rides on a gloo group.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -19,14 +18,35 @@ SIZES = [1, 3, 1000, 1024, 1025, 4097, 49_408, 200_001]
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from tensordiffeq_amd.parallel.dist import free_port
+    return free_port()
 
 
-def _worker(rank, world, port, q):
+def _guard(fn, rank, world, port, q):
+    """A failing rank reports its traceback at once (the parent then stops every rank and fails)
+    instead of leaving the others waiting in the rendezvous."""
+    try:
+        fn(rank, world, port, q)
+    except BaseException:  # noqa: BLE001 - reported to the parent, then re-raised
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise
+
+
+def _collect(procs, q, timeout):
+    got = {}
+    for _ in procs:
+        r, res = q.get(timeout=timeout)
+        if "error" in res:
+            for p in procs:   # exactly the processes this test started
+                if p.is_alive():
+                    p.kill()
+            pytest.fail(f"rank {r} failed:\n{res['error']}")
+        got[r] = res
+    return got
+
+
+def _worker_body(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE="1", TDQ_PEER_TIMEOUT_S="20")
     from tensordiffeq_amd.parallel import dist as pdist
@@ -68,6 +88,10 @@ def _worker(rank, world, port, q):
     pdist.destroy()
 
 
+def _worker(rank, world, port, q):
+    _guard(_worker_body, rank, world, port, q)
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 4])
 def test_peer_allreduce_ranks_one_gpu(world):
@@ -77,7 +101,7 @@ def test_peer_allreduce_ranks_one_gpu(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=250) for _ in procs)
+    got = _collect(procs, q, 250)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -97,7 +121,7 @@ def test_peer_allreduce_ranks_one_gpu(world):
             assert np.all(got[r]["graph"][rep] == v), (rep, r)
 
 
-def _timeout_worker(rank, world, port, q):
+def _timeout_worker_body(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE="1", TDQ_PEER_TIMEOUT_S="2")
     from tensordiffeq_amd.parallel import dist as pdist
@@ -121,6 +145,10 @@ def _timeout_worker(rank, world, port, q):
     pdist.destroy()
 
 
+def _timeout_worker(rank, world, port, q):
+    _guard(_timeout_worker_body, rank, world, port, q)
+
+
 @pytest.mark.timeout(200)
 def test_peer_allreduce_times_out_instead_of_hanging():
     """A rank that never arrives: the waiting rank's kernel gives up after TDQ_PEER_TIMEOUT_S, sets
@@ -131,7 +159,7 @@ def test_peer_allreduce_times_out_instead_of_hanging():
     procs = [ctx.Process(target=_timeout_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=150) for _ in procs)
+    got = _collect(procs, q, 150)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
