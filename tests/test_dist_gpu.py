@@ -28,6 +28,17 @@ def _build(dist, world=1, precision=None, n_f=N_F):
 
 
 def _worker(rank, world, port, q, precision, peer="0"):
+    """A failing rank reports its traceback at once (the parent stops both ranks and fails)
+    instead of leaving the other waiting in a collective until the test's timeout."""
+    try:
+        _worker_body(rank, world, port, q, precision, peer)
+    except BaseException:  # noqa: BLE001 - reported to the parent, then re-raised
+        import traceback
+        q.put({"error": f"rank {rank}: " + traceback.format_exc()})
+        raise
+
+
+def _worker_body(rank, world, port, q, precision, peer):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDQ_PEER_ALLREDUCE=peer,
                       TDQ_STEP_UNROLL="4")
@@ -78,6 +89,11 @@ def test_dp_two_ranks_on_gpu_match_single_process(precision, peer):
     for p in procs:
         p.start()
     res = q.get(timeout=500)
+    if "error" in res:
+        for p in procs:   # exactly the processes this test started
+            if p.is_alive():
+                p.kill()
+        pytest.fail(res["error"])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
