@@ -38,7 +38,9 @@
 // and adjoint as straight-line code; other plans interpret the partition table.
 // History (AC-baseline, 402 points, order 4; profiles/): interpreted 256-thread first build
 // 0.31 + 0.40 ms per step; this layout 26 + 57 us isolated (profiles/r4g_kernel_stats_hi_isolated.txt);
-// MFMA layer GEMMs: chain -16 %, forward -7 % of workgroup cycles (profiles/r4x_hi_phase_stamps_mfma.txt).
+// MFMA layer GEMMs: chain -16 %, forward -7 % of workgroup cycles (profiles/r4x_hi_phase_stamps_mfma.txt);
+// A rows split once at the store instead of per wave: forward 35.0 -> 30.4k, chain 38.8 -> 33.2k cycles,
+// bit-identical (profiles/r4asplit_*; the AC-baseline step does not move: 0.221-0.224 vs 0.220-0.222 ms).
 #include "jet_common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -213,10 +215,14 @@ __device__ __forceinline__ void hi_tanh_b(const HiSpec& sp, const float (&z)[S],
 // LDS of the forward / adjoint-chain kernels (floats, dynamic, sized per launch):
 //   W [HI_W][HI_WS]          one layer's weights (row stride 132: the 8-float MFMA fragment rows
 //                            of 16 lanes land on distinct banks)
-//   A [HI_NP][S][HI_AS]      the workgroup's activations / adjoints (MFMA A rows)
+//   A 2 x [HI_NP][S][HI_AB]  the workgroup's activations / adjoints as MFMA A rows, split once into
+//                            bf16 hi and lo at the store (every wave reads the same rows)
 //   R [HI_MR][HI_AS]         GEMM product (rows point * S + stream; both 16-row MFMA tiles)
 //   V [HI_TG][nvs][HI_W]     (chain) vector-parameter partials (nvs slots, hi_nvs)
 constexpr int HI_MR = 32;  // GEMM rows: HI_NP points x at most HI_MAXS streams
+// bf16 row stride of the split A rows: 272 B = 68 words, so the 16 rows of a ds_read_b128 pass
+// (one 8-element column group) start 4 banks apart - conflict-free
+constexpr int HI_AB = 136;
 static_assert(HI_NP * HI_MAXS <= HI_MR, "two 16-row MFMA tiles cover the workgroup's rows");
 struct HiLds {
   float* W;
@@ -225,17 +231,18 @@ struct HiLds {
   float* V;
   int S;
   __device__ float& w(int k, int f) const { return W[k * HI_WS + f]; }
-  __device__ float& a(int p, int s, int k) const { return A[(p * S + s) * HI_AS + k]; }
+  __device__ __bf16* ah() const { return reinterpret_cast<__bf16*>(A); }
+  __device__ __bf16* al() const { return reinterpret_cast<__bf16*>(A) + HI_NP * S * HI_AB; }
 };
 __host__ __device__ inline size_t hi_lds_floats(int S, int nvs) {
-  return (size_t)HI_W * HI_WS + (size_t)(HI_NP * S + HI_MR) * HI_AS + (size_t)HI_TG * nvs * HI_W;
+  return (size_t)HI_W * HI_WS + (size_t)HI_NP * S * HI_AB + (size_t)HI_MR * HI_AS + (size_t)HI_TG * nvs * HI_W;
 }
 __device__ inline HiLds hi_lds_map(float* base, int S) {
   HiLds L;
   L.S = S;
   L.W = base;
   L.A = L.W + HI_W * HI_WS;
-  L.R = L.A + HI_NP * S * HI_AS;
+  L.R = L.A + HI_NP * S * HI_AB;  // (two bf16 arrays = HI_AB floats per row)
   L.V = L.R + HI_MR * HI_AS;
   return L;
 }
@@ -335,16 +342,20 @@ __device__ __forceinline__ f32x4 hi_mma3(const hbf16x8& ah, const hbf16x8& al, c
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
 }
-// A rows of the workgroup (L.A is [m][HI_AS]); rows past 4 S read as zero
-__device__ __forceinline__ void hi_arow(const HiLds& L, int m, int k0, int S, float (&x)[8]) {
+// element (m, k) of the A rows, split into bf16 hi + lo (hi_split's rounding)
+__device__ __forceinline__ void hi_put_a(const HiLds& L, int m, int k, float x) {
+  const __bf16 hx = (__bf16)x;
+  L.ah()[m * HI_AB + k] = hx;
+  L.al()[m * HI_AB + k] = (__bf16)(x - (float)hx);
+}
+// A fragment (row m, columns k0 .. k0 + 7) of the workgroup, hi and lo; rows past 4 S read as zero
+__device__ __forceinline__ void hi_arow(const HiLds& L, int m, int k0, int S, hbf16x8& h, hbf16x8& lo) {
   const bool in = m < HI_NP * S;
-  const float* a = L.A + (in ? m : 0) * HI_AS + k0;
-  const f32x4 u = *reinterpret_cast<const f32x4*>(a), v = *reinterpret_cast<const f32x4*>(a + 4);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    x[j] = in ? u[j] : 0.f;
-    x[4 + j] = in ? v[j] : 0.f;
-  }
+  const int o = (in ? m : 0) * HI_AB + k0;
+  const hbf16x8 u = *reinterpret_cast<const hbf16x8*>(L.ah() + o), v = *reinterpret_cast<const hbf16x8*>(L.al() + o);
+  const hbf16x8 z = {};
+  h = in ? u : z;
+  lo = in ? v : z;
 }
 // TRANS = false (forward): out[m][c] = sum_k A[m][k] W[k][c]; true (adjoint chain): out[m][c] =
 // sum_o A[m][o] W[c][o]
@@ -355,9 +366,10 @@ __device__ __forceinline__ void hi_mma(const HiLds& L, int S, int kin) {
   const int nk = (kin + 31) >> 5;
   for (int kk = 0; kk < nk; ++kk) {
     const int k0 = 32 * kk + 8 * g;
-    float a0[8], a1[8], w[8];
-    hi_arow(L, p, k0, S, a0);
-    hi_arow(L, 16 + p, k0, S, a1);
+    float w[8];
+    hbf16x8 a0h, a0l, a1h, a1l, wh, wl;
+    hi_arow(L, p, k0, S, a0h, a0l);
+    hi_arow(L, 16 + p, k0, S, a1h, a1l);
     if constexpr (TRANS) {
       const float* r = &L.w(col, k0);
       const f32x4 u = *reinterpret_cast<const f32x4*>(r), v = *reinterpret_cast<const f32x4*>(r + 4);
@@ -370,9 +382,6 @@ __device__ __forceinline__ void hi_mma(const HiLds& L, int S, int kin) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) w[j] = L.w(k0 + j, col);
     }
-    hbf16x8 a0h, a0l, a1h, a1l, wh, wl;
-    hi_split(a0, a0h, a0l);
-    hi_split(a1, a1h, a1l);
     hi_split(w, wh, wl);
     c0 = hi_mma3(a0h, a0l, wh, wl, c0);
     c1 = hi_mma3(a1h, a1l, wh, wl, c1);
@@ -402,7 +411,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
   const int n = ok ? m0 : N - 1;
   HiWRegs wr;
   if (Lh > 1) hi_get_w(wr, P, d, 1);
-  float z[S];
+  float z[S], hl[S];  // hl: the last hidden layer's h (output layer products)
   {  // layer 0: z = x K0 + b0 (value), K0[var] (first order), 0 (higher)
     const int w0 = hw(d, 0);
     const int fc = f < w0 ? f : w0 - 1;
@@ -464,7 +473,10 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         }
       }
 #pragma unroll
-      for (int s = 0; s < S; ++s) L.a(pg, s, f) = h[s];
+      for (int s = 0; s < S; ++s) {
+        hi_put_a(L, pg * S + s, f, h[s]);
+        hl[s] = h[s];
+      }
     }
     HI_TS()
     __syncthreads();  // A (and W) of the next GEMM written; R read
@@ -484,7 +496,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
     for (int s = 0; s < S; ++s)
 #pragma unroll
       for (int q = 0; q < TDQ_MAXO; ++q)
-        if (q < dout) part[((pg * S + s) * TDQ_MAXO + q) * HI_W + f] = L.a(pg, s, f) * ko[q];
+        if (q < dout) part[((pg * S + s) * TDQ_MAXO + q) * HI_W + f] = hl[s] * ko[q];
   }
   __syncthreads();
   for (int c = t; c < HI_NP * S * dout; c += blockDim.x) {
@@ -631,7 +643,7 @@ __global__ void __launch_bounds__(HI_THREADS) __attribute__((amdgpu_waves_per_eu
         for (int s = 0; s < S; ++s) Bb[hi_row(i, n, s, S, N) + f] = zb[s];
       }
 #pragma unroll
-      for (int s = 0; s < S; ++s) L.a(pg, s, f) = zb[s];
+      for (int s = 0; s < S; ++s) hi_put_a(L, pg * S + s, f, zb[s]);
       // vector-parameter partials of this point (padding points: zero adjoints already)
       float* V = L.V + pg * nvs * HI_W;
       V[f] = ok ? zb[0] : 0.f;
