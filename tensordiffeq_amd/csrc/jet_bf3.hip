@@ -13,7 +13,7 @@
 //                 weights snapshot, and the next step's weight images: every updated weight is
 //                 scattered straight into its forward / backward A-image (bf16 hi + lo) or aux
 //                 slot, so the next forward runs without a pack launch.
-#include "jet_bf3.h"
+#include "jet_fused.h"
 #include "optim_common.h"
 
 // A-operand images: img[layer-1][o][kb][hl][lane] = 8 bf16 (hl 0 = hi, 1 = lo)
@@ -272,6 +272,18 @@ int64_t img_floats(int WT, int n_hidden) {  // hi/lo A images, in floats
 
 int64_t aux_alloc(int d_in, int n_hidden, int W) { return ((int64_t)(d_in + n_hidden + 4) * W + 4 + 3) / 4 * 4; }
 
+int64_t stage_floats(int N, int WT, int S, int lo) {  // the wide bf16x3 plans' global fragment stage
+  const int64_t nwg = (N + 63) / 64;
+  return bf3_gstage(WT, S, lo != 0) ? nwg * 4 * stage_wave_elems(WT, S, true) * 2 : 0;
+}
+
+// gradient-slab rows of a backward over N points
+int bf3_rows(int N, const NetDims& d, int WT, int S, int lo) {
+  if (fz_active(d, WT, S, lo)) return fz_rows(N);
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S);
+  return (N + pts_b - 1) / pts_b;
+}
+
 int launch_pack(const float* P, bf16x8* fimg, bf16x8* bimg, float* aux, NetDims d, int WT, hipStream_t st) {
   const int total = 2 * (d.n_hidden - 1) * WT * (WT / 2) * 64 + aux_floats(d, 16 * WT);
   int blocks = (total + 255) / 256;
@@ -304,36 +316,36 @@ int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
 
 extern "C" {
 
-// scratch = saved post-activations Hs | forward A image | backward A image | aux image | (wide
-// bf16x3 plans) the global fragment stage (floats; -1: unsupported).  The forward packs all three
-// images in one launch; the backward reuses them.
+// scratch = forward A image | backward A image | aux image | (wide bf16x3 plans) the global
+// fragment stage | saved post-activations Hs (none when the persistent kernels of jet_fused.h
+// serve the plan: they keep every activation on chip) - floats; -1: unsupported.  The forward
+// packs all three images in one launch; the backward reuses them.
 int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, const int* widths, int n_hidden, int S, int lo) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, 1, n_hidden)) return -1;
   const int WT = width_tiles(d.width);
   if (WT < 2) return -1;
   const int64_t nwg = (N + 63) / 64;
-  const int64_t stage = bf3_gstage(WT, S, lo != 0) ? nwg * 4 * stage_wave_elems(WT, S, true) * 2 : 0;
-  return (int64_t)n_hidden * nwg * S * 4 * WT * 256 + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT) +
-         stage;
+  const int64_t hs = fz_active(d, WT, S, lo) ? 0 : (int64_t)n_hidden * nwg * S * 4 * WT * 256;
+  return hs + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT) + stage_floats(N, WT, S, lo);
 }
 
-// per-workgroup gradient slabs + reduction partials, in floats
+// per-workgroup gradient slabs + reduction partials, in floats (rows: the saved-activation
+// backward's 64-point workgroups or the persistent kernels' workgroups, whichever is more)
 int64_t tdq_jet_bf3_slab_floats(int N, int d_in, const int* widths, int d_out, int n_hidden) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return -1;
   const int WT = width_tiles(d.width);
   if (WT < 2) return -1;
-  const int nwg = (N + 63) / 64;
+  int nwg = (N + 63) / 64;
+  if (fz_rows(N) > nwg) nwg = fz_rows(N);
   const int64_t P = slab_stride(param_count(d));
   return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
 
-// image pointers inside the forward's scratch (right after the saved post-activations Hs)
-static inline void scratch_images(float* scratch, int N, int n_hidden, int S, int WT, float** img, float** bimg,
-                                  float** aux) {
-  const int64_t nwg = (N + 63) / 64;
-  *img = scratch + (int64_t)n_hidden * nwg * S * 4 * WT * 256;
+// image pointers inside the forward's scratch (at its start)
+static inline void scratch_images(float* scratch, int n_hidden, int WT, float** img, float** bimg, float** aux) {
+  *img = scratch;
   *bimg = *img + img_floats(WT, n_hidden);
   *aux = *bimg + img_floats(WT, n_hidden);
 }
@@ -342,8 +354,13 @@ static inline void scratch_images(float* scratch, int N, int n_hidden, int S, in
 static inline bf16x4* scratch_stage(float* scratch, int N, int d_in, int n_hidden, int S, int WT, int lo) {
   if (!bf3_gstage(WT, S, lo != 0)) return nullptr;
   float *img, *bimg, *aux;
-  scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+  scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
   return reinterpret_cast<bf16x4*>(aux + aux_alloc(d_in, n_hidden, 16 * WT));
+}
+
+// the saved post-activations (after the stage)
+static inline float* scratch_hs(float* scratch, int N, int d_in, int n_hidden, int S, int WT, int lo) {
+  return scratch + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT) + stage_floats(N, WT, S, lo);
 }
 
 // lo: 1 = "bf16x3" (activations split hi + lo), 0 = "bf16" (activations rounded to bf16).
@@ -366,13 +383,18 @@ int tdq_jet_fwd_bf3_range(const float* X, const float* P, float* J, float* scrat
   const int nso = spec_nso(S, spec);
   if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  float* Hs = scratch;
+  const bool fz = fz_active(d, WT, S, lo);
+  if (fz && (p_lo != 0 || p_hi != N)) return (int)hipErrorInvalidValue;  // one launch over every point
+  float* Hs = scratch_hs(scratch, N, d_in, n_hidden, S, WT, lo);
   float *img, *bimg, *aux;
-  scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+  scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
   if (pack) {
     int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
     if (rc) return rc;
   }
+  if (fz)
+    return fz_launch(0, X, aux, reinterpret_cast<const bf16x8*>(img), reinterpret_cast<const bf16x8*>(bimg), nullptr, J,
+                     nullptr, N, 0, d, sp, S, nso, st);
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
             scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), p_lo, p_hi};
   return dispatch(true, WT, S, nso, a);
@@ -396,7 +418,7 @@ int tdq_jet_bf3_pack(const float* P, float* scratch, int N, int d_in, const int*
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   float *img, *bimg, *aux;
-  scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+  scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
   return launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT,
                      reinterpret_cast<hipStream_t>(stream));
 }
@@ -419,13 +441,18 @@ int tdq_jet_bwd_bf3_range(const float* X, const float* dJ, const float* Hs, floa
   if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d);
-  // images packed by the forward into its scratch, right after Hs (see tdq_jet_bf3_scratch_floats)
+  // images packed by the forward at the start of its scratch (see tdq_jet_bf3_scratch_floats)
+  float* scr = const_cast<float*>(Hs);
   float *img, *bimg, *aux;
-  scratch_images(const_cast<float*>(Hs), N, n_hidden, S, WT, &img, &bimg, &aux);
+  scratch_images(scr, n_hidden, WT, &img, &bimg, &aux);
+  if (fz_active(d, WT, S, lo)) {  // recompute backward: activations rebuilt on chip, tile by tile
+    if (p_lo != 0 || p_hi != N) return (int)hipErrorInvalidValue;
+    return fz_launch(1, X, aux, reinterpret_cast<const bf16x8*>(img), reinterpret_cast<const bf16x8*>(bimg), dJ,
+                     nullptr, work, N, slab_stride(Ptot), d, sp, S, nso, st);
+  }
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
-  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, const_cast<float*>(Hs), work, N,
-            slab_stride(Ptot), d, sp, st, lo, scratch_stage(const_cast<float*>(Hs), N, d_in, n_hidden, S, WT, lo),
-            p_lo, p_hi};
+  Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, scratch_hs(scr, N, d_in, n_hidden, S, WT, lo),
+            work, N, slab_stride(Ptot), d, sp, st, lo, scratch_stage(scr, N, d_in, n_hidden, S, WT, lo), p_lo, p_hi};
   return dispatch(false, WT, S, nso, a);
 }
 
@@ -440,7 +467,7 @@ int tdq_jet_bwd_bf3_ex(const float* X, const float* P, const float* dJ, const fl
   NetDims d;
   make_dims(d, d_in, widths, 0, d_out, n_hidden);
   const int WT = width_tiles(d.width);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;  // slab rows
+  const int nwg_b = bf3_rows(N, d, WT, S, lo);  // slab rows
   const int Ptot = param_count(d);
   return tdq_slab_reduce_h(work, grad, nwg_b, Ptot, slab_chunks(nwg_b), (int)slab_half(lo != 0), stream);
 }
@@ -473,7 +500,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
   args.grp[0].g = grad;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
+  const int nwg_b = bf3_rows(N, d, WT, S, lo);
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -502,7 +529,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   TailImg ti{nullptr, nullptr, nullptr, d, WT};
   if (scratch != nullptr) {
     float *img, *bimg, *aux;
-    scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+    scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
     ti.fimg = reinterpret_cast<__bf16*>(img);
     ti.bimg = reinterpret_cast<__bf16*>(bimg);
     ti.aux = aux;
@@ -531,7 +558,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
     return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
+  const int nwg_b = bf3_rows(N, d, WT, S, lo);
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -560,7 +587,9 @@ int tdq_bf3_slab_geometry(int N, int d_in, const int* widths, int d_out, int n_h
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
-  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b, chunks = slab_chunks(nwg_b);
+  const bool fz = fz_active(d, WT, S, lo);
+  const int pts_b = fz ? N : 16 * bwd_waves(WT, lo != 0, S), nwg_b = bf3_rows(N, d, WT, S, lo),
+            chunks = slab_chunks(nwg_b);
   out[0] = pts_b;
   out[1] = nwg_b;
   out[2] = chunks;
@@ -579,7 +608,7 @@ int tdq_slab_prereduce_bf3(float* work, int N, int d_in, const int* widths, int 
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
   const int Ptot = param_count(d);
-  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = (N + pts_b - 1) / pts_b;
+  const int nwg_b = bf3_rows(N, d, WT, S, lo);
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c0 < 0 || c1 > chunks || c1 <= c0) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -608,7 +637,7 @@ int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_
   TailImg ti{nullptr, nullptr, nullptr, d, WT};
   if (scratch != nullptr) {
     float *img, *bimg, *aux;
-    scratch_images(scratch, N, n_hidden, S, WT, &img, &bimg, &aux);
+    scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
     ti.fimg = reinterpret_cast<__bf16*>(img);
     ti.bimg = reinterpret_cast<__bf16*>(bimg);
     ti.aux = aux;

@@ -1,0 +1,513 @@
+// Persistent point-tile jet kernels for precision "bf16" (gfx950 / MI355X): the forward of a
+// whole point set, and the RECOMPUTE backward - forward of a 32-point tile with every activation
+// kept on chip (LDS images + registers), then the reverse sweep through the same tile - with the
+// weight gradient dK of every hidden layer accumulated in MFMA accumulator registers across all
+// of a workgroup's tiles.
+//
+// Why (profiles/r3_roofline_bf16.txt): the saved-activation design streams
+// 4.35 KB per point out of the forward and back into the backward (223 + 268 MB per 50k-point
+// step) at 2-4 TB/s, with the backward at 12 % MFMA busy and two wave rounds per launch.  Here:
+//   * one workgroup (4 waves, one per SIMD, the 512-entry register file each) per CU, a static
+//     contiguous share of 32-point tiles per workgroup (deterministic summation order);
+//   * per tile, the forward writes each layer's post-activation streams into [point][feature]
+//     bf16 LDS images - the B operand of the next layer's GEMM (two ds_read_b64 per fragment in
+//     the permuted k order of the weight images) and, read transposed (ds_read_b64_tr_b16), the
+//     A operand of the backward's dK = sum_points sum_streams h_{l-1} zb_l^T;
+//   * the value stream keeps a bf16 "lo" image beside its hi image (hi + lo ~ 2^-17 relative) for
+//     the tanh-jet adjoint's s1 = 1 - h^2; the top layer stays in registers (fp32);
+//   * the reverse sweep writes each zb_l in place of h_l once every wave's dK_{l+1} has read
+//     h_l; layer 0 (input -> width, VALU) is rebuilt from x instead of being kept;
+//   * dK_l (l = 1..LM) lives in AGPR-able accumulators for the whole launch (WT = 8: 192 per
+//     lane); vector-parameter partials (biases, first / output layer) accumulate in LDS; one
+//     bf16 gradient-slab row per workgroup at the end (256 rows instead of 391 for 50k points),
+//     reduced by the existing fused step tail.
+// No saved-activation traffic at all: the backward reads x, dJ and the (L2-resident) weight images.
+// Numerics: the forward is statement-for-statement the saved-activation forward (same bf16
+// operands, same MFMA k order, same tanh jet), so J is bitwise the same; dK sums in another order.
+// Reference behaviour: the nested tf.gradients of the PDE residual and its tape.gradient
+// (tensordiffeq/models.py:116-225, fit.py:125-147).
+#pragma once
+#include "jet_bf3.h"
+
+#define FZ_PT 32  // points per tile (two 16-point MFMA column tiles; waves 0-3 / 4-7)
+#define FZ_WAVES 8
+
+__host__ __device__ constexpr int fz_nslot(int LM) { return LM < 2 ? 2 : LM; }
+// bf16 elements of the image area: slot 0 holds S streams, slots >= 1 one more (the value lo image)
+__host__ __device__ constexpr int fz_img_elems(int WT, int S, int LM) {
+  return (S + (fz_nslot(LM) - 1) * (S + 1)) * FZ_PT * bf3_img_rs(WT);
+}
+// float area after the images: aux copy | xs | ubs | (MODE 1) per-column-tile partials
+// (biases of layers 0..LM, K0, Ko), bo | (MODE 0) output-layer partial dots
+__host__ __device__ inline int fz_aux_floats(const NetDims& d, int W) { return (aux_floats(d, W) + 3) / 4 * 4; }
+__host__ __device__ inline int fz_fl_floats(const NetDims& d, int WT, int S, int LM, int mode) {
+  const int W = 16 * WT;
+  const int common = fz_aux_floats(d, W) + FZ_PT * TDQ_MAXD + S * FZ_PT * 4;
+  return common + (mode == 1 ? 2 * ((LM + 1) * W + d.d_in * W + 4 * W) + 4 : 4 * S * FZ_PT * 4);
+}
+__host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int LM, int mode) {
+  return fz_img_elems(WT, S, LM) * 2 + fz_fl_floats(d, WT, S, LM, mode) * 4;
+}
+
+// Precision bf16 forward tanh jet with e = exp(2 min(z, 15)), r = 1 / (1 + e):
+//   tanh z = 1 - 2 r,  s1 = 1 - tanh^2 z = 4 e r^2
+// (exp, rcp and ~6 FMA-class ops instead of the ~12 of tanh_s1's polynomial / select form).  s1 is
+// formed from e, not as 1 - h^2: that cancels for saturated units, whose derivative streams
+// h_a = s1 z_a then carried 4 % error at |z| = 7 (the u_x stream of J moved by 1e-2 against the
+// saved-activation kernels, gpurun_out/r5tanh).  The clamp keeps e finite (tanh(15) = 1 - 2e-13).
+// tanh's own ~6e-8 absolute error near 0 is far below the bf16 rounding every activation takes
+// before the next GEMM.  The epilogue VALU work is as large as the layer's MFMA work at width 128
+// (4 streams: 1 MFMA cycle and ~20 VALU ops per feature x point).
+#ifndef FZ_CHEAP_TANH
+#define FZ_CHEAP_TANH 1  // 0: the saved-activation kernels' tanh_jet_f (A/B builds)
+#endif
+template <int S, int NSO>
+__device__ __forceinline__ void fz_tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
+  if constexpr (!FZ_CHEAP_TANH) {
+    tanh_jet_f<S, NSO>(sp, z, h);
+    return;
+  }
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  f32x4 za[S], zb[S];
+#pragma unroll
+  for (int s = SO; s < S; ++s) {
+    za[s] = sel_first<S, S1>(z, sp.ia[s], sp.selA[s]);
+    zb[s] = sel_first<S, S1>(z, sp.ib[s], sp.selB[s]);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float e = __builtin_amdgcn_exp2f(fminf(z[0][c], 15.f) * 2.8853900817779268f);
+    const float r = __builtin_amdgcn_rcpf(1.f + e);
+    const float hv = fmaf(-2.f, r, 1.f);
+    const float s1 = (4.f * e) * (r * r);
+    const float s2 = -2.f * hv * s1;
+    h[0][c] = hv;
+#pragma unroll
+    for (int s = 1; s < SO; ++s) h[s][c] = s1 * z[s][c];
+#pragma unroll
+    for (int s = SO; s < S; ++s) h[s][c] = fmaf(s2 * za[s][c], zb[s][c], s1 * z[s][c]);
+  }
+}
+
+// Image addressing.  Element (row, feature 16 t + 4 g + e) of a [point][feature] image with row
+// stride RS lives at row * RS + ((16 t + 4 ch) ^ rsw) + e, ch = g ^ ((row >> 2) & 3) (4-column chunk
+// swizzle), rsw = 64 * bit 3 of row (64-column half swap) - the backward images' conflict-free
+// layout (jet_bf3.h).  For row = 16 q + p, (16 t + 4 ch) ^ rsw = 16 t + 4 ch + (bit 2 of t ? -rsw : rsw),
+// so every access is one of two per-lane bases plus an offset that is uniform (t) or immediate
+// (q, k-block, stream): no per-access address registers (the XOR form pinned one per access).
+struct FzLane {
+  int lo, r2;  // lane base for feature tiles with bit 2 of t clear; minus r2 (= 2 rsw) when set
+};
+template <int RS>
+__device__ __forceinline__ FzLane fz_lane(int p, int g) {
+  const int ch = g ^ ((p >> 2) & 3), rsw = (p & 8) << 3;
+  return FzLane{p * RS + 4 * ch + rsw, 2 * rsw};
+}
+template <int RS>
+__device__ __forceinline__ int fz_at(const FzLane& L, int q, int t) {
+  // (arithmetic, not a select between two members: that became an indexed scratch load)
+  return L.lo - ((t >> 2) & 1) * L.r2 + 16 * q * RS + 16 * t;
+}
+template <int RS>
+__device__ __forceinline__ void fz_put(__bf16* im, const FzLane& L, int q, int t, bf16x4 v) {
+  *reinterpret_cast<bf16x4*>(im + fz_at<RS>(L, q, t)) = v;
+}
+template <int RS>
+__device__ __forceinline__ bf16x4 fz_get(const __bf16* im, const FzLane& L, int q, int t) {
+  return *reinterpret_cast<const bf16x4*>(im + fz_at<RS>(L, q, t));
+}
+// B fragment of k-block kb (features in the weight images' permuted k order) for column tile q
+template <int RS>
+__device__ __forceinline__ bf16x8 fz_bfrag(const __bf16* im, const FzLane& L, int q, int kb) {
+  return cat8(fz_get<RS>(im, L, q, 2 * kb), fz_get<RS>(im, L, q, 2 * kb + 1));
+}
+__device__ __forceinline__ f32x4 fz_bf4(bf16x4 v) {
+  const u32x2 u = __builtin_bit_cast(u32x2, v);
+  return f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+               __uint_as_float(u[1] & 0xffff0000u)};
+}
+
+// acc[oo][s] = sum_kb A(o0 + oo, kb) B(kb, s) for the 16 points of column tile q: A from a weight
+// image in global memory (hi only, one k-block ahead), B from the LDS image `im` (S stream images of
+// FZ_PT rows; the SIMD's other wave covers the LDS latency).
+template <int WT, int S, int OPW>
+__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __restrict__ wimg, int layer, int o0,
+                                        const __bf16* im, int q, const FzLane& L, int l) {
+  constexpr int KB = WT / 2, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS, NSTEP = WT * KB;
+  const Tl Wi = tl_make(wimg + (size_t)(layer - 1) * NSTEP * 128, l);
+  bf16x8 a[2][OPW], dummy;
+#pragma unroll
+  for (int oo = 0; oo < OPW; ++oo) img_frag<false>(Wi, (o0 + oo) * KB, a[0][oo], dummy);
+#pragma unroll
+  for (int oo = 0; oo < OPW; ++oo)
+#pragma unroll
+    for (int s = 0; s < S; ++s) acc[oo][s] = zero4();
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int oo = 0; oo < OPW; ++oo) img_frag<false>(Wi, (o0 + oo) * KB + kb + 1, a[(kb + 1) & 1][oo], dummy);
+    }
+    bf16x8 b[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) b[s] = fz_bfrag<RS>(im + s * SIMG, L, q, kb);
+#pragma unroll
+    for (int oo = 0; oo < OPW; ++oo)
+#pragma unroll
+      for (int s = 0; s < S; ++s) acc[oo][s] = mfma_bf(a[kb & 1][oo], b[s], acc[oo][s]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// dK[r][c] += sum over the tile's points and streams of H^T Z (transposed LDS reads; the wave's
+// NR x NC block of 16 x 16 output tiles at row tiles r0.., column tiles c0..)
+template <int WT, int S, int NR, int NC>
+__device__ __forceinline__ void fz_dk(f32x4 (&dk)[NR][NC], const __bf16* H, const __bf16* Z, int r0, int c0, int l) {
+  constexpr int RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
+  const int g = l >> 4;
+  const int tr_row = 8 * g + ((l & 15) >> 2);
+  const int swz = (g & 1) << 6;
+  const int tr_col1 = 4 * ((l & 3) ^ ((2 * g) & 3)), tr_col2 = 4 * ((l & 3) ^ ((2 * g + 1) & 3));
+  // (16 (r0 + r) + tr_col) ^ swz = ((16 r0) ^ swz) + 16 r + tr_col as long as no carry crosses
+  // bit 6: blocks of 4 tiles start on multiples of 64 columns, blocks of 2 on multiples of 32 (and
+  // 16 r + tr_col <= 28) - one base per read, immediates after
+  static_assert((NR == 4 || NR <= 2) && (NC == 4 || NC <= 2), "fz_dk: tile blocks of 1, 2 or 4");
+  const int a1 = tr_row * RS + tr_col1 + ((16 * r0) ^ swz), a2 = (tr_row + 4) * RS + tr_col2 + ((16 * r0) ^ swz);
+  const int z1 = tr_row * RS + tr_col1 + ((16 * c0) ^ swz), z2 = (tr_row + 4) * RS + tr_col2 + ((16 * c0) ^ swz);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    bf16x8 A[NR], B[NC];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) A[r] = cat8(tr_read(H + s * SIMG + a1 + 16 * r), tr_read(H + s * SIMG + a2 + 16 * r));
+#pragma unroll
+    for (int c = 0; c < NC; ++c) B[c] = cat8(tr_read(Z + s * SIMG + z1 + 16 * c), tr_read(Z + s * SIMG + z2 + 16 * c));
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dk[r][c] = mfma_bf(A[r], B[c], dk[r][c]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// MODE 0: forward only (J of every point).  MODE 1: recompute backward (dJ given -> slab rows).
+// Eight waves (two per SIMD, so one wave's tanh-jet VALU work runs beside the other's MFMAs):
+// wave w computes column tile q = w >> 2 (16 points) of feature tiles 2 (w & 3).. (OPW of them) in
+// every GEMM / epilogue, and owns an NR x NC block of each hidden layer's dK tiles.
+template <int WT, int S, int NSO, int LM, int MODE>
+__global__ void __launch_bounds__(64 * FZ_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, const bf16x8* __restrict__ Wimg_in,
+                 const bf16x8* __restrict__ Kimg_in, const float* __restrict__ dJ, float* __restrict__ J,
+                 float* __restrict__ slab, int N, int Pst, NetDims d, JetSpec sp, int ntiles) {
+  constexpr int W = 16 * WT, KB = WT / 2, OPW = WT / 4, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
+  constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
+  constexpr int ZS = LM == 1 ? 1 : 0;      // slot of zb_LM (h_0's slot once layer 1 has read it)
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  static_assert(OPW >= 1 && OPW * 4 == WT, "fused kernels: WT = 4 or 8");
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  __bf16* img = reinterpret_cast<__bf16*>(lds_raw);
+  auto slot = [&](int k) { return img + (k == 0 ? 0 : (S + (k - 1) * (S + 1)) * SIMG); };
+  float* fl = reinterpret_cast<float*>(img + fz_img_elems(WT, S, LM));
+  const int naux = fz_aux_floats(d, W);
+  float* aux = fl;                            // the aux image (biases, K0, Ko, bo), copied once
+  float* xs = aux + naux;                     // [FZ_PT][TDQ_MAXD]
+  float* ubs = xs + FZ_PT * TDQ_MAXD;         // [S][FZ_PT][4] dJ of the tile
+  float* part = ubs + S * FZ_PT * 4;          // MODE 1: [2 column tiles][...] partials; MODE 0: outp
+  const int pq = (LM + 1) * W + d.d_in * W + 4 * W;  // partial floats per column tile
+  float* outp = part;                         // MODE 0: [4][S][FZ_PT][4] output-layer partial dots
+
+  const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = w >> 2, wo = w & 3;
+  const int G = gridDim.x, gi = blockIdx.x;
+  const int t0 = (int)((long long)ntiles * gi / G), t1 = (int)((long long)ntiles * (gi + 1) / G);
+  const int r0 = NR * (w >> 1), c0 = NC * (w & 1);  // dK block of this wave
+  const int o0 = wo * OPW;                          // feature tiles of this wave (GEMM outputs)
+  const int row = 16 * q + p;                       // this lane's point in the tile
+  const FzLane L = fz_lane<RS>(p, g);
+  float* accB = part + q * pq;                      // [LM + 1][W]  bias partials (layer 0..LM)
+  float* accK0 = accB + (LM + 1) * W;               // [d_in][W]
+  float* accKo = accK0 + d.d_in * W;                // [W][4]
+  float* accBo = part + 2 * pq;                     // [4]
+  // Loop-invariant weight loads must not be hoisted out of the tile loop (they would pin ~100
+  // VGPRs for the whole launch): the image pointers go through an opaque copy at every tile.
+  const bf16x8* Wimg = Wimg_in;
+  const bf16x8* Kimg = Kimg_in;
+
+  for (int e = tid; e < naux; e += 64 * FZ_WAVES) aux[e] = e < aux_floats(d, W) ? aux_g[e] : 0.f;
+  f32x4 dk[LM][NR][NC];
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int i = 0; i < LM; ++i)
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) dk[i][r][c] = zero4();
+    for (int e = tid; e < 2 * pq + 4; e += 64 * FZ_WAVES) part[e] = 0.f;
+  }
+  const float* Ko = aux + aux_ko(d, W);
+
+  // layer 0 (input -> width, VALU) of feature tile o0 + oo at this lane's point
+  auto layer0 = [&](int oo, f32x4(&h)[S]) {
+    float x[TDQ_MAXD];
+#pragma unroll
+    for (int j = 0; j < TDQ_MAXD; ++j) x[j] = xs[row * TDQ_MAXD + j];
+    h0_jet<WT, S, NSO>(sp, aux, d, x, o0 + oo, g, h);
+  };
+
+  for (int t = t0; t < t1; ++t) {
+    const int pb = t * FZ_PT;
+    asm volatile("" : "+s"(Wimg), "+s"(Kimg));
+    __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
+    for (int e = tid; e < FZ_PT * TDQ_MAXD; e += 64 * FZ_WAVES) {
+      const int pt = e / TDQ_MAXD, j = e - pt * TDQ_MAXD;
+      const int n = min(pb + pt, N - 1);
+      xs[e] = j < d.d_in ? X[(size_t)n * d.d_in + j] : 0.f;
+    }
+    if constexpr (MODE == 1) {
+      for (int e = tid; e < S * FZ_PT * 4; e += 64 * FZ_WAVES) {
+        const int s = e / (FZ_PT * 4), r = e - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
+        const int n = pb + pt;
+        ubs[e] = (n < N && qo < d.d_out) ? dJ[((size_t)s * N + n) * d.d_out + qo] : 0.f;
+      }
+    }
+    __syncthreads();
+
+    // ---- layer 0 -> slot 0 ----------------------------------------------------------------
+#pragma unroll
+    for (int oo = 0; oo < OPW; ++oo) {
+      f32x4 h[S];
+      layer0(oo, h);
+#pragma unroll
+      for (int s = 0; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
+    }
+    __syncthreads();
+
+    // ---- hidden layers 1..LM on MFMA ------------------------------------------------------
+#pragma unroll
+    for (int ly = 1; ly <= LM; ++ly) {
+      const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
+      f32x4 acc[OPW][S];
+      fz_gemm<WT, S, OPW>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
+      f32x4 hq[OPW][S];  // MODE 0, top layer: the streams for the output dots
+#pragma unroll
+      for (int oo = 0; oo < OPW; ++oo) {
+        const int to = o0 + oo;
+        f32x4 z[S], h[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) z[s] = acc[oo][s];
+        z[0] += *reinterpret_cast<const f32x4*>(bi + 16 * to + 4 * g);
+        fz_tanh_jet_f<S, NSO>(sp, z, h);
+        if (ly < LM) {
+          __bf16* im = slot(ly);
+          bf16x4 hi, lo;
+          split4(h[0], hi, lo);
+          fz_put<RS>(im, L, q, to, hi);
+          if constexpr (MODE == 1) fz_put<RS>(im + S * SIMG, L, q, to, lo);
+#pragma unroll
+          for (int s = 1; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(h[s]));
+        } else if constexpr (MODE == 0) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) hq[oo][s] = h[s];
+        } else {
+          // reverse through the output layer right here (dJ is known): hb = Ko ub, dKo, then the
+          // top tanh layer's adjoint zb_LM into slot ZS (h_0's slot: its readers, layer 1's GEMM,
+          // are behind the barrier after layer 1; LM = 1: the spare slot 1).  Output columns in a
+          // runtime loop: d_out is 1 for scalar PDEs
+          f32x4 hb[S], zb[S];
+#pragma unroll
+          for (int s = 0; s < S; ++s) hb[s] = zero4();
+          for (int qo = 0; qo < d.d_out; ++qo) {
+            f32x4 kq, pp = zero4();
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kq[c] = Ko[(16 * to + 4 * g + c) * 4 + qo];
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+              const float ub = ubs[(s * FZ_PT + row) * 4 + qo];
+              hb[s] += kq * ub;
+              pp += h[s] * ub;
+            }
+            const float r = row16_sum4(pp);
+            if ((p & 3) == 0) accKo[(16 * to + 4 * g + (p >> 2)) * 4 + qo] += r;
+          }
+          tanh_jet_b<S, NSO>(sp, h, hb, zb);
+          const float r = row16_sum4(zb[0]);
+          if ((p & 3) == 0) accB[LM * W + 16 * to + 4 * g + (p >> 2)] += r;
+#pragma unroll
+          for (int s = 0; s < S; ++s) fz_put<RS>(slot(ZS) + s * SIMG, L, q, to, cvt_hi4(zb[s]));
+        }
+      }
+      if (MODE == 0 && ly == LM) {  // output-layer partial dots of this wave's features -> LDS
+        for (int qo = 0; qo < d.d_out; ++qo) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            float a = 0.f;
+#pragma unroll
+            for (int oo = 0; oo < OPW; ++oo)
+#pragma unroll
+              for (int c = 0; c < 4; ++c) a = fmaf(hq[oo][s][c], Ko[(16 * (o0 + oo) + 4 * g + c) * 4 + qo], a);
+            const float r = col4_sum(a);
+            if (g == 0) outp[((wo * S + s) * FZ_PT + row) * 4 + qo] = r;
+          }
+        }
+      }
+      __syncthreads();
+    }
+
+    if constexpr (MODE == 0) {
+      // ---- output layer: the per-wave partial dots summed in wave order ----------------------
+      const float* bo = aux + aux_bo(d, W);
+      for (int e = tid; e < S * FZ_PT * 4; e += 64 * FZ_WAVES) {
+        const int s = e / (FZ_PT * 4), r = e - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
+        const int n = pb + pt;
+        if (n < N && qo < d.d_out) {
+          float a = outp[((0 * S + s) * FZ_PT + pt) * 4 + qo];
+#pragma unroll
+          for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * 4 + qo];
+          if (s == 0) a += bo[qo];
+          J[((size_t)s * N + n) * d.d_out + qo] = a;
+        }
+      }
+    } else {
+      if (w == 0 && l < 4) {  // dbo (ubs is complete since the tile's first barriers)
+        float a = 0.f;
+        for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + l];
+        accBo[l] += a;
+      }
+      // ---- hidden layers LM..1: dK_l, hb_{l-1} = K_l zb_l, adjoint of tanh layer l-1 --------
+#pragma unroll
+      for (int ly = LM; ly >= 1; --ly) {
+        const __bf16* Z = slot(ly == LM ? ZS : ly);
+        __bf16* H = slot(ly - 1);
+        fz_dk<WT, S, NR, NC>(dk[ly - 1], H, Z, r0, c0, l);
+        f32x4 acc[OPW][S];
+        fz_gemm<WT, S, OPW>(acc, Kimg, ly, o0, Z, q, L, l);
+        if (ly >= 2) __syncthreads();  // every wave's dK reads of H are done: zb_{ly-1} goes in place
+#pragma unroll
+        for (int oo = 0; oo < OPW; ++oo) {
+          const int to = o0 + oo;
+          f32x4 h[S], zb[S];
+          if (ly >= 2) {
+            h[0] = fz_bf4(fz_get<RS>(H, L, q, to)) + fz_bf4(fz_get<RS>(H + S * SIMG, L, q, to));
+#pragma unroll
+            for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(H + s * SIMG, L, q, to));
+            tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
+            const float r = row16_sum4(zb[0]);
+            if ((p & 3) == 0) accB[(ly - 1) * W + 16 * to + 4 * g + (p >> 2)] += r;
+#pragma unroll
+            for (int s = 0; s < S; ++s) fz_put<RS>(H + s * SIMG, L, q, to, cvt_hi4(zb[s]));
+          } else {
+            // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
+            float x[TDQ_MAXD];
+#pragma unroll
+            for (int j = 0; j < TDQ_MAXD; ++j) x[j] = xs[row * TDQ_MAXD + j];
+            h0_jet<WT, S, NSO>(sp, aux, d, x, to, g, h);
+            tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
+            const int fo = 16 * to + 4 * g + (p >> 2);
+            {
+              const float r = row16_sum4(zb[0]);
+              if ((p & 3) == 0) accB[fo] += r;
+            }
+            for (int j = 0; j < d.d_in; ++j) {
+              f32x4 vv;
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                float a = x[j] * zb[0][c];
+#pragma unroll
+                for (int s = 1; s < SO; ++s) a += (sp.var[s] == j) ? zb[s][c] : 0.f;
+                vv[c] = a;
+              }
+              const float r = row16_sum4(vv);
+              if ((p & 3) == 0) accK0[j * W + fo] += r;
+            }
+          }
+        }
+        if (ly == 2) {  // rebuild h_0 into slot 0 (zb_LM there is consumed)
+          if (LM == 2) __syncthreads();  // (LM = 2: it was this step's Z)
+#pragma unroll
+          for (int oo = 0; oo < OPW; ++oo) {
+            f32x4 h[S];
+            layer0(oo, h);
+#pragma unroll
+            for (int s = 0; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
+          }
+        }
+        if (ly >= 2) __syncthreads();
+      }
+    }
+  }
+
+  if constexpr (MODE == 1) {
+    // ---- this workgroup's gradient-slab row (bf16) ------------------------------------------
+    __bf16* gs = reinterpret_cast<__bf16*>(slab) + (size_t)gi * Pst;
+#pragma unroll
+    for (int ly = 1; ly <= LM; ++ly) {
+      const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
+      const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * 2;
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)dk[ly - 1][r][c][e]), Gt.r,
+                                                  voff, ((16 * r + e) * W + 16 * c) * 2, 0);
+    }
+    __syncthreads();  // LDS partials complete
+    const float* pA = part;
+    const float* pB = part + pq;
+    for (int f = tid; f < W; f += 64 * FZ_WAVES) {
+      gs[d.d_in * W + f] = (__bf16)(pA[f] + pB[f]);  // b0
+      for (int ly = 1; ly <= LM; ++ly)
+        gs[off_layer(d, ly) + W * W + f] = (__bf16)(pA[ly * W + f] + pB[ly * W + f]);
+      for (int j = 0; j < d.d_in; ++j) {
+        const int k = (LM + 1) * W + j * W + f;
+        gs[j * W + f] = (__bf16)(pA[k] + pB[k]);
+      }
+      for (int qo = 0; qo < d.d_out; ++qo) {
+        const int k = (LM + 1 + d.d_in) * W + f * 4 + qo;
+        gs[off_layer(d, LM + 1) + f * d.d_out + qo] = (__bf16)(pA[k] + pB[k]);
+      }
+    }
+    if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (__bf16)accBo[tid];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct FzArgs {
+  const float* X;
+  const float* aux;
+  const bf16x8* fimg;
+  const bf16x8* bimg;
+  const float* dJ;
+  float* J;
+  float* slab;
+  int N, Pst, G, ntiles;
+  NetDims d;
+  JetSpec sp;
+  hipStream_t st;
+};
+
+template <int WT, int S, int NSO, int LM, int MODE>
+int launch_fused(const FzArgs& a) {
+  const size_t lds = fz_lds_bytes(a.d, WT, S, LM, MODE);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_fused_kernel<WT, S, NSO, LM, MODE>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((jet_fused_kernel<WT, S, NSO, LM, MODE>), dim3(a.G), dim3(64 * FZ_WAVES), lds, a.st, a.X, a.aux, a.fimg,
+                     a.bimg, a.dJ, a.J, a.slab, a.N, a.Pst, a.d, a.sp, a.ntiles);
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// jet_fused.hip
+bool fz_active(const NetDims& d, int WT, int S, int lo);
+int fz_rows(int N);
+int fz_launch(int mode, const float* X, const float* aux, const bf16x8* fimg, const bf16x8* bimg, const float* dJ,
+              float* J, float* slab, int N, int Pst, const NetDims& d, const JetSpec& sp, int S, int nso,
+              hipStream_t st);

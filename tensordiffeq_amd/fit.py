@@ -587,6 +587,12 @@ def point_ranges(program, fop):
         return None
     if cfg["precision"] not in ("bf16x3", "bf16") or cfg.get("engine") == "layered":
         return None
+    from .ops import jet_hip
+    try:
+        if jet_hip.fused_active(cfg):  # one persistent launch per pass already fills the GPU
+            return None
+    except Exception:  # noqa: BLE001 - no native library: no ranges either way
+        return None
     if spec == "auto":
         # sweeps on MI355X with the specialized loss kernel: bf16 0.38 (0.2018 ms vs 0.2035 at 0.45,
         # 3 passes, profiles/r3_yz_split_sweep_jit.jsonl), bf16x3 0.30-0.40 equal within noise.
@@ -609,7 +615,6 @@ def point_ranges(program, fop):
     # preferred cuts: a row boundary of the slab reduction's chunks (slab_chunk_lo), so the first
     # range's rows are pre-reduced while the second range's backward runs (prereduce_chunk) with
     # every summation order unchanged; else the nearest multiple of 128 points
-    from .ops import jet_hip
     try:
         pts_b, nwg, chunks, _ = jet_hip.slab_geometry(cfg, N)
         bounds = [(nwg * c // chunks) * pts_b for c in range(1, chunks)]

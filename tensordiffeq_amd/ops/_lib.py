@@ -55,6 +55,10 @@ def _declare(lib):
         "tdq_dp_tail_b_bf3": (I, [P, I, I, P, I, I, I, P, I, P, P, P]),
         "tdq_jet_bf3_scratch_floats": (L, [I, I, P, I, I, I]),
         "tdq_jet_bf3_slab_floats": (L, [I, I, P, I, I]),
+        # persistent point-tile kernels (csrc/jet_fused.h) behind the split-bf16 entry points
+        "tdq_jet_fused_active": (I, [I, P, I, I, I, I]),
+        "tdq_jet_fused_rows": (I, [I]),
+        "tdq_jet_fused_override": (I, [I]),
         "tdq_adam_multi": (I, [P, I, P, P, P]),
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),

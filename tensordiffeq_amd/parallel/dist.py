@@ -141,10 +141,38 @@ def free_port(lo=20000, hi=32000):
 _free_port = free_port
 
 
+# rank variables of launchers that start one process per task themselves (torchrun, Slurm srun,
+# Open MPI / MPICH / MVAPICH mpirun, PMIx): such a process must never self-launch more ranks
+_LAUNCHER_VARS = ("WORLD_SIZE", "SLURM_PROCID", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "PMIX_RANK",
+                  "MV2_COMM_WORLD_SIZE")
+
+
 def launcher_env():
-    """True when a launcher (torchrun / torch.distributed.run / an MPI-style wrapper) already
-    set up this process as one rank."""
-    return "WORLD_SIZE" in os.environ
+    """True when a launcher (torchrun / torch.distributed.run / srun / an MPI-style wrapper)
+    already set up this process as one rank."""
+    return any(v in os.environ for v in _LAUNCHER_VARS)
+
+
+def relaunch_argv():
+    """The arguments that re-run this program under ``torch.distributed.run``, or None when it
+    is not a plain script / module run (an interactive interpreter, a Jupyter / IPython kernel,
+    ``python -c``, an embedding host): those must train at world 1 rather than re-run
+    something else N times.  ``python -m pkg.mod args`` -> ``-m pkg.mod args``."""
+    import sys
+    if hasattr(sys, "ps1") or "ipykernel" in sys.modules or "IPython" in sys.modules:
+        return None
+    main = sys.modules.get("__main__")
+    argv = list(sys.argv)
+    if main is None or not argv or not argv[0] or argv[0] == "-c":
+        return None
+    spec = getattr(main, "__spec__", None)
+    if spec is not None and getattr(spec, "name", None) and spec.name != "__main__":
+        mod = spec.name[:-len(".__main__")] if spec.name.endswith(".__main__") else spec.name
+        return ["-m", mod] + argv[1:]
+    f = getattr(main, "__file__", None)
+    if not f or not os.path.exists(argv[0]) or os.path.abspath(f) != os.path.abspath(argv[0]):
+        return None
+    return argv
 
 
 def visible_devices():
@@ -168,8 +196,8 @@ def self_launch(nproc, argv=None, env=None):
     127.0.0.1 with a free port."""
     import subprocess
     import sys
-    argv = list(sys.argv if argv is None else argv)
-    if not argv or not argv[0] or argv[0] == "-c" or not os.path.exists(argv[0]):
+    argv = relaunch_argv() if argv is None else list(argv)
+    if not argv or not argv[0] or argv[0] == "-c" or (argv[0] != "-m" and not os.path.exists(argv[0])):
         raise RuntimeError("cannot self-launch ranks: the program was not started from a script file; "
                            "use 'python -m torch.distributed.run --nproc-per-node N script.py'")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(nproc)}",
@@ -202,6 +230,11 @@ def maybe_self_launch(n=None, why="dist=True"):
     if os.environ.get("TDQ_DIST_AUTOLAUNCH", "1") == "0":
         warnings.warn(f"{why}: {n} devices visible but TDQ_DIST_AUTOLAUNCH=0 and no launcher - training at "
                       "world 1", stacklevel=3)
+        return
+    if relaunch_argv() is None:
+        warnings.warn(f"{why}: {n} devices visible but this is not a plain script or module run (interactive "
+                      "session, notebook kernel, python -c) - training at world 1; launch with "
+                      "'torch.distributed.run --nproc-per-node N' for N ranks", stacklevel=3)
         return
     print(f"[tensordiffeq_amd] {why}: launching {n} ranks (one per device) with torch.distributed.run",
           file=sys.stderr, flush=True)

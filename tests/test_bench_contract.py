@@ -135,6 +135,51 @@ def test_compile_dist_true_one_device_warns(tmp_path):
     assert len(recs) == 1 and recs[0]["world"] == 1 and not recs[0]["dist"]
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("how", ["ipykernel", "python-c", "slurm"])
+def test_dist_true_never_relaunches_non_scripts(how, tmp_path):
+    """a notebook kernel (argv[0] = ipykernel_launcher.py), ``python -c`` and a task that
+    a non-torchrun launcher (srun) already started must train at world 1 instead of re-running
+    something N times."""
+    env = _env()
+    env["TDQ_DIST_NPROC"] = "2"
+    env["OUT_DIR"] = str(tmp_path)
+    if how == "ipykernel":
+        p = tmp_path / "ipykernel_launcher.py"
+        p.write_text("import sys, types\nsys.modules['ipykernel'] = types.ModuleType('ipykernel')\n" + SCRIPT_DIST)
+        cmd = [sys.executable, str(p)]
+    elif how == "python-c":
+        cmd = [sys.executable, "-c", SCRIPT_DIST]
+    else:
+        p = tmp_path / "dist_script.py"
+        p.write_text(SCRIPT_DIST)
+        env["SLURM_PROCID"] = "0"
+        cmd = [sys.executable, str(p)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "launching 2 ranks" not in r.stderr
+    recs = [json.loads(q.read_text()) for q in sorted(tmp_path.glob("rank*.json"))]
+    assert len(recs) == 1 and recs[0]["world"] == 1
+
+
+def test_relaunch_argv_forms(monkeypatch):
+    import types
+    from tensordiffeq_amd.parallel import dist as tdist
+    main = types.ModuleType("__main__")
+    main.__file__ = os.path.join(ROOT, "bench.py")
+    main.__spec__ = None
+    monkeypatch.setitem(sys.modules, "__main__", main)
+    monkeypatch.setattr(sys, "argv", [os.path.join(ROOT, "bench.py"), "--gpus", "2"])
+    monkeypatch.delitem(sys.modules, "ipykernel", raising=False)
+    monkeypatch.delitem(sys.modules, "IPython", raising=False)
+    assert tdist.relaunch_argv() == [os.path.join(ROOT, "bench.py"), "--gpus", "2"]
+    main.__spec__ = types.SimpleNamespace(name="examples.ac_dist")       # python -m examples.ac_dist
+    assert tdist.relaunch_argv() == ["-m", "examples.ac_dist", "--gpus", "2"]
+    main.__spec__ = None
+    monkeypatch.setattr(sys, "argv", ["/elsewhere/ipykernel_launcher.py", "-f", "kernel.json"])
+    assert tdist.relaunch_argv() is None                                  # __main__ is not argv[0]
+
+
 PROBLEM_ARGS = {"ac-sa": ["--npts", "256"], "ac-baseline": ["--npts", "256"], "poisson": ["--npts", "256"],
                 "ac-dist": ["--global-npts", "512"], "discovery": ["--global-npts", "512"]}
 

@@ -1,0 +1,117 @@
+"""Persistent point-tile jet kernels (csrc/jet_fused.h): the forward and the recompute backward
+that serve precision "bf16" at width 128 with S <= 4 streams and 1-3 MFMA hidden layers.
+
+Checked against float64 torch jets / autograd (the same oracles as tests/test_hip_kernels.py) and
+against the saved-activation kernels of csrc/jet_bf3.h (switched on and off in-process with
+``jet_hip.fused_override``), over the tile geometry's edge cases: a single partial tile, several
+tiles per workgroup, point counts that are not multiples of the 32-point tile.
+"""
+import pytest
+import torch
+
+from tensordiffeq_amd.jet import JetPlan, jet_forward
+from tensordiffeq_amd.models.networks import TanhMLP
+
+pytestmark = pytest.mark.gpu
+
+TOL_FWD = 5e-2    # bf16 bounds of tests/test_hip_kernels.py (shallow nets)
+TOL_BWD = 1.4e-2
+
+CASES = [
+    # layer_sizes, requests, N
+    ([2, 128, 128, 128, 128, 1], [(0,), (1,), (0, 0)], 1000),    # AC-SA plan: LM = 3, S = 4
+    ([2, 128, 128, 128, 128, 1], [(0,), (1,), (0, 0)], 20000),   # several tiles per workgroup
+    ([2, 128, 128, 128, 128, 1], [(0,), (1,), (0, 0)], 5),       # one partial tile
+    ([2, 128, 128, 1], [(0,), (1,), (0, 0)], 333),               # LM = 1
+    ([2, 128, 128, 128, 2], [(0,)], 97),                         # LM = 2, S = 2, d_out = 2
+    ([3, 128, 128, 128, 128, 1], [(0, 0), (1,)], 515),           # d_in = 3
+    ([2, 128, 128, 128, 128, 1], [], 100),                       # value stream only
+    ([2, 128, 128, 128, 1], [(0,), (1,)], 64),                   # S = 3, first order only
+]
+
+
+def _setup(sizes, reqs, N, seed=0):
+    torch.manual_seed(seed)
+    net = TanhMLP(sizes, device="cuda")
+    with torch.no_grad():
+        net.flat.add_(0.05 * torch.randn_like(net.flat))  # non-zero biases
+    X = (torch.rand(N, sizes[0], device="cuda") * 2 - 1).contiguous()
+    return net, X, JetPlan(reqs, sizes[0])
+
+
+@pytest.fixture
+def fused_on():
+    from tensordiffeq_amd.ops import jet_hip
+    jet_hip.fused_override(1)
+    yield jet_hip
+    jet_hip.fused_override(None)
+
+
+def _grad(jet_hip, net, X, plan, G):
+    p = net.flat.detach().clone().requires_grad_(True)
+    J = jet_hip.JetMLPFunction.apply(X, p, net, plan, "bf16")
+    (J.double() * G).sum().backward()
+    return J.detach(), p.grad.double()
+
+
+@pytest.mark.parametrize("sizes,reqs,N", CASES)
+def test_fused_matches_fp64(sizes, reqs, N, fused_on):
+    jet_hip = fused_on
+    from tensordiffeq_amd.ops import jet_mlp
+    net, X, plan = _setup(sizes, reqs, N, seed=1)
+    cfg = jet_mlp.hip_config(net, plan, "bf16")
+    assert jet_hip.fused_active(cfg), cfg
+    G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
+    J, g = _grad(jet_hip, net, X, plan, G)
+    p64 = net.flat.detach().double().clone().requires_grad_(True)
+    Jr = jet_forward(X.double(), net.weights(p64), plan)
+    scale = Jr.detach().abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
+    ferr = ((J.double() - Jr.detach()).abs() / scale).max().item()
+    (Jr * G).sum().backward()
+    g_ref = p64.grad
+    rel = ((g - g_ref).norm() / g_ref.norm()).item()
+    print(f"FUSED_ERR {sizes} S={plan.S} N={N} fwd {ferr:.3e} bwd {rel:.3e}")
+    assert ferr < TOL_FWD, ferr
+    assert rel < TOL_BWD, rel
+    off = 0
+    for k, b in net.weights(p64.detach()):
+        for blk in (k, b):
+            n = blk.numel()
+            a, r = g[off:off + n], g_ref[off:off + n]
+            assert ((a - r).norm() / r.norm().clamp_min(1e-30)).item() < 20 * TOL_BWD, (off, n)
+            off += n
+
+
+@pytest.mark.parametrize("sizes,reqs,N", [CASES[0], CASES[1], CASES[3]])
+def test_fused_matches_saved_activation_kernels(sizes, reqs, N):
+    """Same bf16 network, two kernel designs.  With the same tanh (an FZ_CHEAP_TANH=0 build) they agree
+    to 1.5e-6 in J (gpurun_out/r5tanh); the persistent kernels' cheaper tanh (~1e-7 absolute) flips
+    some bf16 roundings of the activations, after which the two carry independent bf16 errors:
+    ~1e-2 against each other in the cancelling derivative streams, while each stays at the same
+    distance from the fp64 jet (test_fused_matches_fp64).  Bounds: the bf16 level."""
+    from tensordiffeq_amd.ops import jet_hip
+    net, X, plan = _setup(sizes, reqs, N, seed=2)
+    G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
+    try:
+        jet_hip.fused_override(0)
+        J0, g0 = _grad(jet_hip, net, X, plan, G)
+        jet_hip.fused_override(1)
+        J1, g1 = _grad(jet_hip, net, X, plan, G)
+    finally:
+        jet_hip.fused_override(None)
+    scale = J0.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
+    jerr = ((J1 - J0).abs() / scale).max().item()
+    gerr = ((g1 - g0).norm() / g0.norm()).item()
+    per_stream = ((J1 - J0).abs() / scale).amax(dim=(1, 2)).tolist()
+    print(f"FUSED_VS_SAVED {sizes} N={N} J {jerr:.3e} (streams {['%.1e' % v for v in per_stream]}) grad {gerr:.3e}")
+    assert jerr < 3e-2, jerr
+    assert gerr < 1e-2, gerr
+
+
+def test_fused_deterministic(fused_on):
+    jet_hip = fused_on
+    net, X, plan = _setup(*CASES[1], seed=3)
+    G = torch.randn(plan.S, X.shape[0], 1, device="cuda", dtype=torch.float64)
+    J1, g1 = _grad(jet_hip, net, X, plan, G)
+    J2, g2 = _grad(jet_hip, net, X, plan, G)
+    assert torch.equal(J1, J2) and torch.equal(g1, g2)
