@@ -21,10 +21,11 @@ EXACTLY K steps bracketed by barrier + device synchronize on every rank; the max
 reported.  Weak scaling by default (``--npts`` per GPU); ``--global-npts`` fixes the total
 (strong scaling, e.g. the reference's AC-dist-new config: 500,000 points, examples/AC-dist-new.py).
 
-Accuracy half of the metric (single GPU, after the timed region, ``--acc-seeds``): the reference
-AC-SA schedule (examples/AC-SA.py:64-88: Adam 10k + L-BFGS 10k; Adam in the bench precision,
-L-BFGS in ``newton_precision`` bf16x3) from scratch per seed, relative L2 on data/AC.mat, wall
-time per phase and why L-BFGS stopped.  ``--force-dp`` (single GPU) also times the data-parallel
+Accuracy half of the metric (after the timed region, ``--acc-seeds``, at every GPU count): the
+reference AC-SA schedule (examples/AC-SA.py:64-88: Adam 10k + L-BFGS 10k; Adam in the bench
+precision, L-BFGS in ``newton_precision`` bf16x3) from scratch per seed on its 50k points -
+sharded over the ranks, with their SA weights, at ``--gpus N`` - relative L2 on data/AC.mat, wall
+time per phase and why L-BFGS stopped (``--problem ac-dist``: AC-dist-new's Adam 1001 x 2 on 500k).  ``--force-dp`` (single GPU) also times the data-parallel
 step - a real RCCL process group at world 1, the all-reduce captured in the step graph - next to
 the plain one.
 
@@ -322,21 +323,32 @@ def allreduce_replay_us(ctx, n_floats, calls=10, reps=20):
 
 
 def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop, problem="ac-sa",
-                  layers=None, newton_schedule=None):
+                  layers=None, newton_schedule=None, world=1, npts=None):
     """Reference schedule per seed (AC-SA / AC-baseline: examples/AC-SA.py:9-88, Adam + L-BFGS, L2 on
+    AC.mat; AC-dist: examples/AC-dist-new.py:48-78, 500k points, ``fit(tf_iter=1001)`` twice, L2 on
     AC.mat; discovery: examples/AC-discovery.py, Adam + L-BFGS over network and coefficients,
-    c1 / c2 errors), with phase times and the L-BFGS stop reason."""
+    c1 / c2 errors), with phase times and the L-BFGS stop reason.  ``world > 1``: every rank runs
+    it under data parallelism - the schedule's point set (50k, or AC-dist's 500k) sharded over the
+    ranks with its SA weights, one all-reduce per step - as the reference's distributed example
+    trains with ``dist=True`` before evaluating (AC-dist-new.py:51-54,78)."""
     out = []
     spec = PROBLEMS[problem]
     layers = layers or tuple(int(v) for v in spec["layers"].split(","))
+    dist = world > 1
     for sd in seeds:
-        n = spec["npts"] if problem == "discovery" else 50000
-        m = spec["build"](n, 1, backend, device, False, precision, seed=sd, newton_precision=newton_precision,
+        n = npts or (spec["npts"] if problem in ("discovery", "ac-dist") else 50000)
+        m = spec["build"](n, world, backend, device, dist, precision, seed=sd, newton_precision=newton_precision,
                           lbfgs_stop=lbfgs_stop, layers=layers, newton_schedule=newton_schedule)
         if problem == "discovery":
             m.fit(tf_iter=iters, newton_iter=newton)
             c1, c2 = discovery_c1(m.vars[0]), float(m.vars[1].detach())
             res = {"seed": sd, "c1": c1, "c2": c2, "c1_rel_err": abs(c1 - 1e-4) / 1e-4, "c2_rel_err": abs(c2 - 5.0) / 5.0}
+        elif problem == "ac-dist":
+            m.fit(tf_iter=AC_DIST_ADAM)
+            a1 = m.fit_info.get("adam", {}).get("wall_s", 0.0)
+            m.fit(tf_iter=AC_DIST_ADAM)
+            m.fit_info.setdefault("adam", {})["wall_s"] = a1 + m.fit_info.get("adam", {}).get("wall_s", 0.0)
+            res = {"seed": sd, "l2": float(l2_on_ac_grid(m))}
         else:
             m.fit(tf_iter=iters)
             m.fit(newton_iter=newton)
@@ -354,6 +366,9 @@ def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, ne
         if device.type == "cuda":
             torch.cuda.empty_cache()
     return out
+
+
+AC_DIST_ADAM = 1001  # examples/AC-dist-new.py:52-54: fit(tf_iter=1001) twice
 
 
 def forced_dp_timing(n_glob, backend, device, precision, steps, warmup, min_warmup_s):
@@ -396,8 +411,10 @@ def main(argv=None):
                          "the fused kernels in bf16, wider nets / other precisions the layer-wise engine)")
     ap.add_argument("--no-l2", action="store_true", help="skip the accuracy runs")
     ap.add_argument("--acc-seeds", type=int, nargs="*", default=[0, 1, 2],
-                    help="seeds of the full-schedule accuracy runs (single GPU only)")
+                    help="seeds of the full-schedule accuracy runs (under data parallelism at --gpus N)")
     ap.add_argument("--acc-iters", type=int, default=10000)
+    ap.add_argument("--acc-npts", type=int, default=None,
+                    help="points of the accuracy runs (default: the reference schedule's, 50k / AC-dist 500k)")
     ap.add_argument("--acc-newton", type=int, default=None,
                     help="L-BFGS iterations of the accuracy runs (default 10000; discovery 15000)")
     ap.add_argument("--newton-precision", default="bf16x3")
@@ -442,7 +459,7 @@ def main(argv=None):
         args.acc_newton = 15000 if args.problem == "discovery" else 10000  # discovery: c2 to 0.03 % (r4o)
     # accuracy runs: the reference schedules of the single-GPU configs (AC-dist-new runs Adam 1001
     # twice without L-BFGS and the 10M-point Poisson config is a throughput sizing)
-    acc_ok = args.problem in ("ac-sa", "ac-baseline", "discovery")
+    acc_ok = args.problem in ("ac-sa", "ac-baseline", "ac-dist", "discovery")
     if "TDQ_STEP_UNROLL" not in os.environ:
         # steps per captured graph: a divisor of --steps, so the timed steps are all multi-step graph
         # replays (a 1-step replay leaves ~9 us idle between graphs; 8 and 16 per graph measured
@@ -471,11 +488,12 @@ def main(argv=None):
     del eng, model
 
     acc, acc_err = None, None
-    if not args.no_l2 and world == 1 and args.acc_seeds and acc_ok:
+    if not args.no_l2 and args.acc_seeds and acc_ok:
         try:
             acc = accuracy_runs(args.acc_seeds, device, args.backend, args.precision, args.newton_precision,
                                 args.acc_iters, args.acc_newton, args.lbfgs_stop, problem=args.problem,
-                                layers=layers, newton_schedule=args.newton_schedule)
+                                layers=layers, newton_schedule=args.newton_schedule, world=world,
+                                npts=args.acc_npts)
         except Exception as e:  # pragma: no cover - reported, never hides the throughput number
             acc_err = f"{type(e).__name__}: {e}"
     dp = None
@@ -525,10 +543,17 @@ def main(argv=None):
             l2s = sorted(a["l2"] for a in acc)
             rec["l2_full_schedule"] = l2s[len(l2s) // 2]
             rec["l2_full_schedule_seeds"] = [a["l2"] for a in acc]
-            ref = "AC-SA" if args.problem == "ac-sa" else "AC-baseline"
-            rec["accuracy_schedule"] = (f"Adam {args.acc_iters} ({args.precision}) + L-BFGS {args.acc_newton} "
-                                        f"({args.newton_precision}), N_f 50000, reference examples/{ref}.py; "
-                                        f"median over seeds {args.acc_seeds}")
+            on = f"on {world} GPUs (data parallel, points and SA weights sharded)" if world > 1 else "on 1 GPU"
+            if args.problem == "ac-dist":
+                rec["accuracy_schedule"] = (f"Adam {AC_DIST_ADAM} x 2 ({args.precision}), N_f {args.acc_npts or spec['npts']}, "
+                                            f"reference examples/AC-dist-new.py, {on}; median over seeds "
+                                            f"{args.acc_seeds}")
+            else:
+                ref = "AC-SA" if args.problem == "ac-sa" else "AC-baseline"
+                rec["accuracy_schedule"] = (f"Adam {args.acc_iters} ({args.precision}) + L-BFGS {args.acc_newton} "
+                                            f"({args.newton_precision}), N_f {args.acc_npts or 50000}, reference "
+                                            f"examples/{ref}.py, "
+                                            f"{on}; median over seeds {args.acc_seeds}")
             rec["time_to_solution_s"] = [{"adam_s": a["adam_s"], "lbfgs_s": a["lbfgs_s"]} for a in acc]
             rec["lbfgs"] = [{"reason": a["lbfgs_reason"], "n_iter": a["lbfgs_n_iter"], "stop": a["lbfgs_stop"],
                              **({"phases": a["lbfgs_phases"]} if a.get("lbfgs_phases") else {})} for a in acc]

@@ -29,6 +29,13 @@
 #pragma once
 #include "jet_bf3.h"
 
+// Phase stamps (-DTDQ_PHASE_TIMING build, tools/fused_timing.py): the first tile's phases and the
+// whole tile loop, per wave
+#define FZ_TS(k) \
+  do {                \
+    if (t == t0) TDQ_TS(k); \
+  } while (0)
+
 #define FZ_PT 32  // points per tile (two 16-point MFMA column tiles; waves 0-3 / 4-7)
 #define FZ_WAVES 8
 
@@ -254,6 +261,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
     h0_jet<WT, S, NSO>(sp, aux, d, x, o0 + oo, g, h);
   };
 
+  TDQ_TS(0);
   for (int t = t0; t < t1; ++t) {
     const int pb = t * FZ_PT;
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
@@ -271,6 +279,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
       }
     }
     __syncthreads();
+    FZ_TS(1);
 
     // ---- layer 0 -> slot 0 ----------------------------------------------------------------
 #pragma unroll
@@ -281,6 +290,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
       for (int s = 0; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
     }
     __syncthreads();
+    FZ_TS(2);
 
     // ---- hidden layers 1..LM on MFMA ------------------------------------------------------
 #pragma unroll
@@ -288,6 +298,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
       const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
       f32x4 acc[OPW][S];
       fz_gemm<WT, S, OPW>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
+      FZ_TS(1 + 2 * ly);
       f32x4 hq[OPW][S];  // MODE 0, top layer: the streams for the output dots
 #pragma unroll
       for (int oo = 0; oo < OPW; ++oo) {
@@ -351,6 +362,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
         }
       }
       __syncthreads();
+      FZ_TS(2 + 2 * ly);
     }
 
     if constexpr (MODE == 0) {
@@ -378,10 +390,14 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
       for (int ly = LM; ly >= 1; --ly) {
         const __bf16* Z = slot(ly == LM ? ZS : ly);
         __bf16* H = slot(ly - 1);
+        const int tb = 10 + 5 * (LM - ly);
         fz_dk<WT, S, NR, NC>(dk[ly - 1], H, Z, r0, c0, l);
+        FZ_TS(tb);
         f32x4 acc[OPW][S];
         fz_gemm<WT, S, OPW>(acc, Kimg, ly, o0, Z, q, L, l);
+        FZ_TS(tb + 1);
         if (ly >= 2) __syncthreads();  // every wave's dK reads of H are done: zb_{ly-1} goes in place
+        FZ_TS(tb + 2);
 #pragma unroll
         for (int oo = 0; oo < OPW; ++oo) {
           const int to = o0 + oo;
@@ -421,6 +437,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
             }
           }
         }
+        FZ_TS(tb + 3);
         if (ly == 2) {  // rebuild h_0 into slot 0 (zb_LM there is consumed)
           if (LM == 2) __syncthreads();  // (LM = 2: it was this step's Z)
 #pragma unroll
@@ -432,9 +449,11 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
           }
         }
         if (ly >= 2) __syncthreads();
+        FZ_TS(tb + 4);
       }
     }
   }
+  TDQ_TS(62);
 
   if constexpr (MODE == 1) {
     // ---- this workgroup's gradient-slab row (bf16) ------------------------------------------
@@ -470,6 +489,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
     }
     if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (__bf16)accBo[tid];
   }
+  TDQ_TS(63);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -2,6 +2,12 @@
 // layers at 128-feature padded width (WT = 8), every (S, NSO) with S <= 4, both modes.
 #include "jet_fused.h"
 
+#ifdef TDQ_PHASE_TIMING
+extern "C" int tdq_fz_set_timing_buffer(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(tdq_ts), &p, sizeof(p));
+}
+#endif
+
 int fz_dispatch_w8_l3(int mode, int S, int nso, const FzArgs& a) {
   switch ((S * 16 + nso) * 2 + mode) {
 #define FZ_CASE(S_, N_) \

@@ -3,6 +3,7 @@ BASELINE.json, single process and 2 ranks over gloo (torchrun, 127.0.0.1) - the 
 includes the collective warm-up stop (a rank-local clock once let ranks run different numbers of
 DP steps)."""
 import json
+import math
 import os
 import subprocess
 import sys
@@ -133,6 +134,24 @@ def test_compile_dist_true_one_device_warns(tmp_path):
     assert "training at world 1" in r.stderr
     recs = [json.loads(q.read_text()) for q in sorted(tmp_path.glob("rank*.json"))]
     assert len(recs) == 1 and recs[0]["world"] == 1 and not recs[0]["dist"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("problem", ["ac-sa", "ac-dist"])
+def test_bench_accuracy_under_dp_two_ranks(problem):
+    """at --gpus N the accuracy schedule runs under data parallelism (points and
+    SA weights sharded) and rank 0's JSON carries its L2 next to the throughput (tiny CPU sizes)."""
+    args = ["--steps", "2", "--warmup", "1", "--min-warmup-s", "0.01", "--problem", problem, "--gpus", "2",
+            "--acc-seeds", "0", "--acc-iters", "3", "--acc-newton", "3", "--acc-npts", "512"]
+    args += ["--npts", "256"] if problem == "ac-sa" else ["--global-npts", "512"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       env=_env(), timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    assert rec["n_gpus"] == 2
+    assert rec["l2_full_schedule"] is not None and math.isfinite(rec["l2_full_schedule"]), rec
+    assert "on 2 GPUs" in rec["accuracy_schedule"]
+    assert len(rec["time_to_solution_s"]) == 1
 
 
 @pytest.mark.timeout(300)
