@@ -190,7 +190,7 @@ class CollocationSolverND:
                 # whose sum over ALL weights multiplies every rank's partial mean: those weights stay
                 # replicated and their gradient (the global mean) is all-reduced like theta's
                 sharded = (key == "residual" and t.numel() == self.N_f and ctx.is_distributed
-                           and not self.weight_outside_sum)
+                           and not self._outside_sum_weights())
                 if sharded:
                     t = t.reshape(-1, 1)[self._lo:self._hi]
                 t = t.reshape(-1, 1).contiguous() if t.numel() > 1 else t.reshape(()).contiguous()
@@ -352,9 +352,16 @@ class CollocationSolverND:
     def variables(self):
         return [self._flat()] + list(self.lambdas or [])
 
+    def _outside_sum_weights(self):
+        """Per-point residual weights enter through MSE's outside sum (Adaptive_type 2 without
+        ``g``): their sum over ALL points multiplies every rank's partial mean, so under DP they stay
+        replicated.  With ``g`` the residual term is g_MSE, element-wise g(lam) * f^2 (reference
+        utils.py:47-48), and the weights are sharded with their points like type 1's."""
+        return self.weight_outside_sum and self.g is None
+
     def _lam_replicated(self):
         ctx = self.dist_ctx
-        return [not (k == "residual" and ctx.is_distributed and l.numel() > 1 and not self.weight_outside_sum)
+        return [not (k == "residual" and ctx.is_distributed and l.numel() > 1 and not self._outside_sum_weights())
                 for l, k in zip(self.lambdas, self._lam_kind)]
 
     # ================================================================== loss API =========

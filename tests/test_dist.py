@@ -241,28 +241,46 @@ def test_forced_dp_world1_matches_single_process(monkeypatch):
     assert res["red"] == 2   # theta + the IC's SA weights; residual SA weights stay local
 
 
-def _build_type2(dist):
+def _g_square(lam):
+    return lam * lam
+
+
+def _build_type2(dist, with_g=False):
     from tests.test_solver import allen_cahn
     D, bcs, f, _ = allen_cahn(n_f=301, sa=False)
     g = torch.Generator().manual_seed(3)
     kw = dict(Adaptive_type=2, dict_adaptive={"residual": [True], "BCs": [False, False]},
               init_weights={"residual": [torch.rand(301, 1, generator=g)], "BCs": [None, None]})
+    if with_g:   # g_MSE: element-wise g(lam) f^2 - the weights shard with their points
+        kw["g"] = _g_square
     torch.manual_seed(0)
     m = tdq.CollocationSolverND(verbose=False)
     m.compile([2, 12, 12, 1], f, D, bcs, backend="jet", device="cpu", dist=dist, **kw)
     return m
 
 
-def _worker_type2(rank, world, port, q):
+def _worker_type2(rank, world, port, q, with_g=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     from tensordiffeq_amd.parallel import dist as pdist
     pdist.reset_context()
     ctx = pdist.init_distributed(backend="gloo", device="cpu")
-    m = _build_type2(True)
+    m = _build_type2(True, with_g)
     m.fit(tf_iter=5)
-    res = {"hist": [h["Total Loss"] for h in m.losses], "flat": _np(m.u_model.flat), "lam": _np(m.lambdas[0])}
+    lam = m.lambdas[0].detach()
+    if with_g:   # sharded: gather the ranks' slices in rank order
+        import torch.distributed as tdist
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        tdist.all_gather(sizes, torch.tensor([lam.shape[0]]))
+        mx = int(max(sizes))
+        buf = [torch.zeros(mx, 1) for _ in range(world)]
+        pad = torch.zeros(mx, 1)
+        pad[:lam.shape[0]] = lam
+        tdist.all_gather(buf, pad)
+        lam = torch.cat([b[:int(n)] for b, n in zip(buf, sizes)])
+    res = {"hist": [h["Total Loss"] for h in m.losses], "flat": _np(m.u_model.flat), "lam": _np(lam),
+           "lam_local": int(m.lambdas[0].shape[0])}
     if rank == 0:
         q.put(res)
     ctx.barrier()
@@ -287,6 +305,30 @@ def test_dp_adaptive_type2_per_point_weights():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert res["hist"] == pytest.approx(ref_hist, rel=1e-4)
+    assert torch.allclose(_t(res["flat"]), ref.u_model.flat.detach(), atol=1e-5)
+    assert torch.allclose(_t(res["lam"]), ref.lambdas[0].detach(), atol=1e-5)
+
+
+@pytest.mark.timeout(300)
+def test_dp_adaptive_type2_with_g_shards_weights():
+    """Adaptive_type 2 with ``g`` uses g_MSE (element-wise g(lam) f^2), so the per-point
+    weights are sharded with their points (replicated ones failed to broadcast against the rank's
+    residual); the trajectory and the gathered weights equal single-process training."""
+    ref = _build_type2(False, with_g=True)
+    ref.fit(tf_iter=5)
+    ref_hist = [h["Total Loss"] for h in ref.losses]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_type2, args=(r, 2, port, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=280)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res["lam_local"] < 301
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-4)
     assert torch.allclose(_t(res["flat"]), ref.u_model.flat.detach(), atol=1e-5)
     assert torch.allclose(_t(res["lam"]), ref.lambdas[0].detach(), atol=1e-5)
