@@ -1,7 +1,9 @@
 // Shared helpers for the gfx950 (CDNA4) kernels of tensordiffeq_amd.
 #pragma once
+#ifndef __HIPCC_RTC__  // (hipRTC, ops/fused_step.py: the HIP device API is implicit)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

@@ -1257,6 +1257,7 @@ jet_bwd_bf3_kernel(const float* __restrict__ X, const float* __restrict__ aux, c
 // ------------------------------------------------------------------------------------------
 // host-side launch templates (instantiated per width class in jet_bf3_w{2,4,8}.hip)
 // ------------------------------------------------------------------------------------------
+#ifndef __HIPCC_RTC__
 inline size_t fwd_bf3_lds(int WT, int S, bool lo) {
   return bf3_gstage(WT, S, lo) ? 0 : (size_t)2 * S * WT * 1024 * (lo ? 2 : 1);
 }
@@ -1371,3 +1372,4 @@ int bf3_bwd_w2(int S, int nso, const Bf3Args& a);
 int bf3_bwd_w4(int S, int nso, const Bf3Args& a);
 int bf3_bwd_w8(int S, int nso, const Bf3Args& a);
 int bf3_bwd_w16(int S, int nso, const Bf3Args& a);
+#endif  // __HIPCC_RTC__

@@ -343,6 +343,13 @@ int64_t tdq_jet_bf3_slab_floats(int N, int d_in, const int* widths, int d_out, i
   return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
 
+// floats of `rows` gradient-slab rows + their reduction partials (the fused step's rows)
+int64_t tdq_slab_floats_rows(int rows, int d_in, const int* widths, int d_out, int n_hidden) {
+  NetDims d;
+  if (rows < 1 || !make_dims(d, d_in, widths, 0, d_out, n_hidden)) return -1;
+  return ((int64_t)rows + slab_chunks(rows)) * slab_stride(param_count(d));
+}
+
 // image pointers inside the forward's scratch (at its start)
 static inline void scratch_images(float* scratch, int n_hidden, int WT, float** img, float** bimg, float** aux) {
   *img = scratch;
@@ -486,7 +493,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
                       int S, int lo, const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses,
                       float* total, float* dscal, float* hist, int64_t hist_rows, int64_t* epoch, float* best_loss,
                       int64_t* best_epoch, int* improved, double* const* counters, int ncnt, const void* groups,
-                      int ngroups, float* snap, int c_first, const float* gx, void* stream) {
+                      int ngroups, float* snap, int c_first, const float* gx, int rows, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -500,7 +507,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
   if (args.grp[0].n != Ptot) return (int)hipErrorInvalidValue;
   args.grp[0].g = grad;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int nwg_b = bf3_rows(N, d, WT, S, lo);
+  const int nwg_b = rows > 0 ? rows : bf3_rows(N, d, WT, S, lo);  // rows: the fused step's (ops/fused_step.py)
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -550,7 +557,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
 // objective writes [grad | loss] in place this way.
 int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
-                      float* total, int c_first, const float* gx, void* stream) {
+                      float* total, int c_first, const float* gx, int rows, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -558,7 +565,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
     return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int Ptot = param_count(d);
-  const int nwg_b = bf3_rows(N, d, WT, S, lo);
+  const int nwg_b = rows > 0 ? rows : bf3_rows(N, d, WT, S, lo);
   const int Pst = slab_stride(Ptot), chunks = slab_chunks(nwg_b);
   if (c_first < 0 || c_first >= chunks) return (int)hipErrorInvalidValue;
   float* part = work + (size_t)nwg_b * Pst;
@@ -651,5 +658,46 @@ int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_
   TDQ_CHECK_LAUNCH();
   return 0;
 }
+
+// One launch of a run-time compiled fused training step (csrc/jet_fused.h MODE 2, ops/fused_step.py):
+// forward -> the residual group's loss -> recompute backward over the points [p_lo, N), G
+// workgroups, gradient-slab rows srow.., loss-partial rows prow.. (nacc floats each)
+int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* work, int N, int d_in, const int* widths,
+                          int d_out, int n_hidden, int S, const int* spec, int p_lo, int srow, int G, const void* lptrs,
+                          float* lpart, int prow, int nacc, int seg_lo, void* stream) {
+  if (func == nullptr || N <= 0 || p_lo < 0 || p_lo >= N || G < 1 || srow < 0 || prow < 0 || nacc < 1)
+    return (int)hipErrorInvalidValue;
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  const int WT = width_tiles(d.width);
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  JetSpec sp;
+  if (spec_nso(S, spec) < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
+  float *img, *bimg, *aux;
+  scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
+  FzParams P{};
+  P.X = X;
+  P.aux = aux;
+  P.fimg = reinterpret_cast<const bf16x8*>(img);
+  P.bimg = reinterpret_cast<const bf16x8*>(bimg);
+  P.slab = work;
+  P.N = N;
+  P.Pst = slab_stride(param_count(d));
+  P.ntiles = (N - p_lo + FZ_PT - 1) / FZ_PT;
+  P.p_lo = p_lo;
+  P.srow = srow;
+  P.d = d;
+  P.sp = sp;
+  P.lptrs = reinterpret_cast<const FzLossPtrs*>(lptrs);
+  P.lpart = lpart;
+  P.prow = prow;
+  P.nacc = nacc;
+  P.seg_lo = seg_lo;
+  void* args[] = {(void*)&P};
+  return (int)hipModuleLaunchKernel((hipFunction_t)func, (unsigned)G, 1, 1, 64 * FZ_WAVES, 1, 1, 0,
+                                    reinterpret_cast<hipStream_t>(stream), args, nullptr);
+}
+
+int tdq_fused_params_size() { return (int)sizeof(FzParams); }
 
 }  // extern "C"

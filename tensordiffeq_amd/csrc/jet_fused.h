@@ -40,17 +40,21 @@
 #define FZ_WAVES 8
 
 __host__ __device__ constexpr int fz_nslot(int LM) { return LM < 2 ? 2 : LM; }
-// bf16 elements of the image area: slot 0 holds S streams, slots >= 1 one more (the value lo image)
+// bf16 elements of the image area: every slot holds S stream images plus the value stream's lo image
 __host__ __device__ constexpr int fz_img_elems(int WT, int S, int LM) {
-  return (S + (fz_nslot(LM) - 1) * (S + 1)) * FZ_PT * bf3_img_rs(WT);
+  return (S + 1) * fz_nslot(LM) * FZ_PT * bf3_img_rs(WT);
 }
-// float area after the images: aux copy | xs | ubs | (MODE 1) per-column-tile partials
-// (biases of layers 0..LM, K0, Ko), bo | (MODE 0) output-layer partial dots
+// output-layer partial-dot columns per point: d_out <= 4 (MODE 0), 1 (MODE 2: the fused loss is scalar)
+__host__ __device__ constexpr int fz_oq(int mode) { return mode == 2 ? 1 : 4; }
+// float area after the images: aux copy | xs | ubs | (MODE 1, 2) per-column-tile partials (biases
+// of layers 0..LM, K0, Ko), bo | (MODE 0, 2) output-layer partial dots
 __host__ __device__ inline int fz_aux_floats(const NetDims& d, int W) { return (aux_floats(d, W) + 3) / 4 * 4; }
 __host__ __device__ inline int fz_fl_floats(const NetDims& d, int WT, int S, int LM, int mode) {
   const int W = 16 * WT;
   const int common = fz_aux_floats(d, W) + FZ_PT * TDQ_MAXD + S * FZ_PT * 4;
-  return common + (mode == 1 ? 2 * ((LM + 1) * W + d.d_in * W + 4 * W) + 4 : 4 * S * FZ_PT * 4);
+  const int part = mode >= 1 ? 2 * ((LM + 1) * W + d.d_in * W + 4 * W) + 4 : 0;
+  const int outp = mode != 1 ? 4 * S * FZ_PT * fz_oq(mode) : 0;
+  return common + part + outp;
 }
 __host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int LM, int mode) {
   return fz_img_elems(WT, S, LM) * 2 + fz_fl_floats(d, WT, S, LM, mode) * 4;
@@ -93,6 +97,41 @@ __device__ __forceinline__ void fz_tanh_jet_f(const JetSpec& sp, const f32x4 (&z
     for (int s = 1; s < SO; ++s) h[s][c] = s1 * z[s][c];
 #pragma unroll
     for (int s = SO; s < S; ++s) h[s][c] = fmaf(s2 * za[s][c], zb[s][c], s1 * z[s][c]);
+  }
+}
+
+// Layer 0 (input -> width, VALU) of feature tile t at one point x (LDS row), in the cheap tanh
+// form of fz_tanh_jet_f - computed three times per tile (forward, the h_0 image rebuild for dK_1,
+// the layer-0 adjoint), always by this function, so every pass sees the same h_0.  Its derivative
+// streams are rows of K0: h_a = s1 K0[a], h_ab = s2 K0[a] K0[b] (z_ab = 0).
+template <int WT, int S, int NSO>
+__device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const NetDims& d, const float* xrow, int t,
+                                      int g, f32x4 (&h)[S]) {
+  constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
+  const int f0 = 16 * t + 4 * g;
+  f32x4 z = *reinterpret_cast<const f32x4*>(aux + aux_b0(d, W) + f0);
+  for (int j = 0; j < d.d_in; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+  f32x4 ka[S];
+  ka[0] = zero4();
+#pragma unroll
+  for (int s = 1; s < SO; ++s) ka[s] = *reinterpret_cast<const f32x4*>(aux + sp.var[s] * W + f0);
+#pragma unroll
+  for (int s = SO; s < S; ++s) ka[s] = zero4();
+  f32x4 kp[S];
+#pragma unroll
+  for (int s = SO; s < S; ++s) kp[s] = sel_first<S, S1>(ka, sp.ia[s], sp.selA[s]) * sel_first<S, S1>(ka, sp.ib[s], sp.selB[s]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float e = __builtin_amdgcn_exp2f(fminf(z[c], 15.f) * 2.8853900817779268f);
+    const float r = __builtin_amdgcn_rcpf(1.f + e);
+    const float hv = fmaf(-2.f, r, 1.f);
+    const float s1 = (4.f * e) * (r * r);
+    const float s2 = -2.f * hv * s1;
+    h[0][c] = hv;
+#pragma unroll
+    for (int s = 1; s < SO; ++s) h[s][c] = s1 * ka[s][c];
+#pragma unroll
+    for (int s = SO; s < S; ++s) h[s][c] = s2 * kp[s][c];
   }
 }
 
@@ -168,7 +207,7 @@ __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __re
 
 // dK[r][c] += sum over the tile's points and streams of H^T Z (transposed LDS reads; the wave's
 // NR x NC block of 16 x 16 output tiles at row tiles r0.., column tiles c0..)
-template <int WT, int S, int NR, int NC>
+template <int WT, int S, int NR, int NC, bool SB = true>
 __device__ __forceinline__ void fz_dk(f32x4 (&dk)[NR][NC], const __bf16* H, const __bf16* Z, int r0, int c0, int l) {
   constexpr int RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
   const int g = l >> 4;
@@ -192,35 +231,81 @@ __device__ __forceinline__ void fz_dk(f32x4 (&dk)[NR][NC], const __bf16* H, cons
     for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int c = 0; c < NC; ++c) dk[r][c] = mfma_bf(A[r], B[c], dk[r][c]);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
+// The fused loss's pointer table (csrc/loss_fused.hip LFPtrs, ops/loss_fused.py): value arrays,
+// per-point SA weights and their gradients, scalar parameters
+struct FzLossPtrs {
+  const float* val[16];
+  const float* lam[8];
+  float* dlam[8];
+  const float* scal[8];
+};
+
+struct FzParams {
+  const float* X;
+  const float* aux;
+  const bf16x8* fimg;   // forward A image ([out][in] k order)
+  const bf16x8* bimg;   // backward A image ([in][out])
+  const float* dJ;      // MODE 1
+  float* J;             // MODE 0
+  float* slab;          // MODE 1, 2: gradient-slab rows srow + blockIdx.x
+  int N, Pst, ntiles;
+  int p_lo;             // the tiles cover points [p_lo, N)
+  int srow;
+  NetDims d;
+  JetSpec sp;
+  // MODE 2: the loss of the points [seg_lo, N) (one residual group of the fused loss program)
+  const FzLossPtrs* lptrs;
+  float* lpart;         // loss / scalar-gradient partials, row prow + blockIdx.x, nacc floats each
+  int prow, nacc, seg_lo;
+};
+
+// MODE 0 / 1 builds: no loss code
+struct FzNoLoss {
+  static constexpr int NACC = 1;
+  template <int S>
+  __device__ static void eval(const float (&)[S], const float*, int, bool, const FzLossPtrs&, float (&dJv)[S],
+                              float (&)[1]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) dJv[s] = 0.f;
+  }
+};
+
 // MODE 0: forward only (J of every point).  MODE 1: recompute backward (dJ given -> slab rows).
+// MODE 2: forward -> per-point loss (LossF, generated from the traced program and compiled at run
+// time: ops/fused_step.py) -> backward, all in one launch (slab rows + loss partials).
 // Eight waves (two per SIMD, so one wave's tanh-jet VALU work runs beside the other's MFMAs):
 // wave w computes column tile q = w >> 2 (16 points) of feature tiles 2 (w & 3).. (OPW of them) in
 // every GEMM / epilogue, and owns an NR x NC block of each hidden layer's dK tiles.
-template <int WT, int S, int NSO, int LM, int MODE>
-__global__ void __launch_bounds__(64 * FZ_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
-jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, const bf16x8* __restrict__ Wimg_in,
-                 const bf16x8* __restrict__ Kimg_in, const float* __restrict__ dJ, float* __restrict__ J,
-                 float* __restrict__ slab, int N, int Pst, NetDims d, JetSpec sp, int ntiles) {
+template <int WT, int S, int NSO, int LM, int MODE, class LossF>
+__device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
+  const float* __restrict__ X = P.X;
+  const float* __restrict__ aux_g = P.aux;
+  const float* __restrict__ dJ = P.dJ;
+  float* __restrict__ J = P.J;
+  const int N = P.N, Pst = P.Pst, ntiles = P.ntiles;
+  const NetDims& d = P.d;
+  const JetSpec& sp = P.sp;
   constexpr int W = 16 * WT, KB = WT / 2, OPW = WT / 4, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
   constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
   constexpr int ZS = LM == 1 ? 1 : 0;      // slot of zb_LM (h_0's slot once layer 1 has read it)
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
+  constexpr int OQ = fz_oq(MODE);
   static_assert(OPW >= 1 && OPW * 4 == WT, "fused kernels: WT = 4 or 8");
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  static_assert(MODE != 2 || LM >= 2, "fused-loss mode keeps h_LM in h_0's slot");
   __bf16* img = reinterpret_cast<__bf16*>(lds_raw);
-  auto slot = [&](int k) { return img + (k == 0 ? 0 : (S + (k - 1) * (S + 1)) * SIMG); };
+  auto slot = [&](int k) { return img + k * (S + 1) * SIMG; };
   float* fl = reinterpret_cast<float*>(img + fz_img_elems(WT, S, LM));
   const int naux = fz_aux_floats(d, W);
   float* aux = fl;                            // the aux image (biases, K0, Ko, bo), copied once
   float* xs = aux + naux;                     // [FZ_PT][TDQ_MAXD]
   float* ubs = xs + FZ_PT * TDQ_MAXD;         // [S][FZ_PT][4] dJ of the tile
-  float* part = ubs + S * FZ_PT * 4;          // MODE 1: [2 column tiles][...] partials; MODE 0: outp
+  float* part = ubs + S * FZ_PT * 4;          // MODE 1, 2: [2 column tiles][...] partials
   const int pq = (LM + 1) * W + d.d_in * W + 4 * W;  // partial floats per column tile
-  float* outp = part;                         // MODE 0: [4][S][FZ_PT][4] output-layer partial dots
+  float* outp = part + (MODE >= 1 ? 2 * pq + 4 : 0);  // MODE 0, 2: [4][S][FZ_PT][OQ] output-layer dots
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -237,12 +322,15 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
   float* accBo = part + 2 * pq;                     // [4]
   // Loop-invariant weight loads must not be hoisted out of the tile loop (they would pin ~100
   // VGPRs for the whole launch): the image pointers go through an opaque copy at every tile.
-  const bf16x8* Wimg = Wimg_in;
-  const bf16x8* Kimg = Kimg_in;
+  const bf16x8* Wimg = P.fimg;
+  const bf16x8* Kimg = P.bimg;
 
   for (int e = tid; e < naux; e += 64 * FZ_WAVES) aux[e] = e < aux_floats(d, W) ? aux_g[e] : 0.f;
   f32x4 dk[LM][NR][NC];
-  if constexpr (MODE == 1) {
+  float lacc[LossF::NACC];  // MODE 2: this point-thread's loss / scalar-gradient sums (all tiles)
+#pragma unroll
+  for (int k = 0; k < LossF::NACC; ++k) lacc[k] = 0.f;
+  if constexpr (MODE >= 1) {
 #pragma unroll
     for (int i = 0; i < LM; ++i)
 #pragma unroll
@@ -254,30 +342,34 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
   const float* Ko = aux + aux_ko(d, W);
 
   // layer 0 (input -> width, VALU) of feature tile o0 + oo at this lane's point
-  auto layer0 = [&](int oo, f32x4(&h)[S]) {
-    float x[TDQ_MAXD];
-#pragma unroll
-    for (int j = 0; j < TDQ_MAXD; ++j) x[j] = xs[row * TDQ_MAXD + j];
-    h0_jet<WT, S, NSO>(sp, aux, d, x, o0 + oo, g, h);
-  };
+  auto layer0 = [&](int oo, f32x4(&h)[S]) { fz_h0<WT, S, NSO>(sp, aux, d, xs + row * TDQ_MAXD, o0 + oo, g, h); };
 
+  // this thread's element of a tile's x / dJ (one each: FZ_PT * TDQ_MAXD and S * FZ_PT * 4 are
+  // <= 512), fetched one tile ahead so the global latency hides behind the current tile
+  static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES && S * FZ_PT * 4 <= 64 * FZ_WAVES, "one element per thread");
+  float xpre = 0.f, upre = 0.f;
+  auto fetch = [&](int tt) {
+    const int pb = P.p_lo + tt * FZ_PT;
+    if (tid < FZ_PT * TDQ_MAXD) {
+      const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
+      const int n = min(pb + pt, N - 1);
+      xpre = j < d.d_in ? X[(size_t)n * d.d_in + j] : 0.f;
+    }
+    if (MODE == 1 && tid < S * FZ_PT * 4) {
+      const int s = tid / (FZ_PT * 4), r = tid - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
+      const int n = pb + pt;
+      upre = (n < N && qo < d.d_out) ? dJ[((size_t)s * N + n) * d.d_out + qo] : 0.f;
+    }
+  };
+  if (t0 < t1) fetch(t0);
   TDQ_TS(0);
   for (int t = t0; t < t1; ++t) {
-    const int pb = t * FZ_PT;
+    const int pb = P.p_lo + t * FZ_PT;
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
     __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
-    for (int e = tid; e < FZ_PT * TDQ_MAXD; e += 64 * FZ_WAVES) {
-      const int pt = e / TDQ_MAXD, j = e - pt * TDQ_MAXD;
-      const int n = min(pb + pt, N - 1);
-      xs[e] = j < d.d_in ? X[(size_t)n * d.d_in + j] : 0.f;
-    }
-    if constexpr (MODE == 1) {
-      for (int e = tid; e < S * FZ_PT * 4; e += 64 * FZ_WAVES) {
-        const int s = e / (FZ_PT * 4), r = e - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
-        const int n = pb + pt;
-        ubs[e] = (n < N && qo < d.d_out) ? dJ[((size_t)s * N + n) * d.d_out + qo] : 0.f;
-      }
-    }
+    if (tid < FZ_PT * TDQ_MAXD) xs[tid] = xpre;
+    if (MODE == 1 && tid < S * FZ_PT * 4) ubs[tid] = upre;
+    if (t + 1 < t1) fetch(t + 1);
     __syncthreads();
     FZ_TS(1);
 
@@ -313,12 +405,21 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
           bf16x4 hi, lo;
           split4(h[0], hi, lo);
           fz_put<RS>(im, L, q, to, hi);
-          if constexpr (MODE == 1) fz_put<RS>(im + S * SIMG, L, q, to, lo);
+          if constexpr (MODE >= 1) fz_put<RS>(im + S * SIMG, L, q, to, lo);
 #pragma unroll
           for (int s = 1; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(h[s]));
-        } else if constexpr (MODE == 0) {
+        } else if constexpr (MODE != 1) {
 #pragma unroll
           for (int s = 0; s < S; ++s) hq[oo][s] = h[s];
+          if constexpr (MODE == 2) {  // h_LM waits in h_0's slot (hi / lo value) for the loss
+            __bf16* im = slot(ZS);
+            bf16x4 hi, lo;
+            split4(h[0], hi, lo);
+            fz_put<RS>(im, L, q, to, hi);
+            fz_put<RS>(im + S * SIMG, L, q, to, lo);
+#pragma unroll
+            for (int s = 1; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(h[s]));
+          }
         } else {
           // reverse through the output layer right here (dJ is known): hb = Ko ub, dKo, then the
           // top tanh layer's adjoint zb_LM into slot ZS (h_0's slot: its readers, layer 1's GEMM,
@@ -347,8 +448,8 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
           for (int s = 0; s < S; ++s) fz_put<RS>(slot(ZS) + s * SIMG, L, q, to, cvt_hi4(zb[s]));
         }
       }
-      if (MODE == 0 && ly == LM) {  // output-layer partial dots of this wave's features -> LDS
-        for (int qo = 0; qo < d.d_out; ++qo) {
+      if (MODE != 1 && ly == LM) {  // output-layer partial dots of this wave's features -> LDS
+        for (int qo = 0; qo < (MODE == 2 ? 1 : d.d_out); ++qo) {
 #pragma unroll
           for (int s = 0; s < S; ++s) {
             float a = 0.f;
@@ -357,7 +458,7 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
 #pragma unroll
               for (int c = 0; c < 4; ++c) a = fmaf(hq[oo][s][c], Ko[(16 * (o0 + oo) + 4 * g + c) * 4 + qo], a);
             const float r = col4_sum(a);
-            if (g == 0) outp[((wo * S + s) * FZ_PT + row) * 4 + qo] = r;
+            if (g == 0) outp[((wo * S + s) * FZ_PT + row) * OQ + qo] = r;
           }
         }
       }
@@ -372,14 +473,63 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
         const int s = e / (FZ_PT * 4), r = e - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
         const int n = pb + pt;
         if (n < N && qo < d.d_out) {
-          float a = outp[((0 * S + s) * FZ_PT + pt) * 4 + qo];
+          float a = outp[((0 * S + s) * FZ_PT + pt) * OQ + qo];
 #pragma unroll
-          for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * 4 + qo];
+          for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * OQ + qo];
           if (s == 0) a += bo[qo];
           J[((size_t)s * N + n) * d.d_out + qo] = a;
         }
       }
     } else {
+      if constexpr (MODE == 2) {
+        // ---- J of the tile's points (wave-ordered sums of the partial dots), the per-point loss
+        // (generated code: residual, SA weighting, its reverse sweep) -> dJ into ubs ----------
+        if (tid < FZ_PT) {
+          const int n = pb + tid;
+          const bool active = n < N;
+          float Jv[S], dJv[S];
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            float a = outp[((0 * S + s) * FZ_PT + tid) * OQ];
+#pragma unroll
+            for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + tid) * OQ];
+            Jv[s] = s == 0 ? a + aux[aux_bo(d, W)] : a;
+          }
+          LossF::template eval<S>(Jv, xs + tid * TDQ_MAXD, n - P.seg_lo, active, *P.lptrs, dJv, lacc);
+#pragma unroll
+          for (int s = 0; s < S; ++s) ubs[(s * FZ_PT + tid) * 4] = active ? dJv[s] : 0.f;
+        }
+        __syncthreads();
+        // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
+#pragma unroll
+        for (int oo = 0; oo < OPW; ++oo) {
+          const int to = o0 + oo;
+          __bf16* im = slot(ZS);
+          f32x4 h[S], hb[S], zb[S];
+          h[0] = fz_bf4(fz_get<RS>(im, L, q, to)) + fz_bf4(fz_get<RS>(im + S * SIMG, L, q, to));
+#pragma unroll
+          for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(im + s * SIMG, L, q, to));
+          f32x4 kq, pp = zero4();
+#pragma unroll
+          for (int c = 0; c < 4; ++c) kq[c] = Ko[(16 * to + 4 * g + c) * 4];
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const float ub = ubs[(s * FZ_PT + row) * 4];
+            hb[s] = kq * ub;
+            pp += h[s] * ub;
+          }
+          {
+            const float r = row16_sum4(pp);
+            if ((p & 3) == 0) accKo[(16 * to + 4 * g + (p >> 2)) * 4] += r;
+          }
+          tanh_jet_b<S, NSO>(sp, h, hb, zb);
+          const float r = row16_sum4(zb[0]);
+          if ((p & 3) == 0) accB[LM * W + 16 * to + 4 * g + (p >> 2)] += r;
+#pragma unroll
+          for (int s = 0; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(zb[s]));
+        }
+        __syncthreads();
+      }
       if (w == 0 && l < 4) {  // dbo (ubs is complete since the tile's first barriers)
         float a = 0.f;
         for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + l];
@@ -391,32 +541,46 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
         const __bf16* Z = slot(ly == LM ? ZS : ly);
         __bf16* H = slot(ly - 1);
         const int tb = 10 + 5 * (LM - ly);
-        fz_dk<WT, S, NR, NC>(dk[ly - 1], H, Z, r0, c0, l);
-        FZ_TS(tb);
         f32x4 acc[OPW][S];
         fz_gemm<WT, S, OPW>(acc, Kimg, ly, o0, Z, q, L, l);
-        FZ_TS(tb + 1);
-        if (ly >= 2) __syncthreads();  // every wave's dK reads of H are done: zb_{ly-1} goes in place
-        FZ_TS(tb + 2);
+        FZ_TS(tb);
+        // the tanh-jet adjoint (VALU) and dK_ly (MFMA: every wave reads all of H and Z) in one
+        // scheduling region; zb_{ly-1} goes in place of h_{ly-1} after the barrier
+        bf16x4 zbh[OPW][S];
+        float rb[OPW];
+        if (ly >= 2) {
 #pragma unroll
-        for (int oo = 0; oo < OPW; ++oo) {
-          const int to = o0 + oo;
-          f32x4 h[S], zb[S];
-          if (ly >= 2) {
+          for (int oo = 0; oo < OPW; ++oo) {
+            const int to = o0 + oo;
+            f32x4 h[S], zb[S];
             h[0] = fz_bf4(fz_get<RS>(H, L, q, to)) + fz_bf4(fz_get<RS>(H + S * SIMG, L, q, to));
 #pragma unroll
             for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(H + s * SIMG, L, q, to));
             tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
-            const float r = row16_sum4(zb[0]);
-            if ((p & 3) == 0) accB[(ly - 1) * W + 16 * to + 4 * g + (p >> 2)] += r;
+            rb[oo] = row16_sum4(zb[0]);
 #pragma unroll
-            for (int s = 0; s < S; ++s) fz_put<RS>(H + s * SIMG, L, q, to, cvt_hi4(zb[s]));
-          } else {
-            // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
-            float x[TDQ_MAXD];
+            for (int s = 0; s < S; ++s) zbh[oo][s] = cvt_hi4(zb[s]);
+          }
+        }
+        fz_dk<WT, S, NR, NC, false>(dk[ly - 1], H, Z, r0, c0, l);
+        FZ_TS(tb + 1);
+        if (ly >= 2) {
+          __syncthreads();  // every wave's dK reads of H are done
+          FZ_TS(tb + 2);
 #pragma unroll
-            for (int j = 0; j < TDQ_MAXD; ++j) x[j] = xs[row * TDQ_MAXD + j];
-            h0_jet<WT, S, NSO>(sp, aux, d, x, to, g, h);
+          for (int oo = 0; oo < OPW; ++oo) {
+            const int to = o0 + oo;
+            if ((p & 3) == 0) accB[(ly - 1) * W + 16 * to + 4 * g + (p >> 2)] += rb[oo];
+#pragma unroll
+            for (int s = 0; s < S; ++s) fz_put<RS>(H + s * SIMG, L, q, to, zbh[oo][s]);
+          }
+        } else {
+          // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
+#pragma unroll
+          for (int oo = 0; oo < OPW; ++oo) {
+            const int to = o0 + oo;
+            f32x4 h[S], zb[S];
+            layer0(oo, h);
             tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
             const int fo = 16 * to + 4 * g + (p >> 2);
             {
@@ -424,10 +588,11 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
               if ((p & 3) == 0) accB[fo] += r;
             }
             for (int j = 0; j < d.d_in; ++j) {
+              const float xj = xs[row * TDQ_MAXD + j];
               f32x4 vv;
 #pragma unroll
               for (int c = 0; c < 4; ++c) {
-                float a = x[j] * zb[0][c];
+                float a = xj * zb[0][c];
 #pragma unroll
                 for (int s = 1; s < SO; ++s) a += (sp.var[s] == j) ? zb[s][c] : 0.f;
                 vv[c] = a;
@@ -455,9 +620,9 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
   }
   TDQ_TS(62);
 
-  if constexpr (MODE == 1) {
+  if constexpr (MODE >= 1) {
     // ---- this workgroup's gradient-slab row (bf16) ------------------------------------------
-    __bf16* gs = reinterpret_cast<__bf16*>(slab) + (size_t)gi * Pst;
+    __bf16* gs = reinterpret_cast<__bf16*>(P.slab) + (size_t)(P.srow + gi) * Pst;
 #pragma unroll
     for (int ly = 1; ly <= LM; ++ly) {
       const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
@@ -489,12 +654,29 @@ jet_fused_kernel(const float* __restrict__ X, const float* __restrict__ aux_g, c
     }
     if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (__bf16)accBo[tid];
   }
+  if constexpr (MODE == 2) {  // loss partials: the point-threads (wave 0, lanes < FZ_PT) summed
+    if (w == 0) {
+#pragma unroll
+      for (int k = 0; k < LossF::NACC; ++k) {
+        const float v = col4_sum(row16_sum(lacc[k]));
+        if (l == 0 && k < P.nacc) P.lpart[(size_t)(P.prow + gi) * P.nacc + k] = v;
+      }
+    }
+  }
   TDQ_TS(63);
+}
+
+template <int WT, int S, int NSO, int LM, int MODE>
+__global__ void __launch_bounds__(64 * FZ_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+jet_fused_kernel(FzParams P) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  fz_body<WT, S, NSO, LM, MODE, FzNoLoss>(P, lds_raw);
 }
 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+#ifndef __HIPCC_RTC__
 struct FzArgs {
   const float* X;
   const float* aux;
@@ -519,8 +701,22 @@ int launch_fused(const FzArgs& a) {
     attr = true;
   }
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL((jet_fused_kernel<WT, S, NSO, LM, MODE>), dim3(a.G), dim3(64 * FZ_WAVES), lds, a.st, a.X, a.aux, a.fimg,
-                     a.bimg, a.dJ, a.J, a.slab, a.N, a.Pst, a.d, a.sp, a.ntiles);
+  FzParams P{};
+  P.X = a.X;
+  P.aux = a.aux;
+  P.fimg = a.fimg;
+  P.bimg = a.bimg;
+  P.dJ = a.dJ;
+  P.J = a.J;
+  P.slab = a.slab;
+  P.N = a.N;
+  P.Pst = a.Pst;
+  P.ntiles = a.ntiles;
+  P.p_lo = 0;
+  P.srow = 0;
+  P.d = a.d;
+  P.sp = a.sp;
+  hipLaunchKernelGGL((jet_fused_kernel<WT, S, NSO, LM, MODE>), dim3(a.G), dim3(64 * FZ_WAVES), lds, a.st, P);
   TDQ_CHECK_LAUNCH();
   return 0;
 }
@@ -531,3 +727,4 @@ int fz_rows(int N);
 int fz_launch(int mode, const float* X, const float* aux, const bf16x8* fimg, const bf16x8* bimg, const float* dJ,
               float* J, float* slab, int N, int Pst, const NetDims& d, const JetSpec& sp, int S, int nso,
               hipStream_t st);
+#endif  // __HIPCC_RTC__

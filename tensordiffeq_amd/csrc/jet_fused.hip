@@ -72,6 +72,20 @@ int tdq_jet_fused_active(int d_in, const int* widths, int d_out, int n_hidden, i
 
 int tdq_jet_fused_rows(int N) { return fz_rows(N); }
 
+// LDS bytes of a persistent-kernel workgroup (mode 0 / 1 / 2 of jet_fused.h), -1 if the network is
+// not one the kernels take (the run-time compiled fused step declares it statically)
+int tdq_jet_fused_lds(int d_in, const int* widths, int d_out, int n_hidden, int S, int mode) {
+  NetDims d;
+  if (!make_dims(d, d_in, widths, 0, d_out, n_hidden) || mode < 0 || mode > 2) return -1;
+  const int WT = width_tiles(d.width), LM = d.n_hidden - 1;
+  if (WT != 8 || S < 1 || S > 4 || LM < 1 || LM > 3 || (mode == 2 && LM < 2) || !d.uniform || d.width != 16 * WT)
+    return -1;
+  return (int)fz_lds_bytes(d, WT, S, LM, mode);
+}
+
+// compute units of the current device (the persistent kernels' workgroup count)
+int tdq_device_cus() { return fz_cus(); }
+
 // tests only: force the persistent kernels off (0) / on (1) or back to TDQ_FUSED (-1).  Scratch and
 // slab sizes follow the switch, so buffers must be allocated after it (a new model / forward).
 int tdq_jet_fused_override(int v) {

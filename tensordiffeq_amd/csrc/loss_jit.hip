@@ -17,11 +17,12 @@
 
 extern "C" {
 
-// Compile `src` for `arch` (e.g. "gfx950").  On success *code (malloc'ed, free with
-// tdq_rtc_free) holds the code object of *size bytes.  log: the compiler log (truncated to
-// log_len); returns 0 or a nonzero hipRTC / HIP error code.
-int tdq_rtc_compile(const char* src, const char* name, const char* arch, void** code, long long* size, char* log,
-                    int log_len) {
+// Compile `src` for `arch` (e.g. "gfx950") with the options `opts` (space-separated; nullptr: the
+// fused-loss kernels' set below).  On success *code (malloc'ed, free with tdq_rtc_free) holds the
+// code object of *size bytes.  log: the compiler log (truncated to log_len); returns 0 or a nonzero
+// hipRTC / HIP error code.
+int tdq_rtc_compile_ex(const char* src, const char* name, const char* arch, const char* opts, void** code,
+                       long long* size, char* log, int log_len) {
   *code = nullptr;
   *size = 0;
   if (log_len > 0) log[0] = 0;
@@ -30,19 +31,25 @@ int tdq_rtc_compile(const char* src, const char* name, const char* arch, void** 
   if (r != HIPRTC_SUCCESS) return 1000 + (int)r;
   char archopt[64];
   snprintf(archopt, sizeof(archopt), "--offload-arch=%s", arch);
-  // statement-level FMA contraction only: a*b + c inside one statement (as in the interpreter's
-  // statements), never across the SSA temporaries the interpreter keeps in LDS
-  // fp32 division / sqrt correctly rounded, as hipcc compiles the interpreter
-  const char* opts[] = {archopt, "-O3", "-std=c++17", "-ffp-contract=on", "-fhip-fp32-correctly-rounded-divide-sqrt"};
-  r = hiprtcCompileProgram(prog, 5, opts);
+  // default: statement-level FMA contraction only (a*b + c inside one statement, as in the
+  // interpreter's statements, never across the SSA temporaries it keeps in LDS) and fp32 division /
+  // sqrt correctly rounded, as hipcc compiles the interpreter
+  const char* dflt = "-O3 -std=c++17 -ffp-contract=on -fhip-fp32-correctly-rounded-divide-sqrt";
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s", opts != nullptr ? opts : dflt);
+  const char* ov[24];
+  int no = 0;
+  ov[no++] = archopt;
+  for (char* t = strtok(buf, " "); t != nullptr && no < 24; t = strtok(nullptr, " ")) ov[no++] = t;
+  r = hiprtcCompileProgram(prog, no, ov);
   size_t lsz = 0;
   if (hiprtcGetProgramLogSize(prog, &lsz) == HIPRTC_SUCCESS && lsz > 1 && log_len > 1) {
-    char* buf = (char*)malloc(lsz);
-    if (buf != nullptr && hiprtcGetProgramLog(prog, buf) == HIPRTC_SUCCESS) {
-      strncpy(log, buf, (size_t)log_len - 1);
+    char* lb = (char*)malloc(lsz);
+    if (lb != nullptr && hiprtcGetProgramLog(prog, lb) == HIPRTC_SUCCESS) {
+      strncpy(log, lb, (size_t)log_len - 1);
       log[log_len - 1] = 0;
     }
-    free(buf);
+    free(lb);
   }
   if (r != HIPRTC_SUCCESS) {
     hiprtcDestroyProgram(&prog);
@@ -68,6 +75,11 @@ int tdq_rtc_compile(const char* src, const char* name, const char* arch, void** 
   *code = out;
   *size = (long long)csz;
   return 0;
+}
+
+int tdq_rtc_compile(const char* src, const char* name, const char* arch, void** code, long long* size, char* log,
+                    int log_len) {
+  return tdq_rtc_compile_ex(src, name, arch, nullptr, code, size, log, log_len);
 }
 
 void tdq_rtc_free(void* p) { free(p); }

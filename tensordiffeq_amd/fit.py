@@ -283,6 +283,11 @@ class AdamEngine:
             self._bufs = (J, saved, jet_hip.alloc_backward(saved), torch.empty_like(self.flat))
         return self._bufs
 
+    def _fused_step(self):
+        """The one-launch residual step (ops/fused_step.py) or None."""
+        from .ops import fused_step
+        return fused_step.for_program(self.program)
+
     def _point_ranges(self, fop):
         if getattr(self, "_ranges", 0) == 0:
             self._ranges = point_ranges(self.program, fop)
@@ -305,9 +310,7 @@ class AdamEngine:
         # persistent buffers: every captured step (the 1-step and the K-step graph) reads the weight
         # images the previous step's tail wrote into this one scratch
         J, saved, work, grad = self._step_buffers()
-        rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
-        pre = prereduce_chunk(prog, rng)
-        run_ranges(prog, fop, self.flat, rng, self._streams, pack=not in_graph, bufs=(J, saved, work), prereduce=pre)
+        pre, kw = self._run_points(J, saved, work, pack=not in_graph)
         grads = self._fused_grads(fop, grad, fop.dlam, fop.dscal)
         packed = fused.group_array(self._opt_groups(grads))
         if packed is None:  # gradient tensors the single launch cannot take: reduce, then Adam
@@ -315,9 +318,23 @@ class AdamEngine:
                                "(set TDQ_FUSED_TAIL=0)")
         hi = prog.hi_op
         jet_hip.step_tail(saved, work, grad, fop, st, self.counters, packed[0], packed[1], st["best_flat"],
-                          write_images=in_graph, c_first=pre, gextra=hi.grad if hi is not None else None)
+                          write_images=in_graph, c_first=pre, gextra=hi.grad if hi is not None else None, **kw)
         self._tail_saved = saved
         return fop.total
+
+    def _run_points(self, J, saved, work, pack):
+        """Gradient slabs + loss partials of every point: the fused residual step beside the
+        boundary chain, else the point ranges' forward -> loss -> backward chains.  Returns
+        ``(first slab chunk of the tail, tail keyword arguments)``."""
+        prog, fop = self.program, self.program.fused_op
+        fs = self._fused_step()
+        if fs is not None:
+            fs.run(saved, J, work, self.flat, pack=pack)
+            return 0, fs.tail_kw()
+        rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
+        pre = prereduce_chunk(prog, rng)
+        run_ranges(prog, fop, self.flat, rng, self._streams, pack=pack, bufs=(J, saved, work), prereduce=pre)
+        return pre, {}
 
     def _dp_tail_phase_b(self, loss, grads, terms):
         """DP graph half after the all-reduce: bookkeeping, then Adam + snapshot + weight images."""
@@ -408,9 +425,7 @@ class AdamEngine:
         # persistent step buffers (as in _tail_step): the 1-step and the K-step graph read the
         # weight images that the previous step's dp_tail_b wrote into this one scratch
         J, saved, work, _ = self._step_buffers()
-        rng = self._point_ranges(fop) or [(0, prog.X_all.shape[0], 0, fop.n_blocks)]
-        pre = prereduce_chunk(prog, rng)
-        run_ranges(prog, fop, self.flat, rng, self._streams, pack=False, bufs=(J, saved, work), prereduce=pre)
+        pre, kw = self._run_points(J, saved, work, pack=False)
         n_p = self.flat.numel()
         red_idx = self.red_idx
         if not red_idx or red_idx[0] != 0:
@@ -424,7 +439,7 @@ class AdamEngine:
         grad_view = buf[:n_p]
         hi = prog.hi_op
         jet_hip.dp_tail_a(saved, work, grad_view, fop, total=buf[n_p + n_e:n_p + n_e + 1],
-                          losses=buf[n_p + n_e + 1:], c_first=pre, gextra=hi.grad if hi is not None else None)
+                          losses=buf[n_p + n_e + 1:], c_first=pre, gextra=hi.grad if hi is not None else None, **kw)
         grads = self._fused_grads(fop, grad_view, fop.dlam, fop.dscal)
         if others:
             torch.cat([grads[i].reshape(-1) for i in others], out=buf[n_p:n_p + n_e])
@@ -680,87 +695,35 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
         raise RuntimeError("point ranges: the first range must hold the high-order points")
     cur = torch.cuda.current_stream(flat.device)
     # the high-order points' extra streams (a hundred workgroups of long per-layer chains; they
-    # touch only their own J rows) run on range 0's stream: TDQ_HI_PLACE = serial_before (default:
-    # forward before range 0's forward, gradient between its loss and its backward - with range 0
-    # the longer range (point_ranges) that gradient runs beside range 1's backward), serial_after
-    # (gradient after range 0's backward), side_after / side_before (forward on a third graph branch
-    # beside range 0's forward, joined before its loss).  AC-baseline step on MI355X: serial_before
-    # at cut 0.62 0.231-0.237 ms; at cut 0.38 serial 0.275 ms, side branch 0.302-0.307 ms (three
-    # branches contend for the CUs) - profiles/r4l_place.jsonl, r4q_place_cut_sweep.jsonl,
-    # r4s_place.jsonl.  A third branch for the gradient made hipStreamEndCapture crash on MI355X /
-    # ROCm 7.2.
-    place = os.environ.get("TDQ_HI_PLACE", "serial_before")
-    hs = hop.stream if (hop is not None and place.startswith("side")) else None
-    if place in ("cross", "split") and len(ranges) != 2:
-        place = "serial_before"
-    # split: the adjoint chain between range 0's loss and backward (it needs that loss's adjoints),
-    # the weight-gradient tiles + reduction at the end of range 1's branch (which idles while the
-    # longer range 0 finishes), joined there by an event edge.  Bitwise the same step; measured
-    # 0.2196-0.2205 vs 0.2198-0.2215 ms (noise level: the tiles then steal whole CUs from range 0's
-    # backward, whose 159 KB LDS leaves no room beside it) - profiles/r4split_*; not the default
-    split = place == "split" and hop is not None
-    ev_chain = torch.cuda.Event() if split else None
-    bwd_first = place.endswith("before")
-    if hs is not None:
-        hs.wait_stream(cur)
-        with torch.cuda.stream(hs):
-            hop.forward(J, flat)
+    # touch only their own J rows) run on range 0's stream: their forward before range 0's forward,
+    # their gradient between its loss and its backward - with range 0 the longer range
+    # (point_ranges) that gradient runs beside range 1's backward.  AC-baseline step on MI355X:
+    # 0.231-0.237 ms at cut 0.62; the other placements measured in round 4 (gradient after the
+    # backward, forward on a third graph branch, the two pieces across the branches, the gradient
+    # split between them) were equal or slower - profiles/r4l_place.jsonl, r4q_place_cut_sweep.jsonl,
+    # r4s_place.jsonl, r4u_*, r4split_* - and were removed.
 
-    def chain(k, lo, hi, b0, nb, st):
-        if k == 0 and hop is not None and hs is None:
+    def chain(k, lo, hi, b0, nb):
+        if k == 0 and hop is not None:
             hop.forward(J, flat)
         jet_hip.forward_range(saved, J, lo, hi)
-        if k == 0 and hs is not None:
-            st.wait_stream(hs)
         fop.run_range(J, b0, nb)
-        if k == 0 and split:
-            hop.backward(fop.dJ, flat, part=1)
-            ev_chain.record(st)
-        elif k == 0 and hop is not None and bwd_first:
+        if k == 0 and hop is not None:
             hop.backward(fop.dJ, flat)
         jet_hip.backward_range(saved, fop.dJ, work, lo, hi)
         if k == 0 and prereduce:
             jet_hip.slab_prereduce(saved, work, 0, prereduce)
-        if k == 0 and hop is not None and not bwd_first and not split:
-            hop.backward(fop.dJ, flat)
-        if k == 1 and split:
-            st.wait_event(ev_chain)
-            hop.backward(fop.dJ, flat, part=2)
 
     if len(ranges) == 1:
-        chain(0, *ranges[0], cur)
+        chain(0, *ranges[0])
         return saved, work
     # (keeping one range on the current stream measured the same: the graph runtime picks the
     # hardware queues of its branches itself, and the join still waits ~9 us across queues)
     for st in streams[:len(ranges)]:
         st.wait_stream(cur)
-    if place == "cross" and hop is not None and len(ranges) == 2:
-        # high-order forward at the head of range 1's branch (range 0 waits for it before its loss),
-        # their gradient on range 0's branch between its loss and its backward: the two pieces on
-        # the two branches, still two branches (captured in dependency order).  Measured slower:
-        # 0.297-0.306 vs 0.214 ms - with the cross edge the graph runtime ran range 0's forward
-        # behind range 1's whole chain on one queue (profiles/r4u_*); kept for A/B only
-        (lo0, hi0, b00, nb0), (lo1, hi1, b01, nb1) = ranges
-        st0, st1 = streams[0], streams[1]
-        with torch.cuda.stream(st1):
-            hop.forward(J, flat)
-        with torch.cuda.stream(st0):
-            jet_hip.forward_range(saved, J, lo0, hi0)
-        st0.wait_stream(st1)   # (st1 holds only the high-order forward so far)
-        with torch.cuda.stream(st0):
-            fop.run_range(J, b00, nb0)
-            hop.backward(fop.dJ, flat)
-            jet_hip.backward_range(saved, fop.dJ, work, lo0, hi0)
-            if prereduce:
-                jet_hip.slab_prereduce(saved, work, 0, prereduce)
-        with torch.cuda.stream(st1):
-            jet_hip.forward_range(saved, J, lo1, hi1)
-            fop.run_range(J, b01, nb1)
-            jet_hip.backward_range(saved, fop.dJ, work, lo1, hi1)
-    else:
-        for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
-            with torch.cuda.stream(st):
-                chain(k, lo, hi, b0, nb, st)
+    for k, ((lo, hi, b0, nb), st) in enumerate(zip(ranges, streams)):
+        with torch.cuda.stream(st):
+            chain(k, lo, hi, b0, nb)
     for st in streams[:len(ranges)]:
         cur.wait_stream(st)
     return saved, work
@@ -808,6 +771,15 @@ class LossGradEngine:
                     self._streams = [torch.cuda.Stream(device=self.flat.device) for _ in (self._ranges or ())]
                 hi = prog.hi_op
                 gx = hi.grad if hi is not None else None
+                from .ops import fused_step
+                fs = fused_step.for_program(prog)
+                if fs is not None:
+                    J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                                     rows=fop.fl.n_streams)
+                    work = jet_hip.alloc_backward(saved)
+                    fs.run(saved, J, work, self.flat, pack=True)
+                    jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:], gextra=gx, **fs.tail_kw())
+                    return fg
                 if self._ranges:
                     pre = prereduce_chunk(prog, self._ranges)
                     saved, work = run_ranges(prog, fop, self.flat, self._ranges, self._streams, prereduce=pre)

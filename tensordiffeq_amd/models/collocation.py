@@ -23,7 +23,7 @@ from tqdm.auto import tqdm
 
 from .. import checkpoint
 from ..fit import AdamEngine, LossGradEngine, ParamGroup
-from ..optimizers import Adam, eager_lbfgs, graph_lbfgs
+from ..optimizers import Adam, eager_lbfgs
 from ..output import print_screen
 from ..parallel import dist as pdist
 from .loss import LossProgram, Term
@@ -527,6 +527,10 @@ class CollocationSolverND:
             info["n_iter"] = sum(p["n_iter"] for p in phases)
             info["phases"] = phases
             return info
+        if sched:
+            from .loss import _warn_once
+            _warn_once("newton_schedule is honoured by the device L-BFGS only (newton_eager=True on a GPU, "
+                       "TDQ_LBFGS=device); this L-BFGS path runs one phase at newton_precision")
         return self._fit_lbfgs_phase(newton_iter, None, newton_eager)
 
     def _fit_lbfgs_phase(self, newton_iter, eng=None, newton_eager=True):
@@ -587,15 +591,19 @@ class CollocationSolverND:
             info = {"impl": "host", "n_iter": int(getattr(state, "nIter", 0)), "func_evals": int(fe),
                     "reason": getattr(state, "reason", "?")}
         else:
-            x, _ = graph_lbfgs(eng, flat.detach().clone(), newton_iter, on_eval=on_eval)
+            # the reference's graph-mode L-BFGS (tfp lbfgs_minimize, fit.py:107-122): line-search
+            # L-BFGS with 10 pairs and tolerance 1e-20, state on the device (optimizers/lbfgs_wolfe.py)
+            from ..fit import _use_graphs
+            from ..optimizers import lbfgs_wolfe
+            opt = lbfgs_wolfe.minimize(eng.evaluate_fg, flat.data, newton_iter,
+                                       all_reduce=ctx.all_reduce_ if ctx.is_distributed else None,
+                                       capture_all_reduce=ctx.capturable(flat.numel() + 1),
+                                       use_graph=_use_graphs(self.device), on_iter=on_eval)
             ctx.check_health()
-            with torch.no_grad():
-                flat.copy_(x)
-            f, _ = eng(flat.detach().clone())
-            self.min_loss["l-bfgs"] = float(f)
-            self.best_epoch["l-bfgs"] = newton_iter
-            info = {"impl": "strong-wolfe", "n_iter": int(newton_iter), "func_evals": int(eng.n_evals),
-                    "reason": "maxIter"}
+            self.min_loss["l-bfgs"] = float(opt.min_loss)
+            self.best_epoch["l-bfgs"] = int(opt.n_iter)
+            info = {"impl": "strong-wolfe" + (" (device)" if opt.use_graph else ""), "n_iter": int(opt.n_iter),
+                    "func_evals": int(opt.func_eval), "reason": opt.reason}
         bar.close()
         self._best_flat["l-bfgs"] = flat.detach().clone()
         self.best_model["l-bfgs"] = _FlatModel(self.u_model, self._best_flat["l-bfgs"])

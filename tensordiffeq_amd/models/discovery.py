@@ -253,7 +253,10 @@ class DiscoveryModel:
             info = {"impl": "host", "n_iter": int(getattr(state, "nIter", 0)), "reason": getattr(state, "reason", "?"),
                     "min_loss": float(min_loss)}
         self._sync_user_vars()
-        self.var_history.append(("lbfgs", [float(v.detach()) for v in self.vars]))
+        # (step, values) like the Adam entries: the step count after the L-BFGS iterations
+        last = self.var_history[-1][0] if self.var_history else 0
+        self.var_history.append((int(last) + int(info["n_iter"]), [float(v.detach()) for v in self.vars]))
+        info["var_history_index"] = len(self.var_history) - 1
         if self.verbose and ctx.rank == 0:
             print(f"L-BFGS stopped after {info['n_iter']} iterations: {info['reason']}")
         return info

@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 _lock = threading.Lock()
 _lib = None
@@ -48,10 +48,10 @@ def _declare(lib):
         "tdq_jet_bwd_bf3_range": (I, [P, P, P, P, I, I, I, I, P, I, I, I, P, I, P]),
         "tdq_jet_bf3_pack": (I, [P, P, I, I, P, I, I, I, P]),
         "tdq_step_tail_bf3": (I, [P, P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P] + [P, L, P, P, P, P]
-                              + [P, I, P, I, P, I, P, P]),
+                              + [P, I, P, I, P, I, P, I, P]),
         "tdq_bf3_slab_geometry": (I, [I, I, P, I, I, I, I, P]),
         "tdq_slab_prereduce_bf3": (I, [P, I, I, P, I, I, I, I, I, I, P]),
-        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, I, P, P]),
+        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, I, P, I, P]),
         "tdq_dp_tail_b_bf3": (I, [P, I, I, P, I, I, I, P, I, P, P, P]),
         "tdq_jet_bf3_scratch_floats": (L, [I, I, P, I, I, I]),
         "tdq_jet_bf3_slab_floats": (L, [I, I, P, I, I]),
@@ -59,6 +59,11 @@ def _declare(lib):
         "tdq_jet_fused_active": (I, [I, P, I, I, I, I]),
         "tdq_jet_fused_rows": (I, [I]),
         "tdq_jet_fused_override": (I, [I]),
+        "tdq_fused_step_launch": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, I, P, P, I, I, I, P]),
+        "tdq_fused_params_size": (I, []),
+        "tdq_jet_fused_lds": (I, [I, P, I, I, I, I]),
+        "tdq_device_cus": (I, []),
+        "tdq_slab_floats_rows": (L, [I, I, P, I, I]),
         "tdq_adam_multi": (I, [P, I, P, P, P]),
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
@@ -90,6 +95,7 @@ def _declare(lib):
         "tdq_peer_allreduce": (I, [P, I, I, I, L, I, P, P, P, P, L, P]),
         # run-time specialized fused-loss kernels (csrc/loss_jit.hip, ops/loss_jit.py)
         "tdq_rtc_compile": (I, [c.c_char_p, c.c_char_p, c.c_char_p, P, P, c.c_char_p, I]),
+        "tdq_rtc_compile_ex": (I, [c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, P, P, c.c_char_p, I]),
         "tdq_rtc_free": (None, [P]),
         "tdq_rtc_load": (I, [P, c.c_char_p, P, P]),
         "tdq_rtc_unload": (I, [P]),

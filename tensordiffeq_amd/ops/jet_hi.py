@@ -97,8 +97,6 @@ class HiJetOp:
         self.Z = torch.empty(max(1, int(nz)), dtype=torch.float32, device=device)
         self.work = torch.empty(max(1, int(nw)), dtype=torch.float32, device=device)
         self.grad = torch.zeros(net.flat.numel(), dtype=torch.float32, device=device)
-        # side stream of the step's graph (fit.run_ranges): these kernels overlap the fused ones
-        self.stream = torch.cuda.Stream(device) if torch.device(device).type == "cuda" else None
 
     def _args(self):
         return (self.sizes[0], self._w, self.sizes[-1], len(self.widths), self._si, self._sc)

@@ -236,14 +236,16 @@ def slab_prereduce(saved, work, c0, c1):
 
 
 def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, snapshot, write_images=True,
-              c_first=0, gextra=None):
+              c_first=0, gextra=None, rows=0, lpart=None, n_lblocks=None):
     """End of a single-process Adam step in two launches (csrc/jet_bf3.hip ``tdq_step_tail_bf3``):
     slab reduction + loss reduction + bookkeeping, then the reduced gradient fused into Adam
     (theta, SA weights), the best-weights snapshot and - ``write_images`` - the next step's
     weight images.  ``book``: the engine's device state dict; ``group_array``: ctypes array of
     ``fused._Group`` with theta first; ``c_first``: first-pass chunks below it were pre-reduced
     (:func:`slab_prereduce`); ``gextra``: a gradient added to theta's (the high-order points',
-    :class:`~tensordiffeq_amd.ops.jet_hi.HiJetOp`)."""
+    :class:`~tensordiffeq_amd.ops.jet_hi.HiJetOp`).  ``rows`` / ``lpart`` / ``n_lblocks``: the fused
+    step's slab rows and loss-partial rows (:class:`~.fused_step.FusedStepOp`) instead of the
+    backward's and the loss kernel's."""
     lib = _lib.load()
     X, P, scratch, cfg, spec, S = saved
     hist = book["hist"]
@@ -251,12 +253,13 @@ def step_tail(saved, work, grad, fop, book, counters, group_array, n_groups, sna
     rc = lib.tdq_step_tail_bf3(
         _lib.ptr(work), _lib.ptr(grad), _lib.ptr(scratch) if write_images else None,
         X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], S, *_lo_args(cfg),
-        _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms, fop.n_scal,
+        _lib.ptr(fop.partials if lpart is None else lpart), fop.n_blocks if n_lblocks is None else int(n_lblocks),
+        fop.n_terms, fop.n_scal,
         _lib.ptr(fop.losses), _lib.ptr(fop.total), _lib.ptr(fop.dscal),
         _lib.ptr(hist), int(hist.shape[0]), _lib.ptr(book["epoch"]), _lib.ptr(book["best_loss"]),
         _lib.ptr(book["best_epoch"]), _lib.ptr(book["improved"]), ctypes.cast(carr, ctypes.c_void_p), len(counters),
         ctypes.cast(group_array, ctypes.c_void_p), n_groups,
-        _lib.ptr(snapshot) if snapshot is not None else None, int(c_first), _lib.ptr(gextra),
+        _lib.ptr(snapshot) if snapshot is not None else None, int(c_first), _lib.ptr(gextra), int(rows),
         _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_step_tail_bf3")
 
@@ -288,7 +291,8 @@ class JetMLPFunction(torch.autograd.Function):
         return None, backward_raw((X, P, scratch, cfg, spec, S), dJ), None, None, None
 
 
-def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0, gextra=None):
+def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0, gextra=None, rows=0, lpart=None,
+              n_lblocks=None):
     """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
     slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``).  ``total`` (a 1-element
     view): also write the summed loss there; ``losses`` (an ``n_terms`` view, default
@@ -297,9 +301,10 @@ def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0, gextra
     X, P, scratch, cfg, spec, S = saved
     losses = fop.losses if losses is None else losses
     rc = lib.tdq_dp_tail_a_bf3(_lib.ptr(work), _lib.ptr(grad), X.shape[0], cfg["d_in"], _warg(cfg), cfg["d_out"],
-                               cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials), fop.n_blocks, fop.n_terms,
+                               cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials if lpart is None else lpart),
+                               fop.n_blocks if n_lblocks is None else int(n_lblocks), fop.n_terms,
                                fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total), int(c_first),
-                               _lib.ptr(gextra), _lib.stream_ptr(X.device))
+                               _lib.ptr(gextra), int(rows), _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")
 
 

@@ -130,7 +130,8 @@ def hip_eligible(net, plan, device):
 
 def jet_eval(X, net, params, plan, backend, precision=None):
     if backend == "jet":
-        return jet_forward(X, net.weights(params), plan)
+        # float64 parameters: the whole jet in float64 (the fp64 oracle of smoke() / the tests)
+        return jet_forward(X.to(params.dtype) if params.dtype == torch.float64 else X, net.weights(params), plan)
     if backend == "hip":
         from . import jet_hip
         return jet_hip.JetMLPFunction.apply(X, params, net, plan, precision)

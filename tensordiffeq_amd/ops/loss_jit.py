@@ -80,32 +80,16 @@ def _lit(x):
     return f"{f.hex()}f"
 
 
-def _group_code(P, gi_meta, n_points, S, d_in, n_terms):
-    """Straight-line body of one segment group (mirrors loss_fused_kernel statement by statement)."""
-    block_off, phase, n, seg_off, n_slots, loaded = gi_meta
-    L = []
-    e = L.append
-    e(f"    const int i = (blk - {block_off}) * {LF_BLOCK} + tid - {phase};")
-    e(f"    const bool active = i >= 0 && i < {n};")
-    e("    const int ii = active ? i : 0;")
-    nr = max(1, P.n_regs)
-    e("    float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
-    e("    float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
+def _forward_code(P, e, load):
+    """The program's forward statements; ``load(name, r, a, b)``: the statement of an input opcode
+    (STREAM / COORD / VAL / LAM / SCAL)."""
     consts = P.consts
     for op, r, a, b in P.code:
         name = _OPN[op]
-        if name == "STREAM":
-            e(f"    v{r} = J[(size_t){b} * {n_points} + {seg_off[a]} + ii];")
-        elif name == "COORD":
-            e(f"    v{r} = X[(size_t)({seg_off[a]} + ii) * {d_in} + {b}];")
-        elif name == "VAL":
-            e(f"    v{r} = ptr.val[{a}][ii];")
+        if name in ("STREAM", "COORD", "VAL", "LAM", "SCAL"):
+            e(load(name, r, a, b))
         elif name == "CONST":
             e(f"    v{r} = {_lit(consts[a])};")
-        elif name == "LAM":
-            e(f"    v{r} = ptr.lam[{a}][ii];")
-        elif name == "SCAL":
-            e(f"    v{r} = *ptr.scal[{a}];")
         elif name in ("ADD", "SUB", "MUL", "DIV"):
             sym = {"ADD": "+", "SUB": "-", "MUL": "*", "DIV": "/"}[name]
             e(f"    v{r} = v{a} {sym} v{b};")
@@ -121,22 +105,17 @@ def _group_code(P, gi_meta, n_points, S, d_in, n_terms):
             e(f"    {{ const float x = v{a}; v{r} = x * x; }}")
         else:
             raise ValueError(f"loss JIT: opcode {op}")
-    for (f, w, t, c) in P.outputs:
-        cl = _lit(c)
-        e(f"    {{ const float f = v{f}, w = v{w};")
-        e(f"      const float contrib = active ? {cl} * w * f * f : 0.f;")
-        e("      const float s = block_sum(contrib, red);")
-        e(f"      if (tid == 0) acc[{t}] += s;")
-        e(f"      if (active) {{ a{f} += 2.f * {cl} * w * f; a{w} += {cl} * f * f; }} }}")
+
+
+def _reverse_code(P, e, store):
+    """The program's reverse sweep (adjoints ``a<r>``); ``store(name, r, a, b, g)``: the statement
+    of an input opcode's adjoint (STREAM / LAM / SCAL; None: nothing)."""
+    consts = P.consts
     for op, r, a, b in reversed(P.code):
         name = _OPN[op]
         g = f"a{r}"
-        if name == "STREAM":
-            e(f"    if (active) dJ[(size_t){b} * {n_points} + {seg_off[a]} + i] = {g};")
-        elif name == "LAM":
-            e(f"    if (active) ptr.dlam[{a}][i] = {g};")
-        elif name == "SCAL":
-            e(f"    {{ const float s = block_sum(active ? {g} : 0.f, red); if (tid == 0) acc[{n_terms + a}] += s; }}")
+        if name in ("STREAM", "LAM", "SCAL"):
+            e(store(name, r, a, b, g))
         elif name == "ADD":
             e(f"    {{ const float g = {g}; a{a} += g; a{b} += g; }}")
         elif name == "SUB":
@@ -168,6 +147,44 @@ def _group_code(P, gi_meta, n_points, S, d_in, n_terms):
             e(f"    a{a} += {g} * 0.5f / v{r};")
         elif name == "SQUARE":
             e(f"    a{a} += 2.f * {g} * v{a};")
+
+
+def _group_code(P, gi_meta, n_points, S, d_in, n_terms):
+    """Straight-line body of one segment group (mirrors loss_fused_kernel statement by statement)."""
+    block_off, phase, n, seg_off, n_slots, loaded = gi_meta
+    L = []
+    e = L.append
+    e(f"    const int i = (blk - {block_off}) * {LF_BLOCK} + tid - {phase};")
+    e(f"    const bool active = i >= 0 && i < {n};")
+    e("    const int ii = active ? i : 0;")
+    nr = max(1, P.n_regs)
+    e("    float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
+    e("    float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
+
+    def load(name, r, a, b):
+        return {"STREAM": f"    v{r} = J[(size_t){b} * {n_points} + {seg_off[a]} + ii];",
+                "COORD": f"    v{r} = X[(size_t)({seg_off[a]} + ii) * {d_in} + {b}];",
+                "VAL": f"    v{r} = ptr.val[{a}][ii];",
+                "LAM": f"    v{r} = ptr.lam[{a}][ii];",
+                "SCAL": f"    v{r} = *ptr.scal[{a}];"}[name]
+
+    _forward_code(P, e, load)
+    for (f, w, t, c) in P.outputs:
+        cl = _lit(c)
+        e(f"    {{ const float f = v{f}, w = v{w};")
+        e(f"      const float contrib = active ? {cl} * w * f * f : 0.f;")
+        e("      const float s = block_sum(contrib, red);")
+        e(f"      if (tid == 0) acc[{t}] += s;")
+        e(f"      if (active) {{ a{f} += 2.f * {cl} * w * f; a{w} += {cl} * f * f; }} }}")
+
+    def store(name, r, a, b, g):
+        if name == "STREAM":
+            return f"    if (active) dJ[(size_t){b} * {n_points} + {seg_off[a]} + i] = {g};"
+        if name == "LAM":
+            return f"    if (active) ptr.dlam[{a}][i] = {g};"
+        return f"    {{ const float s = block_sum(active ? {g} : 0.f, red); if (tid == 0) acc[{n_terms + a}] += s; }}"
+
+    _reverse_code(P, e, store)
     # dJ of every (point, stream) the program does not read is written as 0
     zero = []
     for sl in range(n_slots):

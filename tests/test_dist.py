@@ -54,6 +54,9 @@ def _worker(rank, world, port, q):
     res["hist"] = [h["Total Loss"] for h in m.losses]
     m.fit(newton_iter=3)
     res["flat_lbfgs"] = _np(m.u_model.flat)
+    m.fit(newton_iter=4, newton_eager=False)      # line-search L-BFGS through the same all-reduce
+    res["flat_wolfe"] = _np(m.u_model.flat)
+    res["wolfe_evals"] = m.fit_info["lbfgs"]["func_evals"]
     if rank == 0:
         q.put(res)
     ctx.barrier()
@@ -71,6 +74,8 @@ def test_dp_gloo_matches_single_process(world):
     ref_flat = ref.u_model.flat.detach().clone()
     ref.fit(newton_iter=3)
     ref_lbfgs = ref.u_model.flat.detach().clone()
+    ref.fit(newton_iter=4, newton_eager=False)
+    ref_wolfe = ref.u_model.flat.detach().clone()
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -88,6 +93,8 @@ def test_dp_gloo_matches_single_process(world):
     assert res["hist"] == pytest.approx(ref_hist, rel=1e-4)
     assert torch.allclose(_t(res["flat_after"]), ref_flat, atol=1e-5)
     assert torch.allclose(_t(res["flat_lbfgs"]), ref_lbfgs, atol=1e-4)
+    assert torch.allclose(_t(res["flat_wolfe"]), ref_wolfe, atol=1e-4)
+    assert res["wolfe_evals"] == ref.fit_info["lbfgs"]["func_evals"]
 
 
 def _worker_batched(rank, world, port, q):

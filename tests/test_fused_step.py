@@ -1,0 +1,150 @@
+"""One-launch residual training step (ops/fused_step.py, csrc/jet_fused.h MODE 2).
+
+CPU: the generated kernel (headers + the residual group's loss as ``GenLoss``) compiles with hipRTC
+for gfx950 for several traced programs, and eligibility is decided from the program's layout.
+GPU: the fused step's loss, SA-weight gradients and parameter gradient match the separate-launch
+step (saved-activation kernels + specialized loss kernel) at the bf16 level, and a short training
+run follows the same trajectory.
+"""
+import ctypes
+
+import pytest
+import torch
+
+import tensordiffeq_amd as tdq
+from tensordiffeq_amd import fusion
+from tests.test_loss_jit import _model
+from tests.test_solver import allen_cahn, burgers
+
+
+def _deep(problem, layers):
+    torch.manual_seed(0)
+    m = tdq.CollocationSolverND(verbose=False)
+    if problem == "burgers":
+        D, bcs, f = burgers(n_f=400)
+        m.compile(layers, f, D, bcs, backend="jet", device="cpu")
+    else:
+        D, bcs, f, kw = allen_cahn(n_f=400)
+        if problem == "ac_g":
+            kw["g"] = lambda lam: lam ** 2 + 0.5 * torch.exp(-lam)
+        m.compile(layers, f, D, bcs, backend="jet", device="cpu", **kw)
+    return m
+
+
+def _compile_ok(src):
+    from tensordiffeq_amd.ops import _lib, fused_step
+    lib = _lib.load()
+    code, size = ctypes.c_void_p(0), ctypes.c_longlong(0)
+    log = ctypes.create_string_buffer(16384)
+    rc = lib.tdq_rtc_compile_ex(src.encode(), b"t.hip", b"gfx950", fused_step.RTC_OPTS.encode(), ctypes.byref(code),
+                                ctypes.byref(size), log, len(log))
+    assert rc == 0, log.value.decode()[:3000]
+    assert size.value > 0
+    lib.tdq_rtc_free(code)
+
+
+@pytest.mark.parametrize("problem,layers", [("ac", [2, 128, 128, 128, 128, 1]), ("ac_g", [2, 128, 128, 128, 1]),
+                                            ("burgers", [2, 128, 128, 128, 128, 1]), ("ac", [2, 128, 128, 1])])
+def test_fused_step_source_compiles(problem, layers):
+    from tensordiffeq_amd.ops import _lib, fused_step, jet_hip
+    from tensordiffeq_amd.ops.jet_mlp import hip_config
+    from tensordiffeq_amd.ops.loss_fused import FusedLossOp
+    if not _lib.available():
+        pytest.skip("native library not built")
+    m = _deep(problem, layers)
+    prog = m.program()
+    fl = fusion.build(prog, m.lambdas)
+    op = FusedLossOp(fl, prog, m.lambdas, fusion.scalar_values(fl, m.lambdas, None), fl.lam_offsets)
+    # the residual group is the last group, alone on the last segment
+    last = len(prog.segments) - 1
+    assert fl.groups[-1].segs == [last]
+    cfg = hip_config(prog.net, prog.plan, "bf16")
+    lib = _lib.load()
+    lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], 2)
+    if lds < 0:   # a 1-MFMA-layer net ([2, 128, 128, 1]): MODE 2 needs two
+        assert cfg["n_hidden"] - 1 < 2
+        return
+    spec = jet_hip.stream_spec(prog.plan)
+    nso = sum(1 for s in range(cfg["S"]) if spec[3 * s] == 2)
+    gen = fused_step.gen_loss(fl.groups[-1].program, op.n_terms, op.n_terms + op.n_scal)
+    assert "Jv[" in gen and "dJv[" in gen
+    _compile_ok(fused_step.kernel_source(cfg["S"], nso, cfg["n_hidden"] - 1, lds, gen))
+
+
+def test_fused_step_not_on_cpu():
+    from tensordiffeq_amd.ops import fused_step
+    m = _model("ac", "cpu", "jet")
+    prog = m.program()
+    assert fused_step.ineligible(prog, getattr(prog, "fused_op", None)) is not None
+
+
+# --------------------------------------------------------------------------- GPU ---------
+def _acsa(n_f, seed=0, problem="ac-sa"):
+    import bench
+    torch.manual_seed(seed)
+    return bench.PROBLEMS[problem]["build"](n_f, 1, "hip", torch.device("cuda", 0), False, "bf16",
+                                            layers=(2, 128, 128, 128, 128, 1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("problem,n_f", [("ac-sa", 50000), ("ac-sa", 3001), ("ac-baseline", 20000)])
+def test_fused_step_matches_separate_launches(problem, n_f, monkeypatch):
+    """One step's gradient (theta, SA weights) and loss terms: fused vs separate launches."""
+    from tensordiffeq_amd.fit import AdamEngine  # noqa: F401 - engine module import check
+    from tensordiffeq_amd.ops import fused_step, jet_hip
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TDQ_FUSED_STEP", flag)
+        m = _acsa(n_f, problem=problem)
+        with torch.no_grad():   # the boundary terms' SA weights off: the residual points dominate
+            for lam in m.lambdas:
+                if lam.numel() != n_f:
+                    lam.zero_()
+        prog = m.program()
+        fop = prog.fused_op
+        fs = fused_step.for_program(prog)
+        if flag == "1":
+            assert fs is not None, prog.fused_step_reason
+        else:
+            assert fs is None
+        from tensordiffeq_amd.fit import LossGradEngine
+        eng = LossGradEngine(m, prog, m.lambdas)
+        fg = eng.evaluate_fg()
+        torch.cuda.synchronize()
+        out[flag] = (fg.double().cpu(), [d.double().cpu().clone() for d in fop.dlam])
+    g1, g0 = out["1"][0][:-1], out["0"][0][:-1]
+    l1, l0 = out["1"][0][-1].item(), out["0"][0][-1].item()
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    print(f"FUSED_STEP {problem} n_f={n_f} loss {l1:.6e} vs {l0:.6e} grad rel {rel:.3e}")
+    assert abs(l1 - l0) <= 2e-2 * abs(l0), (l1, l0)
+    assert rel < 3e-2, rel
+    for a, b in zip(out["1"][1], out["0"][1]):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < 3e-2
+
+
+@pytest.mark.gpu
+def test_fused_step_training_trajectory(monkeypatch):
+    """AC-SA 20k: 200 Adam steps (graphs + fused tail) with and without the fused step end at the
+    same loss within the bf16 level."""
+    hist = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TDQ_FUSED_STEP", flag)
+        m = _acsa(20000)
+        m.fit(tf_iter=200)
+        assert (getattr(m.program(), "_fused_step", None) is not None) == (flag == "1")
+        hist[flag] = [h["Total Loss"] for h in m.losses]
+    a, b = hist["1"], hist["0"]
+    print(f"FUSED_STEP_TRAJ first {a[0]:.5e} / {b[0]:.5e} last {a[-1]:.5e} / {b[-1]:.5e}")
+    assert abs(a[0] - b[0]) <= 2e-2 * abs(b[0])
+    assert abs(a[-1] - b[-1]) <= 0.1 * abs(b[-1])
+
+
+@pytest.mark.gpu
+def test_fused_step_deterministic(monkeypatch):
+    monkeypatch.setenv("TDQ_FUSED_STEP", "1")
+    m = _acsa(20000)
+    from tensordiffeq_amd.fit import LossGradEngine
+    eng = LossGradEngine(m, m.program(), m.lambdas)
+    a = eng.evaluate_fg().clone()
+    b = eng.evaluate_fg().clone()
+    assert torch.equal(a, b)

@@ -264,6 +264,10 @@ def test_discovery_lbfgs_phase_recovers_coefficient():
     c = float(params[0].detach())
     assert m.fit_info["lbfgs"]["n_iter"] > 10
     assert abs(c - 0.5 / math.pi ** 2) / (0.5 / math.pi ** 2) < 0.05, c
+    # var_history: (step, values) throughout - the L-BFGS entry at Adam steps + its iterations
+    steps = [s for s, _ in m.var_history]
+    assert all(isinstance(s, int) for s in steps) and steps == sorted(steps)
+    assert steps[-1] == 300 + m.fit_info["lbfgs"]["n_iter"]
 
 
 def test_tensordiffeq_alias():

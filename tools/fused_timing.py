@@ -21,7 +21,7 @@ NAMES = {0: "start", 1: "tile loads", 2: "layer 0", 3: "gemm 1", 4: "epi 1", 5: 
          7: "gemm 3", 8: "epi 3 (+out bwd)", 62: "all tiles", 63: "slab row"}
 for k, ly in enumerate((3, 2, 1)):
     b = 10 + 5 * k
-    NAMES.update({b: f"dK_{ly}", b + 1: f"gemm K_{ly}", b + 2: f"barrier {ly}", b + 3: f"epi {ly}",
+    NAMES.update({b: f"gemm K_{ly}", b + 1: f"adjoint + dK_{ly}", b + 2: f"barrier {ly}", b + 3: f"write zb {ly}",
                   b + 4: f"rebuild/barrier {ly}"})
 
 
