@@ -115,10 +115,11 @@ def build_problem(n_glob, world, backend, device, dist, precision=None, seed=123
     return model
 
 
-# c1 parametrization of the discovery problem: "log" (c1 = exp(v) from v = -6, Raissi et al.'s form
-# for a small positive coefficient; c1 median 51 % off over seeds 0-4) or "linear" (the reference's
-# raw c1 = v from 0: 5-11x too large) - profiles/r4disc_c1_param_ab.jsonl.  bench --c1-param.
-DISCOVERY_C1 = "log"
+# c1 parametrization of the discovery problem: "linear" (the reference's raw c1 = v from 0, the
+# default) or "log" (c1 = exp(v) from v = -6, Raissi et al.'s form for a small positive coefficient:
+# NOT the reference program; c1 median 51 % off over seeds 0-4, profiles/r4disc_c1_param_ab.jsonl).
+# Why the linear c1 lands 1-10x high: profiles/r5s2_discovery_c1_explained.md.  bench --c1-param.
+DISCOVERY_C1 = "linear"
 
 
 def discovery_c1(v):
@@ -323,14 +324,15 @@ def allreduce_replay_us(ctx, n_floats, calls=10, reps=20):
 
 
 def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, newton, lbfgs_stop, problem="ac-sa",
-                  layers=None, newton_schedule=None, world=1, npts=None):
+                  layers=None, newton_schedule=None, world=1, npts=None, newton_eager=True):
     """Reference schedule per seed (AC-SA / AC-baseline: examples/AC-SA.py:9-88, Adam + L-BFGS, L2 on
     AC.mat; AC-dist: examples/AC-dist-new.py:48-78, 500k points, ``fit(tf_iter=1001)`` twice, L2 on
     AC.mat; discovery: examples/AC-discovery.py, Adam + L-BFGS over network and coefficients,
     c1 / c2 errors), with phase times and the L-BFGS stop reason.  ``world > 1``: every rank runs
     it under data parallelism - the schedule's point set (50k, or AC-dist's 500k) sharded over the
     ranks with its SA weights, one all-reduce per step - as the reference's distributed example
-    trains with ``dist=True`` before evaluating (AC-dist-new.py:51-54,78)."""
+    trains with ``dist=True`` before evaluating (AC-dist-new.py:51-54,78).  ``newton_eager=False``:
+    the L-BFGS phase is the line-search L-BFGS (the reference's graph mode, fit.py:83-89)."""
     out = []
     spec = PROBLEMS[problem]
     layers = layers or tuple(int(v) for v in spec["layers"].split(","))
@@ -351,7 +353,7 @@ def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, ne
             res = {"seed": sd, "l2": float(l2_on_ac_grid(m))}
         else:
             m.fit(tf_iter=iters)
-            m.fit(newton_iter=newton)
+            m.fit(newton_iter=newton, newton_eager=newton_eager)
             res = {"seed": sd, "l2": float(l2_on_ac_grid(m))}
         info = m.fit_info
         lb = info.get("lbfgs", {})
@@ -360,7 +362,8 @@ def accuracy_runs(seeds, device, backend, precision, newton_precision, iters, ne
         res.update({"adam_s": round(info.get("adam", {}).get("wall_s", 0.0), 3),
                     "lbfgs_s": round(lb.get("wall_s", 0.0), 3),
                     "lbfgs_n_iter": lb.get("n_iter"), "lbfgs_reason": lb.get("reason"),
-                    "lbfgs_stop": lb.get("stop")})
+                    "lbfgs_stop": lb.get("stop"), "lbfgs_impl": lb.get("impl"),
+                    "lbfgs_func_evals": lb.get("func_evals")})
         out.append(res)
         del m
         if device.type == "cuda":
@@ -420,6 +423,8 @@ def main(argv=None):
     ap.add_argument("--newton-precision", default="bf16x3")
     ap.add_argument("--newton-schedule", default=None,
                     help="leading L-BFGS phases of the accuracy runs, 'prec:iters,...' (e.g. bf16:7000)")
+    ap.add_argument("--newton-eager", type=int, default=1, choices=[0, 1],
+                    help="0: the accuracy runs' L-BFGS is the line-search L-BFGS (reference graph mode)")
     ap.add_argument("--lbfgs-stop", default=None, choices=["fixed", "legacy"],
                     help="L-BFGS function-change test (default: the library's, legacy = the reference's)")
     ap.add_argument("--force-dp", action="store_true",
@@ -427,8 +432,9 @@ def main(argv=None):
     ap.add_argument("--precision", default="bf16", choices=["bf16x3", "bf16", "fp32"],
                     help="GEMM precision of the HIP jet kernels (bf16x3 = split-bf16 MFMA, fp32 accumulate; "
                          "bf16 = bf16 x bf16 MFMA, fp32 accumulate)")
-    ap.add_argument("--c1-param", default="log", choices=["log", "linear"],
-                    help="discovery: c1 = exp(v) from v = -6 (default) or the reference's raw c1 = v from 0")
+    ap.add_argument("--c1-param", default="linear", choices=["log", "linear"],
+                    help="discovery: the reference's raw c1 = v from 0 (default) or c1 = exp(v) from v = -6 "
+                         "(not the reference's parametrization)")
     args = ap.parse_args(argv)
     global DISCOVERY_C1
     DISCOVERY_C1 = args.c1_param
@@ -493,7 +499,7 @@ def main(argv=None):
             acc = accuracy_runs(args.acc_seeds, device, args.backend, args.precision, args.newton_precision,
                                 args.acc_iters, args.acc_newton, args.lbfgs_stop, problem=args.problem,
                                 layers=layers, newton_schedule=args.newton_schedule, world=world,
-                                npts=args.acc_npts)
+                                npts=args.acc_npts, newton_eager=bool(args.newton_eager))
         except Exception as e:  # pragma: no cover - reported, never hides the throughput number
             acc_err = f"{type(e).__name__}: {e}"
     dp = None
@@ -533,6 +539,8 @@ def main(argv=None):
         }
         if acc is not None and args.problem == "discovery":
             rec["coefficients"] = [{k: a[k] for k in ("seed", "c1", "c2", "c1_rel_err", "c2_rel_err")} for a in acc]
+            rec["c1_parametrization"] = ("reference: c1 = v from 0" if args.c1_param == "linear"
+                                         else "NON-reference: c1 = exp(v) from v = -6")
             rec["accuracy_schedule"] = (f"Adam {args.acc_iters} ({args.precision}) + L-BFGS {args.acc_newton} "
                                         f"({args.newton_precision}) over network + c1, c2 (c1 parametrization "
                                         f"{args.c1_param}); reference "
@@ -556,6 +564,7 @@ def main(argv=None):
                                             f"{on}; median over seeds {args.acc_seeds}")
             rec["time_to_solution_s"] = [{"adam_s": a["adam_s"], "lbfgs_s": a["lbfgs_s"]} for a in acc]
             rec["lbfgs"] = [{"reason": a["lbfgs_reason"], "n_iter": a["lbfgs_n_iter"], "stop": a["lbfgs_stop"],
+                             "impl": a.get("lbfgs_impl"), "func_evals": a.get("lbfgs_func_evals"),
                              **({"phases": a["lbfgs_phases"]} if a.get("lbfgs_phases") else {})} for a in acc]
         elif acc_err is not None:
             rec["l2_full_schedule"] = None

@@ -48,7 +48,13 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // Optional per-phase timestamps (build with -DTDQ_PHASE_TIMING, tools/phase_timing.py): lane 0
 // of every wave stores s_memtime at numbered points into tdq_ts[(wg * 4 + wave) * 64 + k].
 #ifdef TDQ_PHASE_TIMING
+#ifdef __HIPCC_RTC__
+extern "C" {
+__device__ unsigned long long* tdq_ts;  // run-time compiled kernels: set through hipModuleGetGlobal
+}
+#else
 static __device__ unsigned long long* tdq_ts;  // per translation unit (no -fgpu-rdc)
+#endif
 #define TDQ_TS(k)                                                                                 \
   do {                                                                                            \
     if ((threadIdx.x & 63) == 0)                                                                  \

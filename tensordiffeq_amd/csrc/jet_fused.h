@@ -257,20 +257,24 @@ struct FzParams {
   int srow;
   NetDims d;
   JetSpec sp;
-  // MODE 2: the loss of the points [seg_lo, N) (one residual group of the fused loss program)
+  // MODE 2: the loss program's pointer table (the generated loss maps a point to its group)
   const FzLossPtrs* lptrs;
   float* lpart;         // loss / scalar-gradient partials, row prow + blockIdx.x, nacc floats each
-  int prow, nacc, seg_lo;
+  int prow, nacc, seg_lo;  // (seg_lo: unused by the generated loss)
 };
 
-// MODE 0 / 1 builds: no loss code
+// MODE 0 / 1 builds: no loss code.  The MODE 2 interface (ops/fused_step.py generates it):
+//   eval<S, OQ>(jv, xs, t, n, N, ptrs, ubs, acc) on the tile's point-thread t (point n of the
+//   fused point set): J of the tile's point k, stream s at jv[(s * FZ_PT + k) * OQ], coordinates
+//   at xs[k * TDQ_MAXD + j]; writes dJ of the points it owns to ubs[(s * FZ_PT + k) * 4] (zero for
+//   points outside every loss group) and adds loss / scalar-gradient sums to acc
 struct FzNoLoss {
   static constexpr int NACC = 1;
-  template <int S>
-  __device__ static void eval(const float (&)[S], const float*, int, bool, const FzLossPtrs&, float (&dJv)[S],
+  template <int S, int OQ>
+  __device__ static void eval(const float*, const float*, int t, int, int, const FzLossPtrs&, float* ubs,
                               float (&)[1]) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) dJv[s] = 0.f;
+    for (int s = 0; s < S; ++s) ubs[(s * FZ_PT + t) * 4] = 0.f;
   }
 };
 
@@ -482,24 +486,22 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       }
     } else {
       if constexpr (MODE == 2) {
-        // ---- J of the tile's points (wave-ordered sums of the partial dots), the per-point loss
-        // (generated code: residual, SA weighting, its reverse sweep) -> dJ into ubs ----------
-        if (tid < FZ_PT) {
-          const int n = pb + tid;
-          const bool active = n < N;
-          float Jv[S], dJv[S];
+        // ---- J of the tile's points: the wave-ordered sums of the partial dots, in place of wave
+        // 0's (each (stream, point) entry read and written by one thread) ----------------------
+        if (tid < S * FZ_PT) {
+          const int s = tid / FZ_PT, pt = tid - s * FZ_PT;
+          float a = outp[((0 * S + s) * FZ_PT + pt) * OQ];
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            float a = outp[((0 * S + s) * FZ_PT + tid) * OQ];
-#pragma unroll
-            for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + tid) * OQ];
-            Jv[s] = s == 0 ? a + aux[aux_bo(d, W)] : a;
-          }
-          LossF::template eval<S>(Jv, xs + tid * TDQ_MAXD, n - P.seg_lo, active, *P.lptrs, dJv, lacc);
-#pragma unroll
-          for (int s = 0; s < S; ++s) ubs[(s * FZ_PT + tid) * 4] = active ? dJv[s] : 0.f;
+          for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * OQ];
+          outp[((0 * S + s) * FZ_PT + pt) * OQ] = s == 0 ? a + aux[aux_bo(d, W)] : a;
         }
         __syncthreads();
+        // ---- the per-point loss (generated code: every loss group of the program - residual, SA
+        // weighting, boundary terms with the two points of a periodic pair side by side - and its
+        // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
+        if (tid < FZ_PT) LossF::template eval<S, OQ>(outp, xs, tid, pb + tid, N, *P.lptrs, ubs, lacc);
+        __syncthreads();
+        FZ_TS(9);
         // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
 #pragma unroll
         for (int oo = 0; oo < OPW; ++oo) {

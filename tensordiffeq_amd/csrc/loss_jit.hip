@@ -100,6 +100,16 @@ int tdq_rtc_load(const void* code, const char* name, void** module, void** func)
   return 0;
 }
 
+// write a pointer into a run-time compiled module's extern "C" __device__ pointer variable
+int tdq_rtc_set_global_ptr(void* module, const char* name, void* value) {
+  hipDeviceptr_t p = nullptr;
+  size_t bytes = 0;
+  hipError_t e = hipModuleGetGlobal(&p, &bytes, (hipModule_t)module, name);
+  if (e != hipSuccess) return (int)e;
+  if (bytes != sizeof(void*)) return (int)hipErrorInvalidValue;
+  return (int)hipMemcpyHtoD(p, &value, sizeof(void*));
+}
+
 int tdq_rtc_unload(void* module) { return (int)hipModuleUnload((hipModule_t)module); }
 
 // One launch of a specialized loss kernel over blocks [blk0, blk0 + nblk) (128 threads each, the

@@ -381,6 +381,7 @@ class AdamEngine:
                 self._graph_saved = self._tail_saved
         else:
             tail = self._tail_eligible()
+            self.dist.settle_collective(self._bucket_floats())
             if self._coll_in_graph():
                 # RCCL: the bucket all-reduce is captured in the step graph - one replay per step
                 g = torch.cuda.CUDAGraph()

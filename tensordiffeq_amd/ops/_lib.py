@@ -99,6 +99,7 @@ def _declare(lib):
         "tdq_rtc_free": (None, [P]),
         "tdq_rtc_load": (I, [P, c.c_char_p, P, P]),
         "tdq_rtc_unload": (I, [P]),
+        "tdq_rtc_set_global_ptr": (I, [P, c.c_char_p, P]),
         "tdq_loss_jit_range": (I, [P, P, P, P, P, P, I, I, P]),
     }
     for name, (res, args) in sig.items():

@@ -1,22 +1,22 @@
-"""One-launch training step of the residual points: forward -> loss -> backward (hipRTC).
+"""One-launch training step: forward -> loss -> backward of every point (hipRTC).
 
 The persistent point-tile kernel of ``csrc/jet_fused.h`` in its MODE 2 runs, per 32-point tile,
-the Taylor-jet forward of the network, the residual group's per-point loss and its reverse sweep,
-and the recompute backward into the tile loop's register-resident weight gradient - so the residual
-points' J and dJ never touch HBM and the step has no forward / loss / backward launch boundaries.
-The loss is the traced program of the fused loss (:mod:`.loss_jit` emits the same statements, here
-as the body of a ``GenLoss::eval`` the kernel calls per point), so the kernel is compiled at run
-time with hipRTC once per (network shape, loss program) and cached per process.
+the Taylor-jet forward of the network, the per-point loss of the fused loss program and its
+reverse sweep, and the recompute backward into the tile loop's register-resident weight gradient -
+so J and dJ never touch HBM and the step has no forward / loss / backward launch boundaries.  The
+loss is the traced program of the fused loss (:mod:`.loss_jit` emits the same statements, here as
+the body of a ``GenLoss::eval`` the kernel calls per point: every loss group, with the two points
+of a periodic pair side by side in the tile), so the kernel is compiled at run time with hipRTC
+once per (network shape, loss program) and cached per process.  A step is then the fused launch
+plus the two-launch step tail (``jet_hip.step_tail`` / ``dp_tail_a``: slab reduction, loss
+bookkeeping, Adam).
 
-The boundary / initial points (the groups before the residual segment) keep the saved-activation
-chain of ``csrc/jet_bf3.h`` (forward range -> loss blocks -> backward range) on a side stream beside
-the fused launch, which leaves them CUs (``FusedStepOp.G``); the fused step tail
-(``jet_hip.step_tail`` / ``dp_tail_a``) then reduces both sets of gradient-slab rows and loss
-partials and runs Adam.
+Programs with order-3/4 boundary streams (``jet_hi.hip``) run only their residual group fused and
+keep the boundary chain (high-order streams, saved-activation forward range, loss blocks, backward
+range) on a side stream beside it.
 
 The reference's step is tensordiffeq/models.py:90-135 (``train_op_inner`` / ``update_loss``): a
-tape over the network, the residual and the boundary MSEs, then the optimizer - here one fused
-launch for the 98% of points that are residual points.
+tape over the network, the residual and the boundary MSEs, then the optimizer.
 
 ``TDQ_FUSED_STEP=0`` keeps the separate launches (``fit.run_ranges``).
 """
@@ -38,6 +38,11 @@ _HEADERS = ("common.h", "jet_common.h", "jet_bf3.h", "jet_fused.h")
 RTC_OPTS = "-O3 -std=c++17 -fno-slp-vectorize -munsafe-fp-atomics"
 
 
+def _opts():
+    """hipRTC options; ``TDQ_FUSED_STEP_TIMING=1`` adds the phase stamps (tools/fused_step_timing.py)."""
+    return RTC_OPTS + (" -DTDQ_PHASE_TIMING" if os.environ.get("TDQ_FUSED_STEP_TIMING") == "1" else "")
+
+
 def enabled():
     return os.environ.get("TDQ_FUSED_STEP", "1") != "0"
 
@@ -57,48 +62,71 @@ def header_source():
     return "\n".join(out)
 
 
-def gen_loss(P, n_terms, nacc):
-    """``struct GenLoss`` of one single-segment group program: the loss statements of
-    :func:`.loss_jit._group_code` per point (J streams and coordinates from the kernel's registers,
-    loss / scalar-gradient sums into the thread's accumulators, dJ into ``dJv``)."""
+def gen_loss(groups, n_terms, nacc, S):
+    """``struct GenLoss`` of the loss groups laid out in the fused point set.  ``groups``: one
+    ``(program, start, n_slots, n)`` per group - its ``n`` instances occupy points ``start + k``
+    (one slot) or the pairs ``start + 2k, start + 2k + 1`` (two slots: a periodic pair side by side,
+    ``start`` even, so a pair never straddles a 32-point tile).  The statements are those of
+    :func:`.loss_jit._group_code` per point: J streams / coordinates from the tile (the partner's
+    from the next point-thread), loss / scalar-gradient sums into the thread's accumulators, dJ
+    of the instance's points into the tile's ``ubs``.  Points outside every group get dJ = 0."""
     L = []
     e = L.append
-    nr = max(1, P.n_regs)
     e("struct GenLoss {")
     e(f"  static constexpr int NACC = {max(1, nacc)};")
-    e("  template <int S>")
-    e("  __device__ static void eval(const float (&Jv)[S], const float* xr, int i, bool active, "
-      "const FzLossPtrs& ptr, float (&dJv)[S], float (&acc)[NACC]) {")
-    e("    const int ii = active ? i : 0;")
+    e("  template <int S, int OQ>")
+    e("  __device__ static void eval(const float* jv, const float* xs, int t, int n, int N, "
+      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC]) {")
+    e("    #define JV(s_, k_) jv[((s_) * FZ_PT + (k_)) * OQ]")
+    e("    #define UB(s_, k_) ubs[((s_) * FZ_PT + (k_)) * 4]")
+    kw = "if"
+    for (P, start, ns, n) in groups:
+        end = start + ns * n
+        e(f"    {kw} (n >= {start} && n < {end} && n < N) {{")
+        kw = "else if"
+        if ns == 2:
+            e(f"      if ((n - {start}) & 1) return;   // the pair's first point-thread owns it")
+            e(f"      const int i = (n - {start}) >> 1;")
+        else:
+            e(f"      const int i = n - {start};")
+        nr = max(1, P.n_regs)
+        e("      float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
+        e("      float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
+        e("      float " + ", ".join(f"dj{sl}_{b} = 0.f" for sl in range(ns) for b in range(S)) + ";")
+
+        def load(name, r, a, b, ns=ns):
+            if name in ("STREAM", "COORD") and a >= ns:
+                raise ValueError("fused step: slot outside the group")
+            return {"STREAM": f"      v{r} = JV({b}, t + {a});",
+                    "COORD": f"      v{r} = xs[(t + {a}) * TDQ_MAXD + {b}];",
+                    "VAL": f"      v{r} = ptr.val[{a}][i];",
+                    "LAM": f"      v{r} = ptr.lam[{a}][i];",
+                    "SCAL": f"      v{r} = *ptr.scal[{a}];"}[name]
+
+        loss_jit._forward_code(P, e, load)
+        for (f, w, tt, c) in P.outputs:
+            cl = loss_jit._lit(c)
+            e(f"      {{ const float f = v{f}, w = v{w};")
+            e(f"        acc[{tt}] += {cl} * w * f * f;")
+            e(f"        a{f} += 2.f * {cl} * w * f; a{w} += {cl} * f * f; }}")
+
+        def store(name, r, a, b, g):
+            if name == "STREAM":
+                if b >= S:
+                    raise ValueError("fused step: stream outside the jet plan")
+                return f"      dj{a}_{b} += {g};"
+            if name == "LAM":
+                return f"      ptr.dlam[{a}][i] = {g};"
+            return f"      acc[{n_terms + a}] += {g};"
+
+        loss_jit._reverse_code(P, e, store)
+        e("      " + " ".join(f"UB({b}, t + {sl}) = dj{sl}_{b};" for sl in range(ns) for b in range(S)))
+        e("      return;")
+        e("    }")
     e("    #pragma unroll")
-    e("    for (int s = 0; s < S; ++s) dJv[s] = 0.f;")
-    e("    float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
-    e("    float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
-
-    def load(name, r, a, b):
-        if name in ("STREAM", "COORD") and a != 0:
-            raise ValueError("fused step: the residual group reads one segment")
-        return {"STREAM": f"    v{r} = Jv[{b}];",
-                "COORD": f"    v{r} = xr[{b}];",
-                "VAL": f"    v{r} = ptr.val[{a}][ii];",
-                "LAM": f"    v{r} = ptr.lam[{a}][ii];",
-                "SCAL": f"    v{r} = *ptr.scal[{a}];"}[name]
-
-    loss_jit._forward_code(P, e, load)
-    for (f, w, t, c) in P.outputs:
-        cl = loss_jit._lit(c)
-        e(f"    {{ const float f = v{f}, w = v{w};")
-        e(f"      acc[{t}] += active ? {cl} * w * f * f : 0.f;")
-        e(f"      if (active) {{ a{f} += 2.f * {cl} * w * f; a{w} += {cl} * f * f; }} }}")
-
-    def store(name, r, a, b, g):
-        if name == "STREAM":
-            return f"    dJv[{b}] += {g};"
-        if name == "LAM":
-            return f"    if (active) ptr.dlam[{a}][i] = {g};"
-        return f"    acc[{n_terms + a}] += active ? {g} : 0.f;"
-
-    loss_jit._reverse_code(P, e, store)
+    e("    for (int s = 0; s < S; ++s) UB(s, t) = 0.f;")
+    e("    #undef JV")
+    e("    #undef UB")
     e("  }")
     e("};")
     return "\n".join(L)
@@ -114,13 +142,15 @@ def kernel_source(S, nso, LM, lds, gen):
 
 
 def _compile(src):
+    """``(module, function)`` of the fused-step kernel in ``src`` (compiled once per process)."""
     lib = _lib.load(required=True)
     arch = loss_jit.device_arch()
-    key = hashlib.sha256((arch + RTC_OPTS + src).encode()).hexdigest()
+    opts = _opts()
+    key = hashlib.sha256((arch + opts + src).encode()).hexdigest()
     if key not in _CACHE:
         code, size = ctypes.c_void_p(0), ctypes.c_longlong(0)
         log = ctypes.create_string_buffer(16384)
-        rc = lib.tdq_rtc_compile_ex(src.encode(), b"tdq_fused_step.hip", arch.encode(), RTC_OPTS.encode(),
+        rc = lib.tdq_rtc_compile_ex(src.encode(), b"tdq_fused_step.hip", arch.encode(), opts.encode(),
                                     ctypes.byref(code), ctypes.byref(size), log, len(log))
         if rc != 0:
             raise RuntimeError(f"hipRTC compile failed ({rc}): {log.value.decode(errors='replace')[:2000]}")
@@ -131,7 +161,7 @@ def _compile(src):
         finally:
             lib.tdq_rtc_free(code)
         _CACHE[key] = (mod, fn)
-    return _CACHE[key][1]
+    return _CACHE[key]
 
 
 def ineligible(prog, fop):
@@ -154,66 +184,109 @@ def ineligible(prog, fop):
     if lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], 2) < 0:
         return f"network {cfg['widths']} / S={cfg['S']} (width-128 MFMA layers 2-3, S <= 4)"
     fl = fop.fl
-    last = len(prog.segments) - 1
-    gr = fl.groups[-1]
-    if gr.segs != [last] or any(last in g.segs for g in fl.groups[:-1]):
-        return "the last segment is not a group of its own"
-    if any(s >= cfg["S"] for (_, s) in gr.program.stream_regs):
-        return "the residual loss reads streams outside the jet plan"
-    seg = prog.segments[last]
-    if seg.offset + gr.n != prog.X_all.shape[0]:
-        return "the residual segment does not end the point set"
-    if getattr(prog, "hi_op", None) is not None and prog.n_hi > seg.offset:
-        return "high-order points inside the residual segment"
+    for gr in fl.groups:
+        if any(s >= cfg["S"] for (_, s) in gr.program.stream_regs) and not _mixed(prog):
+            return "a loss group reads streams outside the jet plan"
+    if _mixed(prog):
+        # high-order boundary points (jet_hi.hip streams): only the residual group runs fused
+        last = len(prog.segments) - 1
+        gr = fl.groups[-1]
+        if gr.segs != [last] or any(last in g.segs for g in fl.groups[:-1]):
+            return "the last segment is not a group of its own"
+        if any(s >= cfg["S"] for (_, s) in gr.program.stream_regs):
+            return "the residual loss reads streams outside the jet plan"
+        seg = prog.segments[last]
+        if seg.offset + gr.n != prog.X_all.shape[0]:
+            return "the residual segment does not end the point set"
+        if prog.n_hi > seg.offset:
+            return "high-order points inside the residual segment"
     return None
 
 
+def _mixed(prog):
+    return getattr(prog, "hi_op", None) is not None
+
+
 class FusedStepOp:
-    """The fused step of a :class:`~tensordiffeq_amd.models.loss.LossProgram` whose residual group
-    is its last segment (built by :func:`for_program`)."""
+    """The fused training step of a :class:`~tensordiffeq_amd.models.loss.LossProgram` (built by
+    :func:`for_program`).
+
+    Single-plan programs: EVERY loss group runs in the one launch - the points re-laid out once
+    into a fused point set (each group's instances contiguous, a periodic group's two segments
+    interleaved pair by pair), so a step is the fused launch + the two-launch step tail.  Mixed
+    programs (order-3/4 boundary streams from jet_hi.hip): the residual group runs fused over its
+    own segment, the boundary chain (high-order streams, saved-activation forward, loss blocks,
+    backward) on a side stream beside it."""
 
     def __init__(self, prog, fop):
         lib = _lib.load(required=True)
         self.prog, self.fop = prog, fop
         cfg = self.cfg = hip_config(prog.net, prog.plan, prog.precision)
-        N = self.N = prog.X_all.shape[0]
         fl = fop.fl
-        self.seg_lo = prog.segments[-1].offset
-        self.b_res = fop.group_meta[-1][0]         # the residual group's first loss block
+        S = cfg["S"]
         self.nacc = fop.n_terms + fop.n_scal
         spec = jet_hip.stream_spec(prog.plan)
-        S = cfg["S"]
         nso = sum(1 for s in range(S) if spec[3 * s] == 2)
         LM = cfg["n_hidden"] - 1
         lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S, 2)
         if lds < 0 or lds > 160 * 1024:
             raise ValueError(f"fused step: {lds} bytes of LDS")
-        self.source = kernel_source(S, nso, LM, lds, gen_loss(fl.groups[-1].program, fop.n_terms, self.nacc))
-        self.func = _compile(self.source)
-        # boundary points: the saved-activation chain over [0, p_bc) - its backward workgroups own
-        # slab rows [0, srow); points [seg_lo, p_bc) ride along with dJ = 0
-        pts_b = jet_hip.slab_geometry(cfg, N)[0]
-        self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
-        self.srow = -(-self.p_bc // pts_b)
-        ntiles = -(-(N - self.seg_lo) // 32)
+        self.lds = lds
+        N = prog.X_all.shape[0]
+        dev = prog.device
+        self.mixed = _mixed(prog)
+        if not self.mixed:
+            # the fused point set: groups in program order, pair groups on even offsets
+            layout, idx, pos = [], [], 0
+            for gr in fl.groups:
+                ns = len(gr.segs)
+                if ns == 2 and pos % 2:
+                    idx.append(-1)
+                    pos += 1
+                layout.append((gr.program, pos, ns, gr.n))
+                offs = [prog.segments[sg].offset for sg in gr.segs]
+                for k in range(gr.n):
+                    idx.extend(o + k for o in offs)
+                pos += ns * gr.n
+            ix = torch.tensor(idx, dtype=torch.long, device=dev)
+            X_f = prog.X_all[ix.clamp_min(0)].clone()
+            X_f[ix < 0] = 0.0
+            self.X = X_f.contiguous()
+            self.N, self.p_lo, self.srow, self.b_res, self.p_bc, self.seg_lo = pos, 0, 0, 0, 0, 0
+        else:
+            self.seg_lo = prog.segments[-1].offset
+            layout = [(fl.groups[-1].program, self.seg_lo, 1, fl.groups[-1].n)]
+            self.X = None                               # the program's X_all
+            self.N, self.p_lo = N, self.seg_lo
+            self.b_res = fop.group_meta[-1][0]          # the residual group's first loss block
+            # boundary points: the saved-activation chain over [0, p_bc) - its backward workgroups
+            # own slab rows [0, srow); points [seg_lo, p_bc) ride along with dJ = 0
+            pts_b = jet_hip.slab_geometry(cfg, N)[0]
+            self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
+            self.srow = -(-self.p_bc // pts_b)
+        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S))
+        self.module, self.func = _compile(self.source)
+        ntiles = -(-(self.N - self.p_lo) // 32)
         cus = max(1, lib.tdq_device_cus())
         rounds = -(-ntiles // cus)
-        # the fewest workgroups with the same tiles per workgroup: the CUs left over run the
-        # boundary chain beside the fused launch (AC-SA 50k: 1563 tiles, 224 workgroups x 7)
-        self.G = min(-(-ntiles // rounds), fop.n_blocks - self.b_res)
-        need = lib.tdq_slab_floats_rows(self.srow + self.G, cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"],
-                                        cfg["n_hidden"])
-        cap = lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"])
-        if self.G < 1 or need < 0 or need > cap:
-            raise ValueError(f"fused step: {self.srow + self.G} slab rows do not fit the backward's buffer")
+        # the fewest workgroups with the same tiles per workgroup (AC-SA 50k: 1592 tiles, 228 x 7):
+        # in the mixed layout the CUs left over run the boundary chain beside the fused launch
+        self.G = -(-ntiles // rounds)
+        if self.mixed:   # the fused rows follow the boundary loss blocks' rows in fop.partials
+            self.G = min(self.G, fop.n_blocks - self.b_res)
         self.rows = self.srow + self.G
+        need = lib.tdq_slab_floats_rows(self.rows, cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"])
+        cap = lib.tdq_jet_bf3_slab_floats(N, cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"])
+        if need < 0 or need > cap:
+            raise ValueError(f"fused step: {self.rows} slab rows do not fit the backward's buffer")
+        # loss partials: the boundary loss blocks' rows (mixed) then one row per fused workgroup
         self.n_lblocks = self.b_res + self.G
-        self.lds = lds
-        self._side = torch.cuda.Stream(device=prog.device) if self.p_bc > 0 else None
+        self.lpart = torch.zeros(max(1, self.n_lblocks * self.nacc), dtype=torch.float32, device=dev)
+        self._side = torch.cuda.Stream(device=dev) if self.p_bc > 0 else None
 
     def run(self, saved, J, work, flat, pack=True):
-        """The step's gradient slabs and loss partials: boundary chain on a side stream, the fused
-        launch on the current one (joined before return).  ``saved`` / ``J`` / ``work``: the
+        """The step's gradient slabs and loss partials (the fused launch; mixed programs: plus the
+        boundary chain on a side stream, joined before return).  ``saved`` / ``J`` / ``work``: the
         persistent step buffers of ``jet_hip.alloc_forward`` / ``alloc_backward``."""
         lib = _lib.load()
         fop, cfg = self.fop, self.cfg
@@ -221,33 +294,54 @@ class FusedStepOp:
             jet_hip.pack_images(saved)
         cur = torch.cuda.current_stream(flat.device)
         side = self._side
-        hop = self.prog.hi_op   # mixed programs: the high-order boundary points' extra streams
-        if side is not None:
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                if hop is not None:
-                    hop.forward(J, flat)
-                jet_hip.forward_range(saved, J, 0, self.p_bc)
-                if self.b_res > 0:
-                    fop.run_range(J, 0, self.b_res)
-                if hop is not None:
-                    hop.backward(fop.dJ, flat)
-                if self.p_bc > self.seg_lo:
-                    fop.dJ[:, self.seg_lo:self.p_bc].zero_()
-                jet_hip.backward_range(saved, fop.dJ, work, 0, self.p_bc)
+        hop = self.prog.hi_op
         X, _, scratch, _, spec, S = saved
         spec_arr = (ctypes.c_int * len(spec))(*spec)
-        rc = lib.tdq_fused_step_launch(self.func, _lib.ptr(X), _lib.ptr(scratch), _lib.ptr(work), self.N,
-                                       cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S, spec_arr,
-                                       self.seg_lo, self.srow, self.G, _lib.ptr(fop.ptrs), _lib.ptr(fop.partials),
-                                       self.b_res, self.nacc, self.seg_lo, _lib.stream_ptr(flat.device))
-        _lib.check(rc, "tdq_fused_step_launch")
-        if side is not None:
-            cur.wait_stream(side)
+        Xf = self.X if self.X is not None else X
+        lpart = fop.partials if self.mixed else self.lpart
+
+        def boundary():
+            hop.forward(J, flat)
+            jet_hip.forward_range(saved, J, 0, self.p_bc)
+            if self.b_res > 0:
+                fop.run_range(J, 0, self.b_res)
+            hop.backward(fop.dJ, flat)
+            if self.p_bc > self.seg_lo:
+                fop.dJ[:, self.seg_lo:self.p_bc].zero_()
+            jet_hip.backward_range(saved, fop.dJ, work, 0, self.p_bc)
+
+        def fused():
+            rc = lib.tdq_fused_step_launch(self.func, _lib.ptr(Xf), _lib.ptr(scratch), _lib.ptr(work), self.N,
+                                           cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S,
+                                           spec_arr, self.p_lo, self.srow, self.G, _lib.ptr(fop.ptrs),
+                                           _lib.ptr(lpart), self.b_res, self.nacc, self.seg_lo,
+                                           _lib.stream_ptr(flat.device))
+            _lib.check(rc, "tdq_fused_step_launch")
+
+        if side is None:
+            fused()
+            return
+        # the fused launch is the graph's first node and the boundary branch forks from before it:
+        # MI355X, AC-SA (side chain layout): 0.1697 vs 0.1813 ms/step with the branch captured
+        # first (profiles/r5ord_*: the fused kernel then started ~6 us later and the join waited
+        # ~10 us on the other queue)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        fused()
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            boundary()
+        cur.wait_stream(side)
+
+    def set_timing_buffer(self, buf):
+        """Phase-stamp build only: the int64 buffer of the stamps ([G * 8 waves][64])."""
+        _lib.check(_lib.load().tdq_rtc_set_global_ptr(self.module, b"tdq_ts", ctypes.c_void_p(buf.data_ptr())),
+                   "tdq_rtc_set_global_ptr")
 
     def tail_kw(self):
         """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows."""
-        return {"rows": self.rows, "lpart": self.fop.partials, "n_lblocks": self.n_lblocks}
+        return {"rows": self.rows, "lpart": self.fop.partials if self.mixed else self.lpart,
+                "n_lblocks": self.n_lblocks}
 
 
 def for_program(prog):

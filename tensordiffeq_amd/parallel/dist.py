@@ -83,6 +83,13 @@ class DistContext:
                 dist.all_reduce(buf, op=dist.ReduceOp.SUM)
         return buf
 
+    def settle_collective(self, n_floats):
+        """Collective: re-decide peer vs RCCL at the step's real bucket size (parallel/peer.py
+        ``settle``, in-graph replay timings); no-op without a peer communicator."""
+        if self.is_distributed and self.peer is not None:
+            from . import peer
+            peer.settle(self, n_floats)
+
     def check_health(self):
         """Raise if the peer all-reduce ever timed out waiting for a rank (read at the
         progress / NaN-check cadence, never inside a step)."""

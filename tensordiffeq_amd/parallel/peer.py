@@ -144,6 +144,7 @@ def _self_test(comm, n):
 
 
 def _time_us(fn, buf, ctx, reps=30):
+    """Host-launched per-call time (a collective that cannot be captured: gloo)."""
     for _ in range(3):
         fn(buf)
     torch.cuda.synchronize(buf.device)
@@ -153,6 +154,66 @@ def _time_us(fn, buf, ctx, reps=30):
         fn(buf)
     torch.cuda.synchronize(buf.device)
     return (time.perf_counter() - t0) / reps * 1e6
+
+
+def _time_us_graph(fn, buf, ctx, calls=10, reps=20):
+    """Per-call time the way the DP step runs the collective: ``calls`` of them captured in one
+    HIP graph, the graph replayed ``reps`` times (bench.allreduce_replay_us measures the same)."""
+    from ..graphs import capture_graph
+    dev = buf.device
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        fn(buf)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with capture_graph(g):
+        for _ in range(calls):
+            fn(buf)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / (reps * calls) * 1e6
+
+
+def _compare(comm, ctx, n_floats):
+    """``(peer us, torch.distributed us)`` per call on an ``n_floats`` buffer, max over ranks: both
+    in-graph when the backend's collective can be captured (RCCL), else the torch one host-launched."""
+    W = ctx.world
+    buf = torch.randn(int(n_floats), device=ctx.device)
+    t_peer = _time_us_graph(comm.all_reduce_, buf, ctx)
+
+    def ref(b):
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+
+    t_ref = _time_us_graph(ref, buf, ctx) if ctx.backend == "nccl" else _time_us(ref, buf, ctx)
+    ts = _gather([t_peer, t_ref], W)
+    return max(x[0] for x in ts), max(x[1] for x in ts)
+
+
+def settle(ctx, n_floats):
+    """Collective (every rank, same point): re-decide peer vs torch.distributed at the step's REAL
+    bucket size with in-graph replay timings (``auto`` mode only; once per size).  Keeps the
+    faster; records the timings in ``ctx.allreduce_info["settled"]``."""
+    comm = ctx.peer
+    if comm is None or mode() != "auto" or ctx.backend != "nccl" or int(n_floats) > comm.cap:
+        return
+    if ctx.allreduce_info.get("settled", {}).get("floats") == int(n_floats):
+        return
+    t_peer, t_ref = _compare(comm, ctx, n_floats)
+    use = _gather(bool(t_peer < t_ref) and comm.err.item() == 0, ctx.world)
+    ctx.allreduce_info["settled"] = {"floats": int(n_floats), "peer_us": round(t_peer, 2),
+                                     "torch_us": round(t_ref, 2), "choice": "peer" if all(use) else "torch"}
+    if not all(use):
+        comm.close()
+        ctx.peer = None
+        ctx.allreduce_info["impl"] = "torch.distributed"
+        ctx.allreduce_info["peer"] = "off: slower in-graph at the step's bucket size"
 
 
 def setup(ctx, bench_floats=49_408):
@@ -208,17 +269,14 @@ def setup(ctx, bench_floats=49_408):
         info["peer"] = f"off: self-test failed ({err or 'wrong sums or a timeout'})"
         comm.close()
         return None
-    buf = torch.randn(bench_floats, device=ctx.device)
-    t_peer = _time_us(comm.all_reduce_, buf, ctx)
-    _log(f"setup: peer {t_peer:.1f} us")
+    # in-graph replay timings (how the step runs the collective); settle() re-decides at the
+    # step's real bucket size once the engine knows it
     if m == "auto":
-        t_ref = _time_us(lambda b: dist.all_reduce(b, op=dist.ReduceOp.SUM), buf, ctx)
+        t_peer, t_ref = _compare(comm, ctx, bench_floats)
     else:
-        t_ref = float("nan")
-    _log(f"setup: torch.distributed {t_ref:.1f} us")
-    ts = _gather([t_peer, t_ref], W)
-    t_peer = max(x[0] for x in ts)
-    t_ref = max(x[1] for x in ts)
+        t_peer, t_ref = _time_us_graph(comm.all_reduce_, torch.randn(bench_floats, device=ctx.device), ctx), float("nan")
+        t_peer = max(_gather(t_peer, W))
+    _log(f"setup: peer {t_peer:.1f} us, torch.distributed {t_ref:.1f} us")
     info.update(peer_us=round(t_peer, 2), torch_us=None if t_ref != t_ref else round(t_ref, 2),
                 bench_floats=bench_floats)
     use = m == "1" or not (t_ref <= t_peer)
