@@ -8,7 +8,9 @@ field                  env var                     meaning
 backend                TDQ_BACKEND                 auto | hip | jet | autograd
 precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 MFMA operands,
                                                    fp32 accumulate / jets / master weights) | fp32
-newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision)
+newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision;
+                                                   "bf16w": bf16 activations with the weights' hi + lo
+                                                   parts, on the fused step - ops/fused_step.py)
 newton_schedule        TDQ_NEWTON_SCHEDULE         leading L-BFGS phases "prec:iters,..." before the
                                                    newton_precision phase (e.g. "bf16:7000")
 seed                   TDQ_SEED                    global seed applied at compile
@@ -102,7 +104,7 @@ class SolverConfig:
             raise ValueError(f"backend {self.backend!r}")
         if self.precision not in ("bf16x3", "bf16", "fp32"):
             raise ValueError(f"precision {self.precision!r}")
-        if self.newton_precision not in (None, "bf16x3", "bf16", "fp32"):
+        if self.newton_precision not in (None, "bf16x3", "bf16", "bf16w", "fp32"):
             raise ValueError(f"newton_precision {self.newton_precision!r}")
         parse_newton_schedule(self.newton_schedule)
         if self.log_every < 1:
@@ -126,7 +128,7 @@ def parse_newton_schedule(spec):
     out = []
     for part in str(spec).split(","):
         prec, _, n = part.strip().partition(":")
-        if prec not in ("bf16x3", "bf16", "fp32") or not n.strip().isdigit():
+        if prec not in ("bf16x3", "bf16", "bf16w", "fp32") or not n.strip().isdigit():
             raise ValueError(f"newton_schedule entry {part!r}: want precision:iterations")
         out.append((prec, int(n)))
     return out

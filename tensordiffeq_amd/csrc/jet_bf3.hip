@@ -557,7 +557,7 @@ int tdq_step_tail_bf3(float* work, float* grad, float* scratch, int N, int d_in,
 // objective writes [grad | loss] in place this way.
 int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
-                      float* total, int c_first, const float* gx, int rows, void* stream) {
+                      float* total, int c_first, const float* gx, int rows, int half_ovr, void* stream) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
@@ -577,7 +577,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
   tb.losses = losses;
   tb.dscal = dscal;
   tb.total = total;
-  const int half = (int)slab_half(lo != 0);
+  const int half = half_ovr >= 0 ? (half_ovr != 0) : (int)slab_half(lo != 0);  // (fused step bf16w: fp32 rows)
   const int nqb = (Pst / (half ? 8 : 4) + 255) / 256, nq2 = (Pst / 4 + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks - c_first), dim3(256), 0, st, work, part, nwg_b, Pst,
                      chunks, nqb, half, c_first, tb);

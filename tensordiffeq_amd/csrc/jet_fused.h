@@ -69,8 +69,12 @@ __host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int
 // tanh's own ~6e-8 absolute error near 0 is far below the bf16 rounding every activation takes
 // before the next GEMM.  The epilogue VALU work is as large as the layer's MFMA work at width 128
 // (4 streams: 1 MFMA cycle and ~20 VALU ops per feature x point).
+// Default OFF: the AC-SA reference schedule with the fused step lands at L2 2.83 / 2.99 / 3.07e-2
+// (seeds 0-2) with it and 2.41 / 2.29 / 1.86e-2 with the saved-activation kernels' tanh_jet_f, at
+// the same step time (0.1689 vs 0.1695 ms; profiles/r5acc_accuracy_ab.jsonl): 1 - 2r loses the
+// relative accuracy of small activations (6e-8 absolute near z = 0).
 #ifndef FZ_CHEAP_TANH
-#define FZ_CHEAP_TANH 1  // 0: the saved-activation kernels' tanh_jet_f (A/B builds)
+#define FZ_CHEAP_TANH 0  // 1: the cheap form above (A/B builds: TDQ_FUSED_STEP_DEFINES=-DFZ_CHEAP_TANH=1)
 #endif
 template <int S, int NSO>
 __device__ __forceinline__ void fz_tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
@@ -176,14 +180,15 @@ __device__ __forceinline__ f32x4 fz_bf4(bf16x4 v) {
 // acc[oo][s] = sum_kb A(o0 + oo, kb) B(kb, s) for the 16 points of column tile q: A from a weight
 // image in global memory (hi only, one k-block ahead), B from the LDS image `im` (S stream images of
 // FZ_PT rows; the SIMD's other wave covers the LDS latency).
-template <int WT, int S, int OPW>
+// WLO: the weights' bf16 lo parts too (a second MFMA per fragment; the activations stay bf16)
+template <int WT, int S, int OPW, bool WLO = false>
 __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __restrict__ wimg, int layer, int o0,
                                         const __bf16* im, int q, const FzLane& L, int l) {
   constexpr int KB = WT / 2, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS, NSTEP = WT * KB;
   const Tl Wi = tl_make(wimg + (size_t)(layer - 1) * NSTEP * 128, l);
-  bf16x8 a[2][OPW], dummy;
+  bf16x8 a[2][OPW], alo[2][OPW];
 #pragma unroll
-  for (int oo = 0; oo < OPW; ++oo) img_frag<false>(Wi, (o0 + oo) * KB, a[0][oo], dummy);
+  for (int oo = 0; oo < OPW; ++oo) img_frag<WLO>(Wi, (o0 + oo) * KB, a[0][oo], alo[0][oo]);
 #pragma unroll
   for (int oo = 0; oo < OPW; ++oo)
 #pragma unroll
@@ -192,7 +197,8 @@ __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __re
   for (int kb = 0; kb < KB; ++kb) {
     if (kb + 1 < KB) {
 #pragma unroll
-      for (int oo = 0; oo < OPW; ++oo) img_frag<false>(Wi, (o0 + oo) * KB + kb + 1, a[(kb + 1) & 1][oo], dummy);
+      for (int oo = 0; oo < OPW; ++oo)
+        img_frag<WLO>(Wi, (o0 + oo) * KB + kb + 1, a[(kb + 1) & 1][oo], alo[(kb + 1) & 1][oo]);
     }
     bf16x8 b[S];
 #pragma unroll
@@ -200,7 +206,10 @@ __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __re
 #pragma unroll
     for (int oo = 0; oo < OPW; ++oo)
 #pragma unroll
-      for (int s = 0; s < S; ++s) acc[oo][s] = mfma_bf(a[kb & 1][oo], b[s], acc[oo][s]);
+      for (int s = 0; s < S; ++s) {
+        acc[oo][s] = mfma_bf(a[kb & 1][oo], b[s], acc[oo][s]);
+        if constexpr (WLO) acc[oo][s] = mfma_bf(alo[kb & 1][oo], b[s], acc[oo][s]);
+      }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -284,7 +293,8 @@ struct FzNoLoss {
 // Eight waves (two per SIMD, so one wave's tanh-jet VALU work runs beside the other's MFMAs):
 // wave w computes column tile q = w >> 2 (16 points) of feature tiles 2 (w & 3).. (OPW of them) in
 // every GEMM / epilogue, and owns an NR x NC block of each hidden layer's dK tiles.
-template <int WT, int S, int NSO, int LM, int MODE, class LossF>
+// WLO (MODE 2, the L-BFGS objective "bf16w"): weight lo parts in every GEMM and fp32 slab rows
+template <int WT, int S, int NSO, int LM, int MODE, class LossF, bool WLO = false>
 __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   const float* __restrict__ X = P.X;
   const float* __restrict__ aux_g = P.aux;
@@ -393,7 +403,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     for (int ly = 1; ly <= LM; ++ly) {
       const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
       f32x4 acc[OPW][S];
-      fz_gemm<WT, S, OPW>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
+      fz_gemm<WT, S, OPW, WLO>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
       FZ_TS(1 + 2 * ly);
       f32x4 hq[OPW][S];  // MODE 0, top layer: the streams for the output dots
 #pragma unroll
@@ -544,7 +554,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
         __bf16* H = slot(ly - 1);
         const int tb = 10 + 5 * (LM - ly);
         f32x4 acc[OPW][S];
-        fz_gemm<WT, S, OPW>(acc, Kimg, ly, o0, Z, q, L, l);
+        fz_gemm<WT, S, OPW, WLO>(acc, Kimg, ly, o0, Z, q, L, l);
         FZ_TS(tb);
         // the tanh-jet adjoint (VALU) and dK_ly (MFMA: every wave reads all of H and Z) in one
         // scheduling region; zb_{ly-1} goes in place of h_{ly-1} after the barrier
@@ -623,38 +633,51 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   TDQ_TS(62);
 
   if constexpr (MODE >= 1) {
-    // ---- this workgroup's gradient-slab row (bf16) ------------------------------------------
-    __bf16* gs = reinterpret_cast<__bf16*>(P.slab) + (size_t)(P.srow + gi) * Pst;
+    // ---- this workgroup's gradient-slab row (bf16; WLO: fp32) --------------------------------
+    using ST = typename SlabType<!WLO>::T;
+    ST* gs = reinterpret_cast<ST*>(P.slab) + (size_t)(P.srow + gi) * Pst;
 #pragma unroll
     for (int ly = 1; ly <= LM; ++ly) {
-      const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
-      const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * 2;
+      const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * (int)sizeof(ST);
+      if constexpr (WLO) {
+        const Tl Gt = tl_make(reinterpret_cast<const float*>(gs + off_layer(d, ly)), 0);
 #pragma unroll
-      for (int r = 0; r < NR; ++r)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
+          for (int c = 0; c < NC; ++c)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)dk[ly - 1][r][c][e]), Gt.r,
-                                                  voff, ((16 * r + e) * W + 16 * c) * 2, 0);
+            for (int e = 0; e < 4; ++e)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dk[ly - 1][r][c][e]), Gt.r, voff,
+                                                    ((16 * r + e) * W + 16 * c) * 4, 0);
+      } else {
+        const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)dk[ly - 1][r][c][e]),
+                                                    Gt.r, voff, ((16 * r + e) * W + 16 * c) * 2, 0);
+      }
     }
     __syncthreads();  // LDS partials complete
     const float* pA = part;
     const float* pB = part + pq;
     for (int f = tid; f < W; f += 64 * FZ_WAVES) {
-      gs[d.d_in * W + f] = (__bf16)(pA[f] + pB[f]);  // b0
+      gs[d.d_in * W + f] = (ST)(pA[f] + pB[f]);  // b0
       for (int ly = 1; ly <= LM; ++ly)
-        gs[off_layer(d, ly) + W * W + f] = (__bf16)(pA[ly * W + f] + pB[ly * W + f]);
+        gs[off_layer(d, ly) + W * W + f] = (ST)(pA[ly * W + f] + pB[ly * W + f]);
       for (int j = 0; j < d.d_in; ++j) {
         const int k = (LM + 1) * W + j * W + f;
-        gs[j * W + f] = (__bf16)(pA[k] + pB[k]);
+        gs[j * W + f] = (ST)(pA[k] + pB[k]);
       }
       for (int qo = 0; qo < d.d_out; ++qo) {
         const int k = (LM + 1 + d.d_in) * W + f * 4 + qo;
-        gs[off_layer(d, LM + 1) + f * d.d_out + qo] = (__bf16)(pA[k] + pB[k]);
+        gs[off_layer(d, LM + 1) + f * d.d_out + qo] = (ST)(pA[k] + pB[k]);
       }
     }
-    if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (__bf16)accBo[tid];
+    if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (ST)accBo[tid];
   }
   if constexpr (MODE == 2) {  // loss partials: the point-threads (wave 0, lanes < FZ_PT) summed
     if (w == 0) {

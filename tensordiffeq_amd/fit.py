@@ -733,9 +733,10 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
 class LossGradEngine:
     """``(f, g_theta)`` at a flat parameter vector (lambdas frozen, B15); DP all-reduced."""
 
-    def __init__(self, solver, program, lambdas):
+    def __init__(self, solver, program, lambdas, weight_lo=False):
         self.s = solver
         self.program = program
+        self.weight_lo = bool(weight_lo)   # newton_precision "bf16w" (ops/fused_step.py wlo)
         self.flat = solver.u_model.flat
         self.lambdas = lambdas
         self.dist = solver.dist_ctx
@@ -773,7 +774,11 @@ class LossGradEngine:
                 hi = prog.hi_op
                 gx = hi.grad if hi is not None else None
                 from .ops import fused_step
-                fs = fused_step.for_program(prog)
+                fs = fused_step.for_program(prog, wlo=self.weight_lo)
+                if fs is None and self.weight_lo:
+                    from .models.loss import _warn_once
+                    _warn_once(f"newton_precision='bf16w' needs the fused step ({prog.fused_step_w_reason}); "
+                               "the L-BFGS objective runs in plain bf16")
                 if fs is not None:
                     J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
                                                      rows=fop.fl.n_streams)

@@ -380,15 +380,22 @@ class CollocationSolverND:
         return lambda w: eng(torch.as_tensor(w, dtype=torch.float32, device=self.device))
 
     def _get_lbfgs_engine(self, precision=None):
-        if precision is not None and precision != (self.newton_precision or self.precision):
-            key = ("lbfgs_engine", precision)
+        """The L-BFGS objective's engine at ``precision`` (default ``newton_precision``).  "bf16w"
+        is the bf16 program evaluated by the fused step with the weights' lo parts
+        (ops/fused_step.py ``wlo``)."""
+        default = self.newton_precision or self.precision
+        prec = precision or default
+        wlo = prec == "bf16w"
+        kprec = "bf16" if wlo else prec
+        if prec != default:
+            key = ("lbfgs_engine", prec)
             eng = self._programs.get(key)
-            prog = self.program(precision=precision)
+            prog = self.program(precision=kprec)
             if eng is None or eng.program is not prog:
-                eng = self._programs[key] = LossGradEngine(self, prog, self.lambdas)
+                eng = self._programs[key] = LossGradEngine(self, prog, self.lambdas, weight_lo=wlo)
             return eng
         if self._lbfgs_engine is None:
-            self._lbfgs_engine = LossGradEngine(self, self.program(precision=self.newton_precision), self.lambdas)
+            self._lbfgs_engine = LossGradEngine(self, self.program(precision=kprec), self.lambdas, weight_lo=wlo)
         return self._lbfgs_engine
 
     def _get_engine(self, batch=None, n_hint=0):

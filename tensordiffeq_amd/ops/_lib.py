@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 _lock = threading.Lock()
 _lib = None
@@ -51,7 +51,7 @@ def _declare(lib):
                               + [P, I, P, I, P, I, P, I, P]),
         "tdq_bf3_slab_geometry": (I, [I, I, P, I, I, I, I, P]),
         "tdq_slab_prereduce_bf3": (I, [P, I, I, P, I, I, I, I, I, I, P]),
-        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, I, P, I, P]),
+        "tdq_dp_tail_a_bf3": (I, [P, P, I, I, P, I, I, I, I, P, I, I, I, P, P, P, I, P, I, I, P]),
         "tdq_dp_tail_b_bf3": (I, [P, I, I, P, I, I, I, P, I, P, P, P]),
         "tdq_jet_bf3_scratch_floats": (L, [I, I, P, I, I, I]),
         "tdq_jet_bf3_slab_floats": (L, [I, I, P, I, I]),

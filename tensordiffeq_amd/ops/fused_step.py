@@ -40,7 +40,9 @@ RTC_OPTS = "-O3 -std=c++17 -fno-slp-vectorize -munsafe-fp-atomics"
 
 def _opts():
     """hipRTC options; ``TDQ_FUSED_STEP_TIMING=1`` adds the phase stamps (tools/fused_step_timing.py)."""
-    return RTC_OPTS + (" -DTDQ_PHASE_TIMING" if os.environ.get("TDQ_FUSED_STEP_TIMING") == "1" else "")
+    extra = os.environ.get("TDQ_FUSED_STEP_DEFINES", "")   # A/B builds, e.g. "-DFZ_CHEAP_TANH=0"
+    return RTC_OPTS + (" -DTDQ_PHASE_TIMING" if os.environ.get("TDQ_FUSED_STEP_TIMING") == "1" else "") + \
+        (" " + extra if extra else "")
 
 
 def enabled():
@@ -132,12 +134,12 @@ def gen_loss(groups, n_terms, nacc, S):
     return "\n".join(L)
 
 
-def kernel_source(S, nso, LM, lds, gen):
+def kernel_source(S, nso, LM, lds, gen, wlo=False):
     return (header_source() + "\n" + gen + "\n"
             'extern "C" __global__ void __launch_bounds__(64 * FZ_WAVES) '
             "__attribute__((amdgpu_waves_per_eu(2, 2))) tdq_fused_step(FzParams P) {\n"
             f"  __shared__ __attribute__((aligned(16))) char lds[{lds}];\n"
-            f"  fz_body<8, {S}, {nso}, {LM}, 2, GenLoss>(P, lds);\n"
+            f"  fz_body<8, {S}, {nso}, {LM}, 2, GenLoss, {'true' if wlo else 'false'}>(P, lds);\n"
             "}\n")
 
 
@@ -218,9 +220,9 @@ class FusedStepOp:
     own segment, the boundary chain (high-order streams, saved-activation forward, loss blocks,
     backward) on a side stream beside it."""
 
-    def __init__(self, prog, fop):
+    def __init__(self, prog, fop, wlo=False):
         lib = _lib.load(required=True)
-        self.prog, self.fop = prog, fop
+        self.prog, self.fop, self.wlo = prog, fop, bool(wlo)
         cfg = self.cfg = hip_config(prog.net, prog.plan, prog.precision)
         fl = fop.fl
         S = cfg["S"]
@@ -264,7 +266,7 @@ class FusedStepOp:
             pts_b = jet_hip.slab_geometry(cfg, N)[0]
             self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
             self.srow = -(-self.p_bc // pts_b)
-        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S))
+        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), wlo=self.wlo)
         self.module, self.func = _compile(self.source)
         ntiles = -(-(self.N - self.p_lo) // 32)
         cus = max(1, lib.tdq_device_cus())
@@ -339,25 +341,36 @@ class FusedStepOp:
                    "tdq_rtc_set_global_ptr")
 
     def tail_kw(self):
-        """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows."""
-        return {"rows": self.rows, "lpart": self.fop.partials if self.mixed else self.lpart,
-                "n_lblocks": self.n_lblocks}
+        """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows (the
+        weight-lo objective: ``dp_tail_a`` only, its slab rows are fp32)."""
+        kw = {"rows": self.rows, "lpart": self.fop.partials if self.mixed else self.lpart,
+              "n_lblocks": self.n_lblocks}
+        if self.wlo:
+            kw["half"] = False
+        return kw
 
 
-def for_program(prog):
-    """The program's :class:`FusedStepOp` (built once), or ``None`` (reason in
-    ``prog.fused_step_reason``)."""
-    if getattr(prog, "_fused_step_built", False):
-        return prog._fused_step
-    prog._fused_step_built = True
-    prog._fused_step = None
+def for_program(prog, wlo=False):
+    """The program's :class:`FusedStepOp` (built once per ``wlo``), or ``None`` (reason in
+    ``prog.fused_step_reason``).  ``wlo``: the L-BFGS objective "bf16w" - bf16 activations, the
+    weights' bf16 hi + lo parts in every GEMM (two MFMAs), fp32 gradient slabs."""
+    key = "_fused_step_w" if wlo else "_fused_step"
+    if getattr(prog, key + "_built", False):
+        return getattr(prog, key)
+    setattr(prog, key + "_built", True)
+    setattr(prog, key, None)
     fop = getattr(prog, "fused_op", None)
     why = ineligible(prog, fop)
+    if why is None and wlo and _mixed(prog):
+        why = "bf16w: mixed programs keep the boundary chain in bf16"
     if why is None:
         try:
-            prog._fused_step = FusedStepOp(prog, fop)
+            setattr(prog, key, FusedStepOp(prog, fop, wlo=wlo))
         except Exception as e:  # noqa: BLE001 - the separate launches serve every program
             why = f"{type(e).__name__}: {e}"
             warnings.warn(f"fused training step unavailable, using separate launches: {why}")
-    prog.fused_step_reason = why
-    return prog._fused_step
+    if wlo:
+        prog.fused_step_w_reason = why
+    else:
+        prog.fused_step_reason = why
+    return getattr(prog, key)

@@ -292,7 +292,7 @@ class JetMLPFunction(torch.autograd.Function):
 
 
 def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0, gextra=None, rows=0, lpart=None,
-              n_lblocks=None):
+              n_lblocks=None, half=None):
     """Data-parallel step before the all-reduce: slab pass 1 + loss reduction (one launch), then
     slab pass 2 into ``grad`` (csrc/jet_bf3.hip ``tdq_dp_tail_a_bf3``).  ``total`` (a 1-element
     view): also write the summed loss there; ``losses`` (an ``n_terms`` view, default
@@ -304,7 +304,8 @@ def dp_tail_a(saved, work, grad, fop, total=None, losses=None, c_first=0, gextra
                                cfg["n_hidden"], S, *_lo_args(cfg), _lib.ptr(fop.partials if lpart is None else lpart),
                                fop.n_blocks if n_lblocks is None else int(n_lblocks), fop.n_terms,
                                fop.n_scal, _lib.ptr(losses), _lib.ptr(fop.dscal), _lib.ptr(total), int(c_first),
-                               _lib.ptr(gextra), int(rows), _lib.stream_ptr(X.device))
+                               _lib.ptr(gextra), int(rows), -1 if half is None else int(bool(half)),
+                               _lib.stream_ptr(X.device))
     _lib.check(rc, "tdq_dp_tail_a_bf3")
 
 

@@ -84,11 +84,10 @@ def test_fused_matches_fp64(sizes, reqs, N, fused_on):
 
 @pytest.mark.parametrize("sizes,reqs,N", [CASES[0], CASES[1], CASES[3]])
 def test_fused_matches_saved_activation_kernels(sizes, reqs, N):
-    """Same bf16 network, two kernel designs.  With the same tanh (an FZ_CHEAP_TANH=0 build) they agree
-    to 1.5e-6 in J (gpurun_out/r5tanh); the persistent kernels' cheaper tanh (~1e-7 absolute) flips
-    some bf16 roundings of the activations, after which the two carry independent bf16 errors:
-    ~1e-2 against each other in the cancelling derivative streams, while each stays at the same
-    distance from the fp64 jet (test_fused_matches_fp64).  Bounds: the bf16 level."""
+    """Same bf16 network, two kernel designs with the same tanh jet (FZ_CHEAP_TANH=0, the default
+    since the cheaper form cost accuracy: profiles/r5acc_accuracy_ab.jsonl): J agreed to 1.5e-6
+    (gpurun_out/r5tanh); the gradients differ by summation order (tile-resident dK vs per-workgroup
+    slabs) and the bf16 slab rounding of different partial sums."""
     from tensordiffeq_amd.ops import jet_hip
     net, X, plan = _setup(sizes, reqs, N, seed=2)
     G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
@@ -104,8 +103,8 @@ def test_fused_matches_saved_activation_kernels(sizes, reqs, N):
     gerr = ((g1 - g0).norm() / g0.norm()).item()
     per_stream = ((J1 - J0).abs() / scale).amax(dim=(1, 2)).tolist()
     print(f"FUSED_VS_SAVED {sizes} N={N} J {jerr:.3e} (streams {['%.1e' % v for v in per_stream]}) grad {gerr:.3e}")
-    assert jerr < 3e-2, jerr
-    assert gerr < 1e-2, gerr
+    assert jerr < 1e-4, jerr
+    assert gerr < 5e-3, gerr
 
 
 def test_fused_deterministic(fused_on):

@@ -156,3 +156,29 @@ def test_fused_step_deterministic(monkeypatch):
     a = eng.evaluate_fg().clone()
     b = eng.evaluate_fg().clone()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_fused_step_weight_lo_gradient_vs_fp64():
+    """newton_precision "bf16w" (the weights' hi + lo parts in every GEMM, fp32 slab rows): the
+    L-BFGS objective's gradient is closer to the fp64 jet than the bf16 step's."""
+    import bench
+    from tensordiffeq_amd.fit import LossGradEngine
+    from tensordiffeq_amd.ops import fused_step
+    dev = torch.device("cuda", 0)
+    m = bench.build_problem(20000, 1, "hip", dev, False, "bf16")
+    prog = m.program()
+    ref = bench.build_problem(20000, 1, "jet", dev, False, "bf16")
+    p64 = m.u_model.flat.detach().double().requires_grad_(True)
+    lams = [lam.detach().double() for lam in m.lambdas]
+    tot, _ = ref.program().evaluate(p64, lams)
+    g64, = torch.autograd.grad(tot, [p64])
+    errs = {}
+    for wlo in (False, True):
+        assert fused_step.for_program(prog, wlo=wlo) is not None
+        fg = LossGradEngine(m, prog, m.lambdas, weight_lo=wlo).evaluate_fg().double()
+        torch.cuda.synchronize()
+        errs[wlo] = (((fg[:-1] - g64).norm() / g64.norm()).item(), abs(fg[-1].item() - tot.item()) / tot.item())
+    print(f"FUSED_STEP_WLO grad/loss rel err vs fp64: bf16 {errs[False]}, bf16w {errs[True]}")
+    assert errs[True][0] < 3e-2 and errs[True][1] < 2e-2
+    assert errs[True][0] <= errs[False][0] * 1.05

@@ -35,7 +35,7 @@ int tdq_jet_bwd_bf3(const float* X, const float* P, const float* dJ, const float
                     int d_in, const int* widths, int d_out, int n_hidden, int S, const int* spec, int lo, void* stream);
 int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widths, int d_out, int n_hidden, int S, int lo,
                       const float* lpart, int n_lblocks, int n_terms, int n_scal, float* losses, float* dscal,
-                      float* total, int c_first, const float* gx, int rows, void* stream);
+                      float* total, int c_first, const float* gx, int rows, int half_ovr, void* stream);
 int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
                            float* x_prev, double* st, double* SY, double* YY, double* coef, double* part, double* part2,
                            float* fhist, int* ticket, int p, int m, int max_iter, int nchunks, int nblk, int fhist_len,
@@ -95,8 +95,8 @@ int main() {
   CHECK(tdq_jet_fwd_bf3(f, f, f, f, 100, 2, w128, 1, 4, 3, spec_bad, 0, nullptr) != 0);  // bad spec
   CHECK(tdq_jet_fwd_bf3(f, f, f, f, 0, 2, w128, 1, 4, 4, spec_ok, 0, nullptr) == 0);     // N = 0: no-op
   CHECK(tdq_jet_bwd_bf3(f, f, f, f, f, f, 100, 2, w128, 1, 0, 4, spec_ok, 1, nullptr) != 0);  // no hidden layer
-  CHECK(tdq_dp_tail_a_bf3(f, f, 100, 2, w128, 1, 4, 9, 0, f, 1, 1, 0, f, f, f, 0, nullptr, 0, nullptr) != 0);
-  CHECK(tdq_dp_tail_a_bf3(f, f, 0, 2, w128, 1, 4, 4, 0, f, 1, 1, 0, f, f, f, 0, nullptr, 0, nullptr) != 0);
+  CHECK(tdq_dp_tail_a_bf3(f, f, 100, 2, w128, 1, 4, 9, 0, f, 1, 1, 0, f, f, f, 0, nullptr, 0, -1, nullptr) != 0);
+  CHECK(tdq_dp_tail_a_bf3(f, f, 0, 2, w128, 1, 4, 4, 0, f, 1, 1, 0, f, f, f, 0, nullptr, 0, -1, nullptr) != 0);
   double* dd = reinterpret_cast<double*>(f);
   int tk[2] = {0, 0};
   CHECK(tdq_lbfgs_update_fused(f, f, f, f, f, f, f, f, dd, dd, dd, dd, dd, dd, f, tk, 100, 65, 10, 1, 1, 0, 12.5,
