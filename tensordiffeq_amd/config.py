@@ -10,7 +10,10 @@ precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf
                                                    fp32 accumulate / jets / master weights) | fp32
 newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision;
                                                    "bf16w": bf16 activations with the weights' hi + lo
-                                                   parts, on the fused step - ops/fused_step.py)
+                                                   parts, on the fused step - ops/fused_step.py;
+                                                   gradient 4e-4 vs fp64 (bf16 3e-3, bf16x3 8e-6), but
+                                                   the fixed-step L-BFGS diverges on AC-SA with it:
+                                                   profiles/r5wlo2_bf16w_lbfgs.json - experimental)
 newton_schedule        TDQ_NEWTON_SCHEDULE         leading L-BFGS phases "prec:iters,..." before the
                                                    newton_precision phase (e.g. "bf16:7000")
 seed                   TDQ_SEED                    global seed applied at compile

@@ -69,12 +69,18 @@ __host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int
 // tanh's own ~6e-8 absolute error near 0 is far below the bf16 rounding every activation takes
 // before the next GEMM.  The epilogue VALU work is as large as the layer's MFMA work at width 128
 // (4 streams: 1 MFMA cycle and ~20 VALU ops per feature x point).
-// Default OFF: the AC-SA reference schedule with the fused step lands at L2 2.83 / 2.99 / 3.07e-2
-// (seeds 0-2) with it and 2.41 / 2.29 / 1.86e-2 with the saved-activation kernels' tanh_jet_f, at
-// the same step time (0.1689 vs 0.1695 ms; profiles/r5acc_accuracy_ab.jsonl): 1 - 2r loses the
-// relative accuracy of small activations (6e-8 absolute near z = 0).
+// Hidden layers: OFF by default - the AC-SA reference schedule with the fused step landed at L2
+// 2.83 / 2.99 / 3.07e-2 (seeds 0-2) with it and 2.41 / 2.29 / 1.86e-2 with the saved-activation
+// kernels' tanh_jet_f, at the same step time (profiles/r5acc_accuracy_ab.jsonl).  Layer 0 (fz_h0):
+// the cheap form stays - seeds 0-5 with it 2.41 / 2.29 / 1.86 / 2.03 / 2.59 / 2.44e-2 (median
+// 2.35e-2, the separate-launch step's 6-seed median), with tanh_s1 there 1.45 / 2.63 / 3.17 / 3.02 /
+// 3.43 / 2.57e-2 (median 2.83e-2) - profiles/r5acc2_l2_six_seeds.jsonl.  (1 - 2r has 6e-8 absolute
+// error near z = 0.)  A/B builds: TDQ_FUSED_STEP_DEFINES="-DFZ_CHEAP_TANH=1" / "-DFZ_CHEAP_H0=0".
 #ifndef FZ_CHEAP_TANH
-#define FZ_CHEAP_TANH 0  // 1: the cheap form above (A/B builds: TDQ_FUSED_STEP_DEFINES=-DFZ_CHEAP_TANH=1)
+#define FZ_CHEAP_TANH 0
+#endif
+#ifndef FZ_CHEAP_H0
+#define FZ_CHEAP_H0 1
 #endif
 template <int S, int NSO>
 __device__ __forceinline__ void fz_tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
@@ -126,10 +132,15 @@ __device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const
   for (int s = SO; s < S; ++s) kp[s] = sel_first<S, S1>(ka, sp.ia[s], sp.selA[s]) * sel_first<S, S1>(ka, sp.ib[s], sp.selB[s]);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const float e = __builtin_amdgcn_exp2f(fminf(z[c], 15.f) * 2.8853900817779268f);
-    const float r = __builtin_amdgcn_rcpf(1.f + e);
-    const float hv = fmaf(-2.f, r, 1.f);
-    const float s1 = (4.f * e) * (r * r);
+    float hv, s1;
+    if constexpr (FZ_CHEAP_H0) {
+      const float e = __builtin_amdgcn_exp2f(fminf(z[c], 15.f) * 2.8853900817779268f);
+      const float r = __builtin_amdgcn_rcpf(1.f + e);
+      hv = fmaf(-2.f, r, 1.f);
+      s1 = (4.f * e) * (r * r);
+    } else {
+      tanh_s1(z[c], hv, s1);   // the saved-activation kernels' tanh (layer 0 of every tile)
+    }
     const float s2 = -2.f * hv * s1;
     h[0][c] = hv;
 #pragma unroll
@@ -638,18 +649,16 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     ST* gs = reinterpret_cast<ST*>(P.slab) + (size_t)(P.srow + gi) * Pst;
 #pragma unroll
     for (int ly = 1; ly <= LM; ++ly) {
-      const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * (int)sizeof(ST);
       if constexpr (WLO) {
-        const Tl Gt = tl_make(reinterpret_cast<const float*>(gs + off_layer(d, ly)), 0);
+        float* row = reinterpret_cast<float*>(gs) + off_layer(d, ly) + (16 * r0 + 4 * g) * W + 16 * c0 + p;
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
           for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dk[ly - 1][r][c][e]), Gt.r, voff,
-                                                    ((16 * r + e) * W + 16 * c) * 4, 0);
+            for (int e = 0; e < 4; ++e) row[(16 * r + e) * W + 16 * c] = dk[ly - 1][r][c][e];
       } else {
+        const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * 2;
         const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
 #pragma unroll
         for (int r = 0; r < NR; ++r)

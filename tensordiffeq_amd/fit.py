@@ -352,14 +352,23 @@ class AdamEngine:
         return loss
 
     def _eager_step(self):
-        if not self.dist.is_distributed and self._tail_eligible():
-            return self._tail_step(in_graph=False)
+        if self._tail_eligible():
+            if not self.dist.is_distributed:
+                return self._tail_step(in_graph=False)
+            # DP: the captured step's own sequence, eagerly (same kernels, so the warm-up step and
+            # the replays share one numerics - the fused step's bf16 kernels)
+            self._dp_half_a_inplace(pack=True)
+            self.dist.all_reduce_(self._bucket_buf)
+            self._dp_half_b(True)
+            return self.static_loss
         loss, grads, terms = self._phase_a(for_step=True)
         loss, grads, terms = self._reduce(loss, grads, terms)
         return self._phase_b(loss, grads, terms)
 
     # ---------------------------------------------------------------- graphs -------------
     def _capture(self):
+        if self._tail_eligible():
+            self._fused_step()   # built (hipRTC compile + module load) outside any capture
         stream = torch.cuda.Stream(device=self.device)
         stream.wait_stream(torch.cuda.current_stream(self.device))
         split = self.dist.is_distributed
@@ -415,7 +424,7 @@ class AdamEngine:
         self._grads_static = grads
         self._red_idx = red_idx
 
-    def _dp_half_a_inplace(self):
+    def _dp_half_a_inplace(self, pack=False):
         """Fused-tail DP step up to the collective with the kernels writing straight into the
         bucket ``[grad theta | other reduced grads | loss | terms]``: slab pass 2 lands in the
         theta slice, the loss reduction in the scalar slice, so only the (small) other reduced
@@ -426,7 +435,7 @@ class AdamEngine:
         # persistent step buffers (as in _tail_step): the 1-step and the K-step graph read the
         # weight images that the previous step's dp_tail_b wrote into this one scratch
         J, saved, work, _ = self._step_buffers()
-        pre, kw = self._run_points(J, saved, work, pack=False)
+        pre, kw = self._run_points(J, saved, work, pack=pack)
         n_p = self.flat.numel()
         red_idx = self.red_idx
         if not red_idx or red_idx[0] != 0:

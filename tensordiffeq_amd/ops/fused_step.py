@@ -357,6 +357,12 @@ def for_program(prog, wlo=False):
     key = "_fused_step_w" if wlo else "_fused_step"
     if getattr(prog, key + "_built", False):
         return getattr(prog, key)
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        # module loads cannot run inside a capture: the engines build the op before capturing
+        # (fit.AdamEngine._capture, the L-BFGS drivers' first eager evaluation) - never cache a
+        # "not available" decided here
+        warnings.warn("fused training step first requested inside a graph capture; using separate launches")
+        return None
     setattr(prog, key + "_built", True)
     setattr(prog, key, None)
     fop = getattr(prog, "fused_op", None)

@@ -161,6 +161,7 @@ def test_forced_dp_rccl_point_ranges(monkeypatch):
     with single launches."""
     precision, n_f = "bf16", 20000
     monkeypatch.setenv("TDQ_SPLIT", "0")
+    monkeypatch.setenv("TDQ_FUSED_STEP", "0")   # point ranges serve the separate-launch step (inherited by the worker)
     ref = _build(False, 1, precision, n_f)
     ref.fit(tf_iter=8)
     ref_hist = [h["Total Loss"] for h in ref.losses]

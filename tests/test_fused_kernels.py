@@ -84,10 +84,12 @@ def test_fused_matches_fp64(sizes, reqs, N, fused_on):
 
 @pytest.mark.parametrize("sizes,reqs,N", [CASES[0], CASES[1], CASES[3]])
 def test_fused_matches_saved_activation_kernels(sizes, reqs, N):
-    """Same bf16 network, two kernel designs with the same tanh jet (FZ_CHEAP_TANH=0, the default
-    since the cheaper form cost accuracy: profiles/r5acc_accuracy_ab.jsonl): J agreed to 1.5e-6
-    (gpurun_out/r5tanh); the gradients differ by summation order (tile-resident dK vs per-workgroup
-    slabs) and the bf16 slab rounding of different partial sums."""
+    """Same bf16 network, two kernel designs.  The hidden layers use the same tanh jet; layer 0 the
+    persistent kernels' cheaper form (1 - 2r, ~6e-8 absolute; kept because the reference schedule's
+    L2 measured better with it, profiles/r5acc2_l2_six_seeds.jsonl), which flips some bf16 roundings
+    of the first activations: J ~1e-2 apart in the cancelling u_x stream (2.8e-3 with tanh_s1 there,
+    gpurun_out/r5suite), each kernel at the bf16 distance from the fp64 jet
+    (test_fused_matches_fp64).  Bounds: the bf16 level."""
     from tensordiffeq_amd.ops import jet_hip
     net, X, plan = _setup(sizes, reqs, N, seed=2)
     G = torch.randn(plan.S, N, sizes[-1], device="cuda", dtype=torch.float64)
@@ -103,7 +105,7 @@ def test_fused_matches_saved_activation_kernels(sizes, reqs, N):
     gerr = ((g1 - g0).norm() / g0.norm()).item()
     per_stream = ((J1 - J0).abs() / scale).amax(dim=(1, 2)).tolist()
     print(f"FUSED_VS_SAVED {sizes} N={N} J {jerr:.3e} (streams {['%.1e' % v for v in per_stream]}) grad {gerr:.3e}")
-    assert jerr < 1e-4, jerr
+    assert jerr < 3e-2, jerr
     assert gerr < 5e-3, gerr
 
 

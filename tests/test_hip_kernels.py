@@ -471,6 +471,8 @@ def test_fused_step_tail_matches_unfused(prec, problem, sizes, monkeypatch):
     Geometries: every width class incl. padded widths, one hidden layer, a wide plan."""
     build = _ac_sa_model if problem == "ac" else _poisson_model
 
+    monkeypatch.setenv("TDQ_FUSED_STEP", "0")   # the tail's mechanics on the same kernels both ways
+
     def run(fused_tail):
         monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
         m = build(prec, sizes=sizes)
@@ -565,6 +567,8 @@ def test_fused_lbfgs_objective_matches_unfused(prec, problem, sizes, monkeypatch
     device L-BFGS trajectory, bit for bit, as the loss-reduce / total / slab / concatenate path."""
     build = _ac_sa_model if problem == "ac" else _poisson_model
 
+    monkeypatch.setenv("TDQ_FUSED_STEP", "0")   # same kernels both ways (the fused step: test_fused_step.py)
+
     def run(fused_tail):
         monkeypatch.setenv("TDQ_FUSED_TAIL", "1" if fused_tail else "0")
         m = build(prec, sizes=sizes)
@@ -609,6 +613,7 @@ def test_point_ranges_match_single_launch(prec, cuts, monkeypatch):
     trajectory, the L-BFGS objective and the L-BFGS trajectory are bitwise those of single
     launches."""
     res = []
+    monkeypatch.setenv("TDQ_FUSED_STEP", "0")   # point ranges serve the separate-launch step
     for split in ("0", cuts):
         monkeypatch.setenv("TDQ_SPLIT", split)
         m = _ac_sa_model(prec, n_f=20000)
