@@ -189,6 +189,11 @@ def ineligible(prog, fop):
     for gr in fl.groups:
         if any(s >= cfg["S"] for (_, s) in gr.program.stream_regs) and not _mixed(prog):
             return "a loss group reads streams outside the jet plan"
+    if _mixed(prog) and os.environ.get("TDQ_FUSED_STEP_MIXED", "0") != "1":
+        # AC-baseline (order-4 periodic streams): the residual fused beside the high-order boundary
+        # chain measured 0.253 ms/step vs 0.211-0.217 on the point-range path (gpurun_out/r5f1):
+        # the jet_hi chain no longer overlaps a second range's backward
+        return "high-order boundary streams (TDQ_FUSED_STEP_MIXED=1 runs the residual fused)"
     if _mixed(prog):
         # high-order boundary points (jet_hi.hip streams): only the residual group runs fused
         last = len(prog.segments) - 1

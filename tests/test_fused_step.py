@@ -100,7 +100,8 @@ def test_fused_step_matches_separate_launches(problem, n_f, monkeypatch):
     """One evaluation: every loss term, the theta gradient and the SA-weight gradients of the fused
     step vs the separate launches (saved-activation kernels + specialized loss kernel).  AC-SA runs
     every group in the fused launch (IC with SA weights, the periodic pairs, the residual);
-    AC-baseline (order-4 periodic streams) its residual only."""
+    AC-baseline (order-4 periodic streams, opt-in) its residual only."""
+    monkeypatch.setenv("TDQ_FUSED_STEP_MIXED", "1")
     from tensordiffeq_amd.fit import LossGradEngine
     from tensordiffeq_amd.ops import fused_step
     out = {}
