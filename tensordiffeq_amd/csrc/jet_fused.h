@@ -29,11 +29,14 @@
 #pragma once
 #include "jet_bf3.h"
 
-// Phase stamps (-DTDQ_PHASE_TIMING build, tools/fused_timing.py): the first tile's phases and the
-// whole tile loop, per wave
+// Phase stamps (-DTDQ_PHASE_TIMING build, tools/fused_timing.py): the phases of tile t0 + FZ_TS_TILE
+// of every workgroup (0: the first, cold tile; 1: a steady-state one) and the whole tile loop, per wave
+#ifndef FZ_TS_TILE
+#define FZ_TS_TILE 0
+#endif
 #define FZ_TS(k) \
   do {                \
-    if (t == t0) TDQ_TS(k); \
+    if (t == t0 + FZ_TS_TILE) TDQ_TS(k); \
   } while (0)
 
 #define FZ_PT 32  // points per tile (two 16-point MFMA column tiles; waves 0-3 / 4-7)
@@ -284,15 +287,18 @@ struct FzParams {
 };
 
 // MODE 0 / 1 builds: no loss code.  The MODE 2 interface (ops/fused_step.py generates it):
-//   eval<S, OQ>(jv, xs, t, n, N, ptrs, ubs, acc) on the tile's point-thread t (point n of the
+//   prefetch(ptrs, n, N, pre): the per-point inputs of point n's loss (SA weights, data values,
+//   scalars) into registers, one tile ahead (their global latency hides behind the current tile);
+//   eval<S, OQ>(jv, xs, t, n, N, ptrs, pre, ubs, acc) on the tile's point-thread t (point n of the
 //   fused point set): J of the tile's point k, stream s at jv[(s * FZ_PT + k) * OQ], coordinates
 //   at xs[k * TDQ_MAXD + j]; writes dJ of the points it owns to ubs[(s * FZ_PT + k) * 4] (zero for
 //   points outside every loss group) and adds loss / scalar-gradient sums to acc
 struct FzNoLoss {
-  static constexpr int NACC = 1;
+  static constexpr int NACC = 1, NPRE = 1;
+  __device__ static void prefetch(const FzLossPtrs&, int, int, float (&pre)[NPRE]) { pre[0] = 0.f; }
   template <int S, int OQ>
-  __device__ static void eval(const float*, const float*, int t, int, int, const FzLossPtrs&, float* ubs,
-                              float (&)[1]) {
+  __device__ static void eval(const float*, const float*, int t, int, int, const FzLossPtrs&, const float (&)[NPRE],
+                              float* ubs, float (&)[1]) {
 #pragma unroll
     for (int s = 0; s < S; ++s) ubs[(s * FZ_PT + t) * 4] = 0.f;
   }
@@ -373,8 +379,12 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   // <= 512), fetched one tile ahead so the global latency hides behind the current tile
   static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES && S * FZ_PT * 4 <= 64 * FZ_WAVES, "one element per thread");
   float xpre = 0.f, upre = 0.f;
+  float lnext[LossF::NPRE], lpre[LossF::NPRE];  // MODE 2: the loss inputs of this thread's point
+#pragma unroll
+  for (int k = 0; k < LossF::NPRE; ++k) lnext[k] = lpre[k] = 0.f;
   auto fetch = [&](int tt) {
     const int pb = P.p_lo + tt * FZ_PT;
+    if (MODE == 2 && tid < FZ_PT) LossF::prefetch(*P.lptrs, pb + tid, N, lnext);
     if (tid < FZ_PT * TDQ_MAXD) {
       const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
       const int n = min(pb + pt, N - 1);
@@ -394,6 +404,10 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
     if (tid < FZ_PT * TDQ_MAXD) xs[tid] = xpre;
     if (MODE == 1 && tid < S * FZ_PT * 4) ubs[tid] = upre;
+    if constexpr (MODE == 2) {
+#pragma unroll
+      for (int k = 0; k < LossF::NPRE; ++k) lpre[k] = lnext[k];
+    }
     if (t + 1 < t1) fetch(t + 1);
     __syncthreads();
     FZ_TS(1);
@@ -520,7 +534,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
         // ---- the per-point loss (generated code: every loss group of the program - residual, SA
         // weighting, boundary terms with the two points of a periodic pair side by side - and its
         // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
-        if (tid < FZ_PT) LossF::template eval<S, OQ>(outp, xs, tid, pb + tid, N, *P.lptrs, ubs, lacc);
+        if (tid < FZ_PT) LossF::template eval<S, OQ>(outp, xs, tid, pb + tid, N, *P.lptrs, lpre, ubs, lacc);
         __syncthreads();
         FZ_TS(9);
         // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----

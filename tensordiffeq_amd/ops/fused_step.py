@@ -64,6 +64,16 @@ def header_source():
     return "\n".join(out)
 
 
+def _pre_loads(P):
+    """The program's per-point input loads (VAL / LAM / SCAL) in code order: ``[(r, name, a)]``."""
+    out = []
+    for op, r, a, b in P.code:
+        name = loss_jit._OPN[op]
+        if name in ("VAL", "LAM", "SCAL"):
+            out.append((r, name, a))
+    return out
+
+
 def gen_loss(groups, n_terms, nacc, S):
     """``struct GenLoss`` of the loss groups laid out in the fused point set.  ``groups``: one
     ``(program, start, n_slots, n)`` per group - its ``n`` instances occupy points ``start + k``
@@ -71,39 +81,71 @@ def gen_loss(groups, n_terms, nacc, S):
     ``start`` even, so a pair never straddles a 32-point tile).  The statements are those of
     :func:`.loss_jit._group_code` per point: J streams / coordinates from the tile (the partner's
     from the next point-thread), loss / scalar-gradient sums into the thread's accumulators, dJ
-    of the instance's points into the tile's ``ubs``.  Points outside every group get dJ = 0."""
+    of the instance's points into the tile's ``ubs``.  Points outside every group get dJ = 0.  The
+    per-point inputs (SA weights, data values, scalars) are loaded by ``prefetch`` one tile ahead."""
+    npre = max([1] + [len(_pre_loads(P)) for (P, _, _, _) in groups])
     L = []
     e = L.append
     e("struct GenLoss {")
-    e(f"  static constexpr int NACC = {max(1, nacc)};")
+    e(f"  static constexpr int NACC = {max(1, nacc)}, NPRE = {npre};")
+
+    def branches(body):
+        kw = "if"
+        for (P, start, ns, n) in groups:
+            end = start + ns * n
+            e(f"    {kw} (n >= {start} && n < {end} && n < N) {{")
+            kw = "else if"
+            if ns == 2:
+                e(f"      if ((n - {start}) & 1) return;   // the pair's first point-thread owns it")
+                e(f"      const int i = (n - {start}) >> 1;")
+            else:
+                e(f"      const int i = n - {start};")
+            body(P, ns)
+            e("      return;")
+            e("    }")
+
+    # ---- prefetch: the group's input loads, in code order, into pre[]
+    e("  __device__ static void prefetch(const FzLossPtrs& ptr, int n, int N, float (&pre)[NPRE]) {")
+
+    # TDQ_FS_PREFETCH=1: the inputs loaded one tile ahead (the loss phase 3.1k -> 2.5k cycles per
+    # tile) - but the step measured 0.1702 vs 0.1679 ms on one box (the extra live registers,
+    # profiles/r5prefab_prefetch_ab.txt), so eval loads them itself by default
+    pref = os.environ.get("TDQ_FS_PREFETCH", "0") == "1"
+
+    def pre_body(P, ns):
+        if not pref:
+            return
+        for j, (r, name, a) in enumerate(_pre_loads(P)):
+            src = {"VAL": f"ptr.val[{a}][i]", "LAM": f"ptr.lam[{a}][i]", "SCAL": f"*ptr.scal[{a}]"}[name]
+            e(f"      pre[{j}] = {src};")
+
+    branches(pre_body)
+    e("  }")
+    # ---- eval
     e("  template <int S, int OQ>")
     e("  __device__ static void eval(const float* jv, const float* xs, int t, int n, int N, "
-      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC]) {")
+      "const FzLossPtrs& ptr, const float (&pre)[NPRE], float* ubs, float (&acc)[NACC]) {")
     e("    #define JV(s_, k_) jv[((s_) * FZ_PT + (k_)) * OQ]")
     e("    #define UB(s_, k_) ubs[((s_) * FZ_PT + (k_)) * 4]")
-    kw = "if"
-    for (P, start, ns, n) in groups:
-        end = start + ns * n
-        e(f"    {kw} (n >= {start} && n < {end} && n < N) {{")
-        kw = "else if"
-        if ns == 2:
-            e(f"      if ((n - {start}) & 1) return;   // the pair's first point-thread owns it")
-            e(f"      const int i = (n - {start}) >> 1;")
-        else:
-            e(f"      const int i = n - {start};")
+
+    def eval_body(P, ns):
         nr = max(1, P.n_regs)
+        slot = {r: j for j, (r, _, _) in enumerate(_pre_loads(P))}
         e("      float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
         e("      float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
         e("      float " + ", ".join(f"dj{sl}_{b} = 0.f" for sl in range(ns) for b in range(S)) + ";")
 
-        def load(name, r, a, b, ns=ns):
+        def load(name, r, a, b):
             if name in ("STREAM", "COORD") and a >= ns:
                 raise ValueError("fused step: slot outside the group")
-            return {"STREAM": f"      v{r} = JV({b}, t + {a});",
-                    "COORD": f"      v{r} = xs[(t + {a}) * TDQ_MAXD + {b}];",
-                    "VAL": f"      v{r} = ptr.val[{a}][i];",
-                    "LAM": f"      v{r} = ptr.lam[{a}][i];",
-                    "SCAL": f"      v{r} = *ptr.scal[{a}];"}[name]
+            if name == "STREAM":
+                return f"      v{r} = JV({b}, t + {a});"
+            if name == "COORD":
+                return f"      v{r} = xs[(t + {a}) * TDQ_MAXD + {b}];"
+            if not pref:
+                return {"VAL": f"      v{r} = ptr.val[{a}][i];", "LAM": f"      v{r} = ptr.lam[{a}][i];",
+                        "SCAL": f"      v{r} = *ptr.scal[{a}];"}[name]
+            return f"      v{r} = pre[{slot[r]}];"
 
         loss_jit._forward_code(P, e, load)
         for (f, w, tt, c) in P.outputs:
@@ -123,8 +165,8 @@ def gen_loss(groups, n_terms, nacc, S):
 
         loss_jit._reverse_code(P, e, store)
         e("      " + " ".join(f"UB({b}, t + {sl}) = dj{sl}_{b};" for sl in range(ns) for b in range(S)))
-        e("      return;")
-        e("    }")
+
+    branches(eval_body)
     e("    #pragma unroll")
     e("    for (int s = 0; s < S; ++s) UB(s, t) = 0.f;")
     e("    #undef JV")
