@@ -64,6 +64,10 @@ def _declare(lib):
         "tdq_jet_fused_lds": (I, [I, P, I, I, I, I]),
         "tdq_device_cus": (I, []),
         "tdq_slab_floats_rows": (L, [I, I, P, I, I]),
+        # hand-written GEMMs of the layer-wise engine (csrc/lay_gemm.hip, ops/jet_layered.py)
+        "tdq_lay_nn": (I, [I, P, P, L, P, P, L, P, L, I, I, I, P]),
+        "tdq_lay_tn": (I, [I, P, P, L, P, P, L, P, I, I, I, I, P]),
+        "tdq_lay_xtz": (I, [P, I, P, I, I, P, I, P]),
         "tdq_adam_multi": (I, [P, I, P, P, P]),
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),

@@ -100,6 +100,51 @@ class _Op:
         return o
 
 
+_PREC = {"bf16": 0, "bf16x3": 1, "fp32": 2}
+
+
+def _hip_gemm():
+    """The hand-written MFMA GEMMs (csrc/lay_gemm.hip) serve CUDA operands unless
+    ``TDQ_LAY_GEMM=0`` (the library GEMMs, kept as the A/B reference)."""
+    import os
+    return os.environ.get("TDQ_LAY_GEMM", "1") != "0" and _lib.available()
+
+
+def _planes(o):
+    """(hi, lo) device planes of an operand in its precision (fp32: the tensor itself)."""
+    if hasattr(o, "f"):
+        return o.f, None
+    return o.h, getattr(o, "l", None)
+
+
+def _mm_w(a, w, prec, out=None):
+    """a @ w for an activation operand ``a`` [M, K] (:class:`_Op`) and fp32 weights ``w`` [K, N]
+    (the weights' transposed operand ``[N, K]`` is formed here - W x W, small)."""
+    return _mm_bt(a, w.t().contiguous(), prec, out)
+
+
+def _mm_bt(a, bt, prec, out=None):
+    """a @ bt^T with ``bt`` [N, K] fp32: the hand-written NN GEMM on CUDA, else the library."""
+    if a.prec != prec:
+        raise ValueError("operand precision mismatch")
+    x = a.f if hasattr(a, "f") else a.h
+    if x.is_cuda and _hip_gemm():
+        bo = _Op(bt, prec) if prec != "fp32" else None
+        ah, al = _planes(a)
+        bh, bl = (bt, None) if bo is None else _planes(bo)
+        M, K = ah.shape
+        N = bh.shape[0]
+        c = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=x.device)
+        if not (c.is_contiguous() and ah.is_contiguous() and bh.is_contiguous()):
+            raise ValueError("GEMM operands must be contiguous")
+        lib = _lib.load(required=True)
+        rc = lib.tdq_lay_nn(_PREC[prec], _lib.ptr(ah), _lib.ptr(al), K, _lib.ptr(bh), _lib.ptr(bl), K,
+                            _lib.ptr(c), N, M, N, K, _lib.stream_ptr(x.device))
+        _lib.check(rc, "tdq_lay_nn")
+        return c
+    return _mm(a, _Op(bt.t(), prec), out)
+
+
 def _mm(a, b, out=None):
     """a @ b for two :class:`_Op` of the same precision (library GEMMs, fp32 output)."""
     if hasattr(a, "f"):
@@ -118,9 +163,25 @@ def _mm(a, b, out=None):
 def _mm_tn(a, b, out):
     """out = a^T b for :class:`_Op` a [L, M], b [L, N] with a long reduction L = S*N (the weight
     gradient): as ONE library GEMM its M x N = W x W output is only a few tiles, so a handful of CUs
-    did all the work (bf16 ~50 TF/s, profiles/r3_ag_*).  The reduction is split into C chunks run as
-    one batched GEMM ([C, M, L/C] x [C, L/C, N]) and the C partial products summed in fixed order."""
-    L = (a.f if hasattr(a, "f") else a.h).shape[0]
+    did all the work (bf16 ~50 TF/s, profiles/r3_ag_*).  The reduction is split into C chunks - the
+    hand-written TN GEMM's grid z on CUDA (csrc/lay_gemm.hip), else one batched library GEMM
+    ([C, M, L/C] x [C, L/C, N]) - and the C partial products summed in fixed order."""
+    x = a.f if hasattr(a, "f") else a.h
+    if x.is_cuda and _hip_gemm():
+        ah, al = _planes(a)
+        bh, bl = _planes(b)
+        L, Ma = ah.shape
+        Nb = bh.shape[1]
+        rows = ((L + 63) // 64 + 31) // 32 * 32      # ~64 chunks, a multiple of 32 rows each
+        nch = -(-L // rows)
+        part = torch.empty((nch, Ma, Nb), dtype=torch.float32, device=x.device)
+        lib = _lib.load(required=True)
+        rc = lib.tdq_lay_tn(_PREC[a.prec], _lib.ptr(ah.contiguous()), _lib.ptr(al), Ma, _lib.ptr(bh.contiguous()),
+                            _lib.ptr(bl), Nb, _lib.ptr(part), L, Ma, Nb, rows, _lib.stream_ptr(x.device))
+        _lib.check(rc, "tdq_lay_tn")
+        torch.sum(part, dim=0, out=out)
+        return out
+    L = x.shape[0]
     C = 64 if L >= 64 * 1024 else max(1, L // 1024)
     L0 = L - L % C
 
@@ -177,19 +238,24 @@ def forward_raw(X, P, net, plan, precision="fp32"):
     K0, b0 = ws[0]
     W0 = K0.shape[1]
     Z = torch.zeros((S, N, W0), dtype=P.dtype, device=X.device)
-    torch.mm(X, K0, out=Z[0])                       # layer 0: the input is exact (no GEMM on streams)
+    if X.is_cuda:   # layer 0: the input is exact fp32, d_in <= 8 columns - FMAs, not a GEMM
+        torch.mul(X[:, :1], K0[0], out=Z[0])
+        for j in range(1, X.shape[1]):
+            Z[0].addcmul_(X[:, j:j + 1], K0[j])
+    else:
+        torch.mm(X, K0, out=Z[0])
     for s in range(1, S):
         if spec[3 * s] == 1:
             Z[s].copy_(K0[spec[3 * s + 1]].expand(N, W0))
     H, op = _epi(True, Z, None, b0, spec, precision)
     Hs, Ho = [H], [op]                               # saved activations and their GEMM operands
     for K, b in ws[1:-1]:
-        Z = _mm(Ho[-1], _Op(K, precision)).view(S, N, K.shape[1])
+        Z = _mm_w(Ho[-1], K, precision).view(S, N, K.shape[1])
         H, op = _epi(True, Z, None, b, spec, precision)
         Hs.append(H)
         Ho.append(op)
     Ko, bo = ws[-1]
-    J = _mm(Ho[-1], _Op(Ko, precision)).view(S, N, Ko.shape[1])
+    J = _mm_w(Ho[-1], Ko, precision).view(S, N, Ko.shape[1])
     J[0] += bo
     return J, ("layered", X, P, net, spec, Hs, Ho, precision)
 
@@ -211,18 +277,29 @@ def backward_raw(saved, dJ, grad=None):
     if dJ.shape[2] == 1:  # an outer product: a K = 1 GEMM ran 10x slower than this broadcast
         HB = (dJ.view(S * N, 1) * Ko.view(1, -1)).view(S, N, Ko.shape[0])
     else:
-        HB = _mm(dJo, _Op(Ko.t().contiguous(), prec)).view(S, N, Ko.shape[0])
+        HB = _mm_bt(dJo, Ko, prec).view(S, N, Ko.shape[0])
     for i in range(len(ws) - 2, 0, -1):
         K, _ = ws[i]
         ZB, ZBo = _epi(False, HB, Hs[i], None, spec, prec)
         _mm_tn(Ho[i - 1], ZBo, gw[i][0])
         torch.sum(ZB[0], dim=0, out=gw[i][1])
-        # K^T materialized (W x W): the library's transposed-B kernels for this shape ran ~4x slower
-        # than its row-major ones (rocprofv3, profiles/r3_ag_*)
-        HB = _mm(ZBo, _Op(K.t().contiguous(), prec)).view(S, N, K.shape[0])
+        # HB = ZB K^T: K itself is the transposed operand [W_in, W_out] of the NN GEMM (library path:
+        # K^T materialized - its transposed-B kernels ran ~4x slower, profiles/r3_ag_*)
+        HB = _mm_bt(ZBo, K, prec).view(S, N, K.shape[0])
     ZB0, _ = _epi(False, HB, Hs[0], None, spec)
     dK0, db0 = gw[0]
-    torch.mm(X.t(), ZB0[0], out=dK0)
+    if X.is_cuda and _hip_gemm():   # X^T ZB0: d_in rows of exact fp32 - chunked FMA partials
+        rows = 32   # many short row chunks: the kernel is latency-bound (one 16-byte Z load per row)
+        lib = _lib.load(required=True)
+        z0 = ZB0[0].contiguous()
+        for j0 in range(0, X.shape[1], 8):   # (the kernel takes up to 8 input columns per launch)
+            xj = X[:, j0:j0 + 8].contiguous()
+            part = torch.empty((-(-N // rows), xj.shape[1], dK0.shape[1]), dtype=torch.float32, device=X.device)
+            _lib.check(lib.tdq_lay_xtz(_lib.ptr(xj), xj.shape[1], _lib.ptr(z0), N, z0.shape[1], _lib.ptr(part), rows,
+                                       _lib.stream_ptr(X.device)), "tdq_lay_xtz")
+            torch.sum(part, dim=0, out=dK0[j0:j0 + xj.shape[1]])
+    else:
+        torch.mm(X.t(), ZB0[0], out=dK0)
     for s in range(1, S):
         if spec[3 * s] == 1:
             dK0[spec[3 * s + 1]] += ZB0[s].sum(dim=0)
