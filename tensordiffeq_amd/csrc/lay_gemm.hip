@@ -20,10 +20,14 @@
 // of 32 through LDS - NN double-buffered with 16-byte fragment reads, TN row-major staging read
 // back with ds_read_b64_tr_b16.  fp32: 64 x 128 (NN, fragments straight from global memory) and
 // 64 x 64 (TN, LDS-transposed) tiles on v_mfma_f32_16x16x4_f32.
-// Measured on MI355X (AC [2,W x4,1], 50k points, Adam step, gpurun_out/r5lay): bf16x3 width 256
-// 4.95 ms vs 5.82 ms on the library GEMMs (hipBLASLt); bf16 width 512 5.56 vs 4.81 ms.
+// The layer jet (lay_jet.h) runs in the GEMM epilogues (lay_nnj_kernel) and in two elementwise end-layer
+// kernels (lay_in_fwd_kernel: X K0 + jet; lay_out_bwd_kernel: dJ Ko^T + adjoint jet), so no fp32
+// activation / adjoint plane of a hidden layer ever goes through HBM.  Measured on MI355X (AC
+// [2, W x 4, 1], 50k points, one Adam step, profiles/r5lay4_*): bf16 width 512 2.81 ms and bf16x3
+// width 256 1.79 ms per step, vs 4.75 / 5.69 ms on the library GEMMs (hipBLASLt) + standalone pass.
 // Reference: tensordiffeq/networks.py:10-20 (any layer list), the reference's tape GEMMs.
 #include "jet_bf3.h"
+#include "lay_jet.h"
 
 namespace {
 
@@ -208,102 +212,138 @@ __global__ void __launch_bounds__(256) lay_tn_kernel(const typename Op<P>::T* __
   }
 }
 
-// dK0 partial: C[z][j][f] = sum over rows n of chunk z of X[n][j] Z[n][f] (the input layer: d_in <=
-// TDQ_MAXD columns of exact fp32 coordinates, no GEMM shape): 4 features per thread (16-byte Z
-// loads), rows unrolled by 4 so several loads are in flight
-__global__ void __launch_bounds__(256) lay_xtz_kernel(const float* __restrict__ X, int d_in,
-                                                      const float* __restrict__ Z, int N, int W,
-                                                      float* __restrict__ Cp, int rows_per_chunk) {
-  const int f = 4 * (blockIdx.x * 256 + threadIdx.x);
+// X^T Z partials, C[z][j][f] = sum over rows n of chunk z of X[n][j] Z[n][f], for D <= TDQ_MAXD
+// columns of exact fp32 X (no GEMM shape): the input layer's dK0 = X^T ZB0 (Z fp32) and the output
+// layer's dKo^T = dJ^T H (X = dJ, Z = the saved post-activations as hi + lo bf16 planes, ZP).  4
+// features per thread (16 / 2 x 8-byte Z loads), short row chunks so that many waves are in flight
+// (the kernel is latency-bound); blockDim.x threads cover 4 blockDim.x features.
+template <int D, bool ZP>
+__global__ void __launch_bounds__(256) lay_xtz_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                                                      const __bf16* __restrict__ Zh, const __bf16* __restrict__ Zl,
+                                                      int N, int W, float* __restrict__ Cp, int rows_per_chunk) {
+  const int f = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
   if (f >= W) return;
   const int n_lo = blockIdx.y * rows_per_chunk, n_hi = min(N, n_lo + rows_per_chunk);
   const bool v4 = (W % 4 == 0);
-  f32x4 a[TDQ_MAXD];
+  f32x4 a[D];
 #pragma unroll
-  for (int j = 0; j < TDQ_MAXD; ++j) a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto zrow = [&](int n) {
-    if (v4) return *reinterpret_cast<const f32x4*>(Z + (long long)n * W + f);
+  for (int j = 0; j < D; ++j) a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int n = n_lo; n < n_hi; ++n) {
+    const long long o = (long long)n * W + f;
     f32x4 z;
+    if (v4) {
+      if constexpr (ZP) {
+        const bf16x4 h = *reinterpret_cast<const bf16x4*>(Zh + o), l = *reinterpret_cast<const bf16x4*>(Zl + o);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[e] = f + e < W ? Z[(long long)n * W + f + e] : 0.f;
-    return z;
-  };
-  int n = n_lo;
-  for (; n + 3 < n_hi; n += 4) {
-    f32x4 z[4];
+        for (int e = 0; e < 4; ++e) z[e] = (float)h[e] + (float)l[e];
+      } else {
+        z = *reinterpret_cast<const f32x4*>(Z + o);
+      }
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) z[u] = zrow(n + u);
+      for (int e = 0; e < 4; ++e)
+        z[e] = f + e < W ? (ZP ? (float)Zh[o + e] + (float)Zl[o + e] : Z[o + e]) : 0.f;
+    }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int j = 0; j < TDQ_MAXD; ++j)
-        if (j < d_in) a[j] += X[(long long)(n + u) * d_in + j] * z[u];
+    for (int j = 0; j < D; ++j) a[j] += X[(long long)n * D + j] * z;
   }
-  for (; n < n_hi; ++n) {
-    const f32x4 z = zrow(n);
+  float* out = Cp + (long long)blockIdx.y * D * W;
 #pragma unroll
-    for (int j = 0; j < TDQ_MAXD; ++j)
-      if (j < d_in) a[j] += X[(long long)n * d_in + j] * z;
-  }
-  float* out = Cp + (long long)blockIdx.y * d_in * W;
-  for (int j = 0; j < d_in; ++j)
+  for (int j = 0; j < D; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (f + e < W) out[(long long)j * W + f + e] = a[j][e];
 }
 
 // ---- bf16 families: 128 x 128 workgroup tiles staged through LDS --------------------------------
-// 4 waves in 2 x 2, each a 64 x 64 block (4 x 4 MFMA tiles): per 32-deep k-step a wave reads 4 A and
-// 4 B fragments from LDS for 16 MFMAs (x3 in bf16x3).  LDS rows of 32 k-values padded to 40 (80 B):
-// the 16 rows of a fragment read land on distinct banks.  Two buffers: the next k-step's global
+// 4 waves in 2 x 2, each a 64 x 64 block (4 x 4 MFMA tiles): per 32-deep k-substep a wave reads 4 A
+// and 4 B fragments from LDS for 16 MFMAs (x3 in bf16x3).  Two buffers: the next k-step's global
 // loads are in flight while the current one is multiplied.
-constexpr int LS = 40;
+
+// 8 bf16 at element offset off + k of a row (zero when !ok or past K)
+__device__ __forceinline__ bf16x8 ldr8(const __bf16* __restrict__ base, long long off, bool ok, int k, int K,
+                                       bool vec) {
+  bf16x8 r;
+  if (ok) {
+    const __bf16* p = base + off + k;
+    if (vec && k + 8 <= K) return *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (k + j < K) ? p[j] : (__bf16)0.f;
+    return r;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)0.f;
+  return r;
+}
 
 // 8 bf16 of (row, k..k+7) of a row-major [nrows][ld] matrix, zero outside
 __device__ __forceinline__ bf16x8 ldg8(const __bf16* __restrict__ base, long long ld, int row, int nrows, int k, int K,
                                        bool vec) {
-  __bf16 v[8];
-  ld8(base, ld, row, nrows, k, K, vec, v);
-  return pack8(v);
+  return ldr8(base, (long long)row * ld, row < nrows, k, K, vec);
 }
 
+// k-depth of a staged step: 64 in bf16 (fewer barriers per MFMA), 32 in bf16x3 (two planes per
+// operand - the 64-deep double buffer would need 144 KB of LDS, one workgroup per CU)
 template <int P>
-__global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__ Ah, const __bf16* __restrict__ Al,
-                                                      long long lda, const __bf16* __restrict__ Bh,
-                                                      const __bf16* __restrict__ Bl, long long ldb,
-                                                      float* __restrict__ C, long long ldc, int M, int N, int K,
-                                                      int vec) {
+constexpr int nn_bk() {
+  return P == 1 ? 32 : 64;
+}
+template <int P>
+constexpr int nn_rows_per_thread() {  // rows of the 128-row tiles one thread stages (8 k-values each)
+  return 128 * (nn_bk<P>() / 8) / 256;
+}
+template <int P>
+constexpr int nn_stage_bytes() {  // {A, B} x 2 buffers x planes x 128 rows x (BK + 8) bf16
+  return 2 * 2 * (P == 1 ? 2 : 1) * 128 * (nn_bk<P>() + 8) * 2;
+}
+
+// the A and B rows a thread stages (element offsets of row starts, validity): row c is tile row
+// tid / (BK / 8) + c * 256 / (BK / 8)
+struct NnRows {
+  long long a[4], b[4];
+  bool va[4], vb[4];
+};
+template <int P>
+__device__ __forceinline__ int nn_row(int c) {
+  constexpr int CPR = nn_bk<P>() / 8;
+  return (int)threadIdx.x / CPR + c * (256 / CPR);
+}
+
+// The main loop of a 128 x 128 tile: acc[i][j] = the wave's (i, j) 16 x 16 block of A B over K.
+// LDS rows of BK k-values padded by 8 (row strides of 40 / 72 bf16: the 16 rows of a fragment read
+// land on distinct banks).
+template <int P>
+__device__ __forceinline__ void nn_loop(__bf16* smem, const __bf16* __restrict__ Ah, const __bf16* __restrict__ Al,
+                                        const __bf16* __restrict__ Bh, const __bf16* __restrict__ Bl,
+                                        const NnRows& R, int K, bool v, f32x4 (&acc)[4][4]) {
   constexpr int NB = P == 1 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) __bf16 sA[2][NB][128 * LS];
-  __shared__ __attribute__((aligned(16))) __bf16 sB[2][NB][128 * LS];
+  constexpr int BK = nn_bk<P>(), LK = BK + 8, NR = nn_rows_per_thread<P>(), CPR = BK / 8;
+  constexpr int SZ = 128 * LK;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, p = l & 15, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
-  const bool v = vec != 0;
-  // staging: chunks t and t + 256 of the 512 8-element chunks of a 128 x 32 tile
-  const int sr0 = tid >> 2, sk = (tid & 3) * 8, sr1 = sr0 + 64;
-  bf16x8 ra[2][NB], rb[2][NB];
+  const int sk = (tid % CPR) * 8;
+  auto sA = [&](int buf, int b) { return smem + (buf * NB + b) * SZ; };
+  auto sB = [&](int buf, int b) { return smem + (2 * NB + buf * NB + b) * SZ; };
+  bf16x8 ra[NR][NB], rb[NR][NB];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const __bf16* A = b ? Al : Ah;
-      const __bf16* B = b ? Bl : Bh;
-      ra[0][b] = ldg8(A, lda, m0 + sr0, M, k0 + sk, K, v);
-      ra[1][b] = ldg8(A, lda, m0 + sr1, M, k0 + sk, K, v);
-      rb[0][b] = ldg8(B, ldb, n0 + sr0, N, k0 + sk, K, v);
-      rb[1][b] = ldg8(B, ldb, n0 + sr1, N, k0 + sk, K, v);
-    }
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        ra[c][b] = ldr8(b ? Al : Ah, R.a[c], R.va[c], k0 + sk, K, v);
+        rb[c][b] = ldr8(b ? Bl : Bh, R.b[c], R.vb[c], k0 + sk, K, v);
+      }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      *reinterpret_cast<bf16x8*>(&sA[buf][b][sr0 * LS + sk]) = ra[0][b];
-      *reinterpret_cast<bf16x8*>(&sA[buf][b][sr1 * LS + sk]) = ra[1][b];
-      *reinterpret_cast<bf16x8*>(&sB[buf][b][sr0 * LS + sk]) = rb[0][b];
-      *reinterpret_cast<bf16x8*>(&sB[buf][b][sr1 * LS + sk]) = rb[1][b];
-    }
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        const int r = nn_row<P>(c);
+        *reinterpret_cast<bf16x8*>(sA(buf, b) + r * LK + sk) = ra[c][b];
+        *reinterpret_cast<bf16x8*>(sB(buf, b) + r * LK + sk) = rb[c][b];
+      }
   };
-  f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -312,16 +352,403 @@ __global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__
   sstore(0);
   __syncthreads();
   int buf = 0;
-  for (int k0 = 0; k0 < K; k0 += 32) {
-    const bool more = k0 + 32 < K;
-    if (more) gload(k0 + 32);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    const bool more = k0 + BK < K;
+    if (more) gload(k0 + BK);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 a[4][NB], b[4][NB];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          a[i][q] = *reinterpret_cast<const bf16x8*>(sA(buf, q) + (wm * 64 + 16 * i + p) * LK + kk + 8 * g);
+          b[i][q] = *reinterpret_cast<const bf16x8*>(sB(buf, q) + (wn * 64 + 16 * i + p) * LK + kk + 8 * g);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (P == 1) {
+            acc[i][j] = mfma_bf(a[i][1], b[j][0], acc[i][j]);
+            acc[i][j] = mfma_bf(a[i][0], b[j][1], acc[i][j]);
+          }
+          acc[i][j] = mfma_bf(a[i][0], b[j][0], acc[i][j]);
+        }
+    }
+    if (more) {
+      sstore(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+}
+
+// XCD-aware tile order: workgroup L runs on XCD L % 8, so the tiles of one XCD are made logically
+// consecutive (consecutive tiles share an A row block - it is read once into that XCD's L2)
+__device__ __forceinline__ int xcd_tile(int L, int total) {
+  const int q = total / 8;
+  return L < 8 * q ? (L % 8) * q + L / 8 : L;
+}
+
+template <int P>
+__global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__ Ah, const __bf16* __restrict__ Al,
+                                                      long long lda, const __bf16* __restrict__ Bh,
+                                                      const __bf16* __restrict__ Bl, long long ldb,
+                                                      float* __restrict__ C, long long ldc, int M, int N, int K,
+                                                      int vec) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[nn_stage_bytes<P>() / 2];
+  const int gx = (N + 127) / 128;
+  const int T = xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (T / gx) * 128, n0 = (T % gx) * 128;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, p = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  NnRows R;
+#pragma unroll
+  for (int c = 0; c < nn_rows_per_thread<P>(); ++c) {
+    const int r = nn_row<P>(c);
+    R.a[c] = (long long)(m0 + r) * lda;
+    R.b[c] = (long long)(n0 + r) * ldb;
+    R.va[c] = m0 + r < M;
+    R.vb[c] = n0 + r < N;
+  }
+  f32x4 acc[4][4];
+  nn_loop<P>(smem, Ah, Al, Bh, Bl, R, K, vec != 0, acc);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn * 64 + 16 * j + p;
+      if (col >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ro = m0 + wm * 64 + 16 * i + 4 * g + r;
+        if (ro < M) C[(long long)ro * ldc + col] = acc[i][j][r];
+      }
+    }
+}
+
+// ---- the layer jet on (point, feature) tiles: GEMM epilogues and the elementwise end layers ------
+// Tiles are PT = 128 / S points x 128 features; thread t owns feature quad 4 (t & 31) of points
+// t >> 5, + 8, ... for all S streams.  Modes:
+//   EPI_FWD   Z -> H = jet(Z + b), written as the next GEMMs' bf16 operands hi = rne(H) and
+//             lo = rne(H - hi) (hi + lo is also the saved post-activation of the adjoint)
+//   EPI_BWD   HB + saved H (hi + lo) -> ZB = adjoint jet, written as bf16 hi (+ lo for bf16x3), and
+//             per-tile column sums of ZB's value stream (the bias gradient's partials)
+//   EPI_BWD0  the input layer's adjoint: no ZB leaves the kernel, only per-tile partials of every
+//             quantity the input layer's gradient needs - column sums of all S streams (bias; the
+//             first-order streams' dK0 rows) and X^T zb (dK0 = X^T ZB0 over the d_in <= 8 exact
+//             fp32 coordinates)
+// Partials: part[tile_y][q][Nout], q < 1 (EPI_BWD) or S + d_in (EPI_BWD0), summed by the caller.
+enum { EPI_FWD = 0, EPI_BWD = 1, EPI_BWD0 = 2 };
+
+struct EpiArgs {
+  int Npts, Nout, d_in;
+  const float* bias;         // EPI_FWD: [Nout]
+  const __bf16 *Hh, *Hl;     // EPI_BWD*: the layer's saved post-activations [S * Npts][Nout]
+  __bf16 *Oh, *Ol;           // EPI_FWD / EPI_BWD outputs [S * Npts][Nout] (Ol nullable in EPI_BWD)
+  float* part;               // EPI_BWD* partials (nullable in EPI_BWD)
+  const float* X;            // EPI_BWD0: [Npts][d_in]
+  LSpec sp;
+};
+
+// src(s, t) -> the f32x4 input (Z or HB) of stream s, tile point t, this thread's feature quad.
+// red: LDS scratch of 4 x (S + TDQ_MAXD) x 128 floats (may alias the source tile: a barrier
+// precedes its first write).  Every thread of the block must call this.
+template <int S, int MODE, class Src>
+__device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, Src src, float* red) {
+  constexpr int PT = 128 / S;
+  constexpr int NS = MODE == EPI_BWD0 ? S : 1;
+  constexpr int NX = MODE == EPI_BWD0 ? TDQ_MAXD : 1;
+  const int tid = threadIdx.x, pt0 = ty * PT;
+  const int f4 = (tid & 31) * 4, col = n0 + f4;
+  const bool cok = col < e.Nout;  // (Nout % 4 == 0: a quad is all in or all out)
+  float bb[4] = {0.f, 0.f, 0.f, 0.f}, ps[NS][4], px[NX][4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q) ps[q][v] = 0.f;
+#pragma unroll
+    for (int q = 0; q < NX; ++q) px[q][v] = 0.f;
+  }
+  if (MODE == EPI_FWD && cok) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) bb[v] = e.bias[col + v];
+  }
+  auto point = [&](int t) {
+    const int n = pt0 + t;
+    if (!cok || n >= e.Npts) return;
+    float x[S][4], y[S][4];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const f32x4 q = src(s, t);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) x[s][v] = q[v];
+    }
+    if constexpr (MODE == EPI_FWD) {
+      lay_jet_fwd<S, 4>(x, bb, e.sp, y);
+    } else {
+      float h[S][4];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const long long o = ((long long)s * e.Npts + n) * e.Nout + col;
+        const bf16x4 hh = *reinterpret_cast<const bf16x4*>(e.Hh + o), hl = *reinterpret_cast<const bf16x4*>(e.Hl + o);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) h[s][v] = (float)hh[v] + (float)hl[v];
+      }
+      lay_jet_bwd<S, 4>(h, x, e.sp, y);
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) ps[q][v] += y[q][v];
+      if constexpr (MODE == EPI_BWD0) {
+#pragma unroll
+        for (int j = 0; j < TDQ_MAXD; ++j) {
+          if (j < e.d_in) {
+            const float xv = e.X[(long long)n * e.d_in + j];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) px[j][v] += xv * y[0][v];
+          }
+        }
+      }
+    }
+    if constexpr (MODE != EPI_BWD0) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const long long o = ((long long)s * e.Npts + n) * e.Nout + col;
+        bf16x4 hv, lv;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          hv[v] = (__bf16)y[s][v];
+          lv[v] = (__bf16)(y[s][v] - (float)hv[v]);
+        }
+        *reinterpret_cast<bf16x4*>(e.Oh + o) = hv;
+        if (e.Ol != nullptr) *reinterpret_cast<bf16x4*>(e.Ol + o) = lv;
+      }
+    }
+  };
+  if constexpr (MODE == EPI_BWD0) {  // (rolled: the partial accumulators already hold 4 (S + 8) registers)
+#pragma unroll 1
+    for (int t = tid >> 5; t < PT; t += 8) point(t);
+  } else {
+    for (int t = tid >> 5; t < PT; t += 8) point(t);
+  }
+  if constexpr (MODE != EPI_FWD) {
+    if (e.part == nullptr) return;  // (uniform)
+    const int NP = MODE == EPI_BWD ? 1 : S + e.d_in;
+    // lanes l and l ^ 32 hold the same features: combine them, then the 4 waves through LDS
+    const int w = tid >> 6;
+    __syncthreads();  // red may alias the source tile
+#pragma unroll
+    for (int q = 0; q < NS + (MODE == EPI_BWD0 ? TDQ_MAXD : 0); ++q) {
+      if (q >= NP) break;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float a = q < NS ? ps[q < NS ? q : 0][v] : px[q >= NS ? q - NS : 0][v];
+        a += __shfl_xor(a, 32, 64);
+        if ((tid & 32) == 0) red[(w * NP + q) * 128 + f4 + v] = a;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < NP * 128; i += 256) {
+      const int q = i >> 7, c = i & 127;
+      if (n0 + c >= e.Nout) continue;
+      const float a = red[q * 128 + c] + red[(NP + q) * 128 + c] + red[(2 * NP + q) * 128 + c] +
+                      red[(3 * NP + q) * 128 + c];
+      e.part[((long long)ty * NP + q) * e.Nout + n0 + c] = a;
+    }
+  }
+}
+
+// NN GEMM + layer jet: the 128 tile rows are S streams x PT points (row s PT + t = stream s of point
+// pt0 + t, global row s Npts + pt0 + t of the stream-major planes), so one tile holds every stream of
+// its points; the accumulators go through LDS (a 128 x 132 fp32 tile) into lay_epilogue.
+constexpr int EPI_CS = 132;  // LDS row stride of the fp32 tile: the 4 row groups of a store land 16 banks apart
+
+struct NnjArgs {
+  const __bf16 *Ah, *Al, *Bh, *Bl;  // A planes [S * Npts][K]; B^T [Nout][K]
+  int K, vec;
+  EpiArgs e;
+};
+
+template <int P, int S, int MODE>
+__global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
+  constexpr int PT = 128 / S;
+  constexpr int STG = nn_stage_bytes<P>();
+  constexpr int EPI = 128 * EPI_CS * 4;
+  static_assert(4 * (TDQ_MAXS + TDQ_MAXD) * 128 * 4 <= EPI, "partials scratch fits the tile");
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(STG > EPI ? STG : EPI) / 2];
+  const int gx = (a.e.Nout + 127) / 128;
+  const int T = xcd_tile(blockIdx.x, gridDim.x);
+  const int ty = T / gx, n0 = (T % gx) * 128, pt0 = ty * PT;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, p = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  NnRows R;
+#pragma unroll
+  for (int c = 0; c < nn_rows_per_thread<P>(); ++c) {
+    const int r = nn_row<P>(c), rs = r / PT, rt = r % PT;
+    R.va[c] = rs < S && pt0 + rt < a.e.Npts;
+    R.a[c] = ((long long)rs * a.e.Npts + pt0 + rt) * a.K;
+    R.b[c] = (long long)(n0 + r) * a.K;
+    R.vb[c] = n0 + r < a.e.Nout;
+  }
+  f32x4 acc[4][4];
+  nn_loop<P>(smem, a.Ah, a.Al, a.Bh, a.Bl, R, a.K, a.vec != 0, acc);
+  __syncthreads();  // every wave is done with the staging buffers
+  float* sC = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sC[(wm * 64 + 16 * i + 4 * g + r) * EPI_CS + wn * 64 + 16 * j + p] = acc[i][j][r];
+  __syncthreads();
+  const int f4 = (tid & 31) * 4;
+  lay_epilogue<S, MODE>(a.e, ty, n0, [&](int s, int t) {
+    return *reinterpret_cast<const f32x4*>(&sC[(s * PT + t) * EPI_CS + f4]);
+  }, sC);
+}
+
+// The input layer forward without a GEMM: Z = X K0 (d_in <= 8 exact fp32 columns), the first-order
+// streams' Z = the K0 row of their coordinate, second-order streams 0 - straight into the jet.
+template <int S>
+__global__ void __launch_bounds__(256) lay_in_fwd_kernel(EpiArgs e, const float* __restrict__ X,
+                                                         const float* __restrict__ K0) {
+  __shared__ float red[4];  // (EPI_FWD: no partials)
+  const int gx = (e.Nout + 127) / 128;
+  const int ty = blockIdx.x / gx, n0 = (blockIdx.x % gx) * 128, pt0 = ty * (128 / S);
+  const int col = n0 + (threadIdx.x & 31) * 4;
+  const bool cok = col < e.Nout;
+  float k[TDQ_MAXD][4];
+#pragma unroll
+  for (int j = 0; j < TDQ_MAXD; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) k[j][v] = (cok && j < e.d_in) ? K0[(long long)j * e.Nout + col + v] : 0.f;
+  lay_epilogue<S, EPI_FWD>(e, ty, n0, [&](int s, int t) {
+    f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (s == 0) {
+      const int n = pt0 + t;
+#pragma unroll
+      for (int j = 0; j < TDQ_MAXD; ++j)
+        if (j < e.d_in) {
+          const float xv = X[(long long)n * e.d_in + j];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) z[v] += xv * k[j][v];
+        }
+    } else if (e.sp.stype[s] == 1) {  // d/dx_c of X K0 = row c of K0 (register-indexed select)
+#pragma unroll
+      for (int j = 0; j < TDQ_MAXD; ++j)
+        if (j == e.sp.coord[s]) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) z[v] = k[j][v];
+        }
+    }
+    return z;
+  }, red);
+}
+
+// The last hidden layer's adjoint without materializing HB = dJ Ko^T (the output layer, d_out <= 4
+// columns): hb computed per (point, feature quad) from dJ and the thread's Ko rows.  MODE EPI_BWD,
+// or EPI_BWD0 when the last hidden layer is the input layer.
+template <int S, int MODE>
+__global__ void __launch_bounds__(256) lay_out_bwd_kernel(EpiArgs e, const float* __restrict__ dJ,
+                                                          const float* __restrict__ Ko, int d_out) {
+  __shared__ __attribute__((aligned(16))) float red[4 * (TDQ_MAXS + TDQ_MAXD) * 128];
+  const int gx = (e.Nout + 127) / 128;
+  const int ty = blockIdx.x / gx, n0 = (blockIdx.x % gx) * 128, pt0 = ty * (128 / S);
+  const int col = n0 + (threadIdx.x & 31) * 4;
+  const bool cok = col < e.Nout;
+  float ko[TDQ_MAXO][4];
+#pragma unroll
+  for (int q = 0; q < TDQ_MAXO; ++q)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) ko[q][v] = (cok && q < d_out) ? Ko[(long long)(col + v) * d_out + q] : 0.f;
+  lay_epilogue<S, MODE>(e, ty, n0, [&](int s, int t) {
+    const float* dj = dJ + ((long long)s * e.Npts + pt0 + t) * d_out;
+    f32x4 hb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < TDQ_MAXO; ++q)
+      if (q < d_out) {
+        const float d = dj[q];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) hb[v] += d * ko[q][v];
+      }
+    return hb;
+  }, red);
+}
+
+
+// TN, bf16 families: 128 x 128 output tiles.  The 32-row k-step of A [rows][Ma] and B [rows][Nb]
+// is staged row-major ([row][feature], 16-byte stores, rows of 144 elements = 72 banks) and the
+// fragments are read with ds_read_b64_tr_b16 (cdna_hip_programming.md T10): a 16-lane group reads
+// rows 8g + q, columns 4p .. 4p + 3 (lane 4q + p) and lane i receives feature column i of those 4
+// k-rows - two reads (rows 8g.., 8g + 4..) give the 8 k-values of a 16x16x32 fragment.
+constexpr int TS = 144;
+template <int P>
+__global__ void __launch_bounds__(256) lay_tn2_kernel(const __bf16* __restrict__ Ah, const __bf16* __restrict__ Al,
+                                                      long long lda, const __bf16* __restrict__ Bh,
+                                                      const __bf16* __restrict__ Bl, long long ldb,
+                                                      float* __restrict__ Cp, int L, int Ma, int Nb,
+                                                      int rows_per_chunk, int vec) {
+  constexpr int NB = P == 1 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][NB][32 * TS];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][NB][32 * TS];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  // XCD-aware order (xcd_tile): the tiles of one row chunk run on one XCD, so its A / B rows are read
+  // from HBM once into that XCD's L2 (round-robin placement read them ~3x)
+  const int gx = (Nb + 127) / 128, gy = (Ma + 127) / 128;
+  const int T = xcd_tile(blockIdx.x, gridDim.x);
+  const int bz = T / (gx * gy), i0 = ((T / gx) % gy) * 128, j0 = (T % gx) * 128;
+  const int r_lo = bz * rows_per_chunk, r_hi = min(L, r_lo + rows_per_chunk);
+  const bool v = vec != 0;
+  // staging: chunks t, t + 256 of the 512 8-feature chunks of a 32-row x 128-feature tile
+  const int rr0 = tid >> 4, rr1 = rr0 + 16, fc = (tid & 15) * 8;
+  // transposed-read address of this lane: row 8g + q, column 4p (+ the tile's first column)
+  const int trq = (l & 15) >> 2, trp = l & 3;
+  const int ta = (8 * g + trq) * TS + 4 * trp, tb = ta + 4 * TS;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // double-buffered: the next 32-row step's global loads are in flight during this step's MFMAs
+  bf16x8 ra[2][NB], rb[2][NB];
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      ra[0][q] = ldg8(q ? Al : Ah, lda, r0 + rr0, r_hi, i0 + fc, Ma, v);
+      ra[1][q] = ldg8(q ? Al : Ah, lda, r0 + rr1, r_hi, i0 + fc, Ma, v);
+      rb[0][q] = ldg8(q ? Bl : Bh, ldb, r0 + rr0, r_hi, j0 + fc, Nb, v);
+      rb[1][q] = ldg8(q ? Bl : Bh, ldb, r0 + rr1, r_hi, j0 + fc, Nb, v);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      *reinterpret_cast<bf16x8*>(&sA[buf][q][rr0 * TS + fc]) = ra[0][q];
+      *reinterpret_cast<bf16x8*>(&sA[buf][q][rr1 * TS + fc]) = ra[1][q];
+      *reinterpret_cast<bf16x8*>(&sB[buf][q][rr0 * TS + fc]) = rb[0][q];
+      *reinterpret_cast<bf16x8*>(&sB[buf][q][rr1 * TS + fc]) = rb[1][q];
+    }
+  };
+  if (r_lo < r_hi) {
+    gload(r_lo);
+    sstore(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int r0 = r_lo; r0 < r_hi; r0 += 32) {
+    const bool more = r0 + 32 < r_hi;
+    if (more) gload(r0 + 32);
     bf16x8 a[4][NB], b[4][NB];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
-        a[i][q] = *reinterpret_cast<const bf16x8*>(&sA[buf][q][(wm * 64 + 16 * i + p) * LS + 8 * g]);
-        b[i][q] = *reinterpret_cast<const bf16x8*>(&sB[buf][q][(wn * 64 + 16 * i + p) * LS + 8 * g]);
+        const int ca = wm * 64 + 16 * i, cb = wn * 64 + 16 * i;
+        a[i][q] = cat8(tr_read(&sA[buf][q][ta + ca]), tr_read(&sA[buf][q][tb + ca]));
+        b[i][q] = cat8(tr_read(&sB[buf][q][ta + cb]), tr_read(&sB[buf][q][tb + cb]));
       }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -339,86 +766,8 @@ __global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__
       buf ^= 1;
     }
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn * 64 + 16 * j + p;
-      if (col >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ro = m0 + wm * 64 + 16 * i + 4 * g + r;
-        if (ro < M) C[(long long)ro * ldc + col] = acc[i][j][r];
-      }
-    }
-}
-
-// TN, bf16 families: 128 x 128 output tiles.  The 32-row k-step of A [rows][Ma] and B [rows][Nb]
-// is staged row-major ([row][feature], 16-byte stores, rows of 144 elements = 72 banks) and the
-// fragments are read with ds_read_b64_tr_b16 (cdna_hip_programming.md T10): a 16-lane group reads
-// rows 8g + q, columns 4p .. 4p + 3 (lane 4q + p) and lane i receives feature column i of those 4
-// k-rows - two reads (rows 8g.., 8g + 4..) give the 8 k-values of a 16x16x32 fragment.
-constexpr int TS = 144;
-template <int P>
-__global__ void __launch_bounds__(256) lay_tn2_kernel(const __bf16* __restrict__ Ah, const __bf16* __restrict__ Al,
-                                                      long long lda, const __bf16* __restrict__ Bh,
-                                                      const __bf16* __restrict__ Bl, long long ldb,
-                                                      float* __restrict__ Cp, int L, int Ma, int Nb,
-                                                      int rows_per_chunk, int vec) {
-  constexpr int NB = P == 1 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) __bf16 sA[NB][32 * TS];
-  __shared__ __attribute__((aligned(16))) __bf16 sB[NB][32 * TS];
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4;
-  const int wm = w >> 1, wn = w & 1;
-  const int i0 = blockIdx.y * 128, j0 = blockIdx.x * 128;
-  const int r_lo = blockIdx.z * rows_per_chunk, r_hi = min(L, r_lo + rows_per_chunk);
-  const bool v = vec != 0;
-  // staging: chunks t, t + 256 of the 512 8-feature chunks of a 32-row x 128-feature tile
-  const int rr0 = tid >> 4, rr1 = rr0 + 16, fc = (tid & 15) * 8;
-  // transposed-read address of this lane: row 8g + q, column 4p (+ the tile's first column)
-  const int trq = (l & 15) >> 2, trp = l & 3;
-  const int ta = (8 * g + trq) * TS + 4 * trp, tb = ta + 4 * TS;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int r0 = r_lo; r0 < r_hi; r0 += 32) {
-#pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const bf16x8 a0 = ldg8(q ? Al : Ah, lda, r0 + rr0, r_hi, i0 + fc, Ma, v);
-      const bf16x8 a1 = ldg8(q ? Al : Ah, lda, r0 + rr1, r_hi, i0 + fc, Ma, v);
-      const bf16x8 b0 = ldg8(q ? Bl : Bh, ldb, r0 + rr0, r_hi, j0 + fc, Nb, v);
-      const bf16x8 b1 = ldg8(q ? Bl : Bh, ldb, r0 + rr1, r_hi, j0 + fc, Nb, v);
-      *reinterpret_cast<bf16x8*>(&sA[q][rr0 * TS + fc]) = a0;
-      *reinterpret_cast<bf16x8*>(&sA[q][rr1 * TS + fc]) = a1;
-      *reinterpret_cast<bf16x8*>(&sB[q][rr0 * TS + fc]) = b0;
-      *reinterpret_cast<bf16x8*>(&sB[q][rr1 * TS + fc]) = b1;
-    }
-    __syncthreads();
-    bf16x8 a[4][NB], b[4][NB];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int ca = wm * 64 + 16 * i, cb = wn * 64 + 16 * i;
-        a[i][q] = cat8(tr_read(&sA[q][ta + ca]), tr_read(&sA[q][tb + ca]));
-        b[i][q] = cat8(tr_read(&sB[q][ta + cb]), tr_read(&sB[q][tb + cb]));
-      }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (P == 1) {
-          acc[i][j] = mfma_bf(a[i][1], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_bf(a[i][0], b[j][1], acc[i][j]);
-        }
-        acc[i][j] = mfma_bf(a[i][0], b[j][0], acc[i][j]);
-      }
-    __syncthreads();
-  }
   const int p = l & 15;
-  float* out = Cp + (long long)blockIdx.z * Ma * Nb;
+  float* out = Cp + (long long)bz * Ma * Nb;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -453,7 +802,9 @@ int tdq_lay_nn(int prec, const void* Ah, const void* Al, long long lda, const vo
   if (prec < 2) {  // the LDS-tiled kernels
     const int vec = aligned16<__bf16>(Ah, lda) && aligned16<__bf16>(Bh, ldb) &&
                     (prec == 0 || (aligned16<__bf16>(Al, lda) && aligned16<__bf16>(Bl, ldb)));
-    dim3 g2((N + 127) / 128, (M + 127) / 128);
+    const long long tiles = (long long)((N + 127) / 128) * ((M + 127) / 128);
+    if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const dim3 g2((unsigned)tiles);
     if (prec == 0)
       hipLaunchKernelGGL(lay_nn2_kernel<0>, g2, dim3(256), 0, st, (const __bf16*)Ah, (const __bf16*)Al, lda,
                          (const __bf16*)Bh, (const __bf16*)Bl, ldb, C, ldc, M, N, K, vec);
@@ -485,7 +836,9 @@ int tdq_lay_tn(int prec, const void* Ah, const void* Al, long long lda, const vo
   if (prec < 2) {  // the 128 x 128 LDS-tiled kernels
     const int vec = aligned16<__bf16>(Ah, lda) && aligned16<__bf16>(Bh, ldb) &&
                     (prec == 0 || (aligned16<__bf16>(Al, lda) && aligned16<__bf16>(Bl, ldb)));
-    dim3 g2((Nb + 127) / 128, (Ma + 127) / 128, nch);
+    const long long tiles = (long long)((Nb + 127) / 128) * ((Ma + 127) / 128) * nch;
+    if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const dim3 g2((unsigned)tiles);
     if (prec == 0)
       hipLaunchKernelGGL(lay_tn2_kernel<0>, g2, dim3(256), 0, st, (const __bf16*)Ah, (const __bf16*)Al, lda,
                          (const __bf16*)Bh, (const __bf16*)Bl, ldb, Cp, L, Ma, Nb, rows_per_chunk, vec);
@@ -504,12 +857,160 @@ int tdq_lay_tn(int prec, const void* Ah, const void* Al, long long lda, const vo
   return 0;
 }
 
-// Cp: nchunks x d_in x W partials of X^T Z (X [N][d_in], Z [N][W], fp32); the caller sums dim 0
-int tdq_lay_xtz(const float* X, int d_in, const float* Z, int N, int W, float* Cp, int rows_per_chunk, void* stream) {
-  if (N <= 0 || W <= 0 || d_in < 1 || d_in > TDQ_MAXD || rows_per_chunk <= 0) return (int)hipErrorInvalidValue;
+// Cp: nchunks x d_in x W partials of X^T Z (X [N][d_in] fp32; Z [N][W] fp32, or - Z == nullptr - the
+// bf16 planes Zh + Zl); the caller sums dim 0
+int tdq_lay_xtz2(const float* X, int d_in, const float* Z, const void* Zh, const void* Zl, int N, int W, float* Cp,
+                 int rows_per_chunk, void* stream) {
+  if (N <= 0 || W <= 0 || d_in < 1 || d_in > TDQ_MAXD || rows_per_chunk <= 0 ||
+      (Z == nullptr && (Zh == nullptr || Zl == nullptr)))
+    return (int)hipErrorInvalidValue;
   const int nch = (N + rows_per_chunk - 1) / rows_per_chunk;
-  hipLaunchKernelGGL(lay_xtz_kernel, dim3((W + 1023) / 1024, nch), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     X, d_in, Z, N, W, Cp, rows_per_chunk);
+  const int quads = (W + 3) / 4;
+  const int bs = quads >= 256 ? 256 : ((quads + 63) / 64) * 64;
+  const dim3 grid((quads + bs - 1) / bs, nch);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const __bf16 *h = (const __bf16*)Zh, *l = (const __bf16*)Zl;
+  switch (d_in) {
+#define TDQ_XTZ(d_)                                                                                          \
+  case d_:                                                                                                   \
+    if (Z != nullptr)                                                                                        \
+      hipLaunchKernelGGL((lay_xtz_kernel<d_, false>), grid, dim3(bs), 0, st, X, Z, h, l, N, W, Cp, rows_per_chunk); \
+    else                                                                                                     \
+      hipLaunchKernelGGL((lay_xtz_kernel<d_, true>), grid, dim3(bs), 0, st, X, Z, h, l, N, W, Cp, rows_per_chunk);  \
+    break;
+    TDQ_XTZ(1) TDQ_XTZ(2) TDQ_XTZ(3) TDQ_XTZ(4) TDQ_XTZ(5) TDQ_XTZ(6) TDQ_XTZ(7) TDQ_XTZ(8)
+#undef TDQ_XTZ
+  }
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+int tdq_lay_xtz(const float* X, int d_in, const float* Z, int N, int W, float* Cp, int rows_per_chunk, void* stream) {
+  if (Z == nullptr) return (int)hipErrorInvalidValue;
+  return tdq_lay_xtz2(X, d_in, Z, nullptr, nullptr, N, W, Cp, rows_per_chunk, stream);
+}
+
+// Host side of the layer-jet kernels: EpiArgs from the common arguments; false when invalid.
+static bool epi_args(EpiArgs& e, int S, const int* spec, int Npts, int Nout, int d_in) {
+  if (Npts <= 0 || Nout <= 0 || Nout % 4 != 0 || d_in < 0 || d_in > TDQ_MAXD) return false;
+  if (!lspec_parse(spec, S, e.sp)) return false;
+  for (int s = 0; s < S; ++s)
+    if (e.sp.stype[s] == 1 && (spec[3 * s + 1] < 0 || spec[3 * s + 1] >= TDQ_MAXD)) return false;
+  e.Npts = Npts;
+  e.Nout = Nout;
+  e.d_in = d_in;
+  e.bias = nullptr;
+  e.Hh = e.Hl = nullptr;
+  e.Oh = e.Ol = nullptr;
+  e.part = nullptr;
+  e.X = nullptr;
+  return true;
+}
+
+static bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
+
+// mode: EPI_FWD (bias, Oh, Ol), EPI_BWD (Hh, Hl, Oh, Ol nullable, part nullable [tiles_y][1][Nout]),
+// EPI_BWD0 (Hh, Hl, part [tiles_y][S + d_in][Nout], X [Npts][d_in]); tiles_y = ceil(Npts / (128 / S)).
+// Planes are contiguous: A [S * Npts][K], B^T [Nout][K], H / outputs [S * Npts][Nout].
+int tdq_lay_nnj(int prec, int mode, int S, const int* spec, const void* Ah, const void* Al, const void* Bh,
+                const void* Bl, int Npts, int K, int Nout, const float* bias, const void* Hh, const void* Hl, void* Oh,
+                void* Ol, float* part, const float* X, int d_in, void* stream) {
+  NnjArgs a;
+  if (!epi_args(a.e, S, spec, Npts, Nout, mode == EPI_BWD0 ? d_in : 0) || K <= 0 || prec < 0 || prec > 1 ||
+      (prec == 1 && (Al == nullptr || Bl == nullptr)) || Ah == nullptr || Bh == nullptr || mode < 0 || mode > 2)
+    return (int)hipErrorInvalidValue;
+  if (mode == EPI_FWD ? (bias == nullptr || Oh == nullptr || Ol == nullptr)
+                      : (Hh == nullptr || Hl == nullptr ||
+                         (mode == EPI_BWD ? Oh == nullptr : (part == nullptr || X == nullptr || d_in < 1))))
+    return (int)hipErrorInvalidValue;
+  if (!aligned8(Oh) || !aligned8(Ol) || !aligned8(Hh) || !aligned8(Hl)) return (int)hipErrorInvalidValue;
+  a.e.bias = bias; a.e.Hh = (const __bf16*)Hh; a.e.Hl = (const __bf16*)Hl;
+  a.e.Oh = (__bf16*)Oh; a.e.Ol = (__bf16*)Ol; a.e.part = part; a.e.X = X;
+  a.Ah = (const __bf16*)Ah; a.Al = (const __bf16*)Al; a.Bh = (const __bf16*)Bh; a.Bl = (const __bf16*)Bl;
+  a.K = K;
+  a.vec = aligned16<__bf16>(Ah, K) && aligned16<__bf16>(Bh, K) &&
+          (prec == 0 || (aligned16<__bf16>(Al, K) && aligned16<__bf16>(Bl, K)));
+  const long long tiles = (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+  if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)tiles);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define TDQ_NNJ_M(P_, S_, M_) hipLaunchKernelGGL((lay_nnj_kernel<P_, S_, M_>), grid, dim3(256), 0, st, a)
+#define TDQ_NNJ(P_, S_)                                 \
+  case S_:                                              \
+    if (mode == EPI_FWD) TDQ_NNJ_M(P_, S_, EPI_FWD);    \
+    else if (mode == EPI_BWD) TDQ_NNJ_M(P_, S_, EPI_BWD); \
+    else TDQ_NNJ_M(P_, S_, EPI_BWD0);                   \
+    break;
+  if (prec == 0) {
+    switch (S) {
+      TDQ_NNJ(0, 1) TDQ_NNJ(0, 2) TDQ_NNJ(0, 3) TDQ_NNJ(0, 4) TDQ_NNJ(0, 5) TDQ_NNJ(0, 6) TDQ_NNJ(0, 7) TDQ_NNJ(0, 8)
+      default: return (int)hipErrorInvalidValue;
+    }
+  } else {
+    switch (S) {
+      TDQ_NNJ(1, 1) TDQ_NNJ(1, 2) TDQ_NNJ(1, 3) TDQ_NNJ(1, 4) TDQ_NNJ(1, 5) TDQ_NNJ(1, 6) TDQ_NNJ(1, 7) TDQ_NNJ(1, 8)
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
+#undef TDQ_NNJ
+#undef TDQ_NNJ_M
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// The input layer forward (lay_in_fwd_kernel): X [Npts][d_in] fp32, K0 [d_in][Nout], bias [Nout] ->
+// the layer's post-activations as hi / lo bf16 planes [S * Npts][Nout].
+int tdq_lay_in_fwd(int S, const int* spec, const float* X, int d_in, const float* K0, const float* bias, int Npts,
+                   int Nout, void* Oh, void* Ol, void* stream) {
+  EpiArgs e;
+  if (!epi_args(e, S, spec, Npts, Nout, d_in) || d_in < 1 || X == nullptr || K0 == nullptr || bias == nullptr ||
+      Oh == nullptr || Ol == nullptr || !aligned8(Oh) || !aligned8(Ol))
+    return (int)hipErrorInvalidValue;
+  for (int s = 0; s < S; ++s)
+    if (e.sp.stype[s] == 1 && e.sp.coord[s] >= d_in) return (int)hipErrorInvalidValue;
+  e.bias = bias; e.Oh = (__bf16*)Oh; e.Ol = (__bf16*)Ol;
+  const long long tiles = (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+  if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)tiles);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (S) {
+#define TDQ_INF(S_) \
+  case S_: hipLaunchKernelGGL((lay_in_fwd_kernel<S_>), grid, dim3(256), 0, st, e, X, K0); break;
+    TDQ_INF(1) TDQ_INF(2) TDQ_INF(3) TDQ_INF(4) TDQ_INF(5) TDQ_INF(6) TDQ_INF(7) TDQ_INF(8)
+#undef TDQ_INF
+    default: return (int)hipErrorInvalidValue;
+  }
+  TDQ_CHECK_LAUNCH();
+  return 0;
+}
+
+// The last hidden layer's adjoint from the output layer (lay_out_bwd_kernel): dJ [S * Npts][d_out]
+// fp32, Ko [Nout][d_out]; mode EPI_BWD / EPI_BWD0 with the outputs of tdq_lay_nnj.
+int tdq_lay_out_bwd(int mode, int S, const int* spec, const float* dJ, int d_out, const float* Ko, const void* Hh,
+                    const void* Hl, int Npts, int Nout, void* Oh, void* Ol, float* part, const float* X, int d_in,
+                    void* stream) {
+  EpiArgs e;
+  if (!epi_args(e, S, spec, Npts, Nout, mode == EPI_BWD0 ? d_in : 0) || (mode != EPI_BWD && mode != EPI_BWD0) ||
+      d_out < 1 || d_out > TDQ_MAXO || dJ == nullptr || Ko == nullptr || Hh == nullptr || Hl == nullptr ||
+      (mode == EPI_BWD ? Oh == nullptr : (part == nullptr || X == nullptr || d_in < 1)) || !aligned8(Oh) ||
+      !aligned8(Ol) || !aligned8(Hh) || !aligned8(Hl))
+    return (int)hipErrorInvalidValue;
+  e.Hh = (const __bf16*)Hh; e.Hl = (const __bf16*)Hl; e.Oh = (__bf16*)Oh; e.Ol = (__bf16*)Ol;
+  e.part = part; e.X = X;
+  const long long tiles = (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+  if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)tiles);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (S) {
+#define TDQ_OB(S_)                                                                                          \
+  case S_:                                                                                                  \
+    if (mode == EPI_BWD) hipLaunchKernelGGL((lay_out_bwd_kernel<S_, EPI_BWD>), grid, dim3(256), 0, st, e, dJ, Ko, d_out); \
+    else hipLaunchKernelGGL((lay_out_bwd_kernel<S_, EPI_BWD0>), grid, dim3(256), 0, st, e, dJ, Ko, d_out);   \
+    break;
+    TDQ_OB(1) TDQ_OB(2) TDQ_OB(3) TDQ_OB(4) TDQ_OB(5) TDQ_OB(6) TDQ_OB(7) TDQ_OB(8)
+#undef TDQ_OB
+    default: return (int)hipErrorInvalidValue;
+  }
   TDQ_CHECK_LAUNCH();
   return 0;
 }

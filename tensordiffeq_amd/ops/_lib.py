@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 _lock = threading.Lock()
 _lib = None
@@ -68,6 +68,10 @@ def _declare(lib):
         "tdq_lay_nn": (I, [I, P, P, L, P, P, L, P, L, I, I, I, P]),
         "tdq_lay_tn": (I, [I, P, P, L, P, P, L, P, I, I, I, I, P]),
         "tdq_lay_xtz": (I, [P, I, P, I, I, P, I, P]),
+        "tdq_lay_xtz2": (I, [P, I, P, P, P, I, I, P, I, P]),
+        "tdq_lay_nnj": (I, [I, I, I, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, I, P]),
+        "tdq_lay_in_fwd": (I, [I, P, P, I, P, P, I, I, P, P, P]),
+        "tdq_lay_out_bwd": (I, [I, I, P, P, I, P, P, P, I, I, P, P, P, P, I, P]),
         "tdq_adam_multi": (I, [P, I, P, P, P]),
         "tdq_step_book": (I, [P, P, I, I, P, L, P, P, P, P, P, I, P]),
         "tdq_best_track": (I, [P, P, P, P, P, P, L, P]),
@@ -79,7 +83,7 @@ def _declare(lib):
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
         "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P]),
-        "tdq_layered_epi": (I, [I, P, P, P, L, I, I, P, P, P, P]),
+        "tdq_layered_epi": (I, [I, P, P, P, L, I, I, P, P, P, P, P, P]),
         # high-order (<= 4) jets of small point sets (csrc/jet_hi.hip, ops/jet_hi.py)
         "tdq_jet_hi_scratch_floats": (L, [I, I]),
         "tdq_jet_hi_work_floats": (L, [I, I, P, I, I]),

@@ -6,13 +6,18 @@ whole layer stack, which bounds the hidden width at 128.  The reference accepts 
 
 * the S derivative streams of a layer are stacked into one ``[S*N, W]`` matrix, so every weight
   multiplication of a layer - forward ``Z = H K``, backward ``HB = ZB K^T`` and the weight gradient
-  ``dK = H^T ZB`` (reduction over all streams and points at once) - is ONE plain library GEMM
-  (hipBLASLt via ``torch.mm``) in the requested precision family: fp32, bf16 (operands rounded
-  once, fp32 output) or bf16x3 (hi/lo split, three bf16 GEMMs: hi*hi + hi*lo + lo*hi); every
-  activation / adjoint is converted once and reused by both GEMMs that read it;
-* the bias, the tanh jet (value, first-, second-order streams) and its adjoint run as one fused,
-  memory-bound HIP pass per layer (``tdq_layered_epi``), the adjoint from the saved
-  post-activations only (no tanh recompute).
+  ``dK = H^T ZB`` (reduction over all streams and points at once) - is ONE GEMM in the requested
+  precision family: fp32, bf16 (operands rounded once, fp32 accumulation) or bf16x3 (hi/lo split:
+  hi*hi + hi*lo + lo*hi).  On the GPU these are the hand-written MFMA kernels of
+  ``csrc/lay_gemm.hip`` (``TDQ_LAY_GEMM=0``: the library GEMMs through ``torch.mm``, the A/B
+  reference);
+* the bias, the tanh jet (value, first-, second-order streams) and its adjoint (``csrc/lay_jet.h``)
+  run in the EPILOGUE of the hidden layers' NN GEMMs in the bf16 families (``tdq_lay_nnj``: a
+  GEMM tile holds all S streams of its points, so the jet runs on the accumulators; the layer's
+  output leaves the kernel only as the next GEMMs' bf16 operands, whose hi + lo sum is also the
+  saved post-activation of the adjoint - no fp32 Z / H round trips through HBM).  The input layer,
+  the output layer's adjoint, fp32 and the library path use the standalone memory-bound epilogue
+  pass (``tdq_layered_epi``), the adjoint from the saved post-activations only (no tanh recompute).
 
 Orders <= 2 (like the fused kernels).  On CPU the same engine runs with torch epilogues (the
 numerics oracle of the HIP pass, tests/test_layered_jet.py).  Same contract as
@@ -172,7 +177,9 @@ def _mm_tn(a, b, out):
         bh, bl = _planes(b)
         L, Ma = ah.shape
         Nb = bh.shape[1]
-        rows = ((L + 63) // 64 + 31) // 32 * 32      # ~64 chunks, a multiple of 32 rows each
+        tiles = -(-Ma // 128) * -(-Nb // 128)
+        want = max(1, min(-(-1024 // tiles), -(-L // 256)))   # >= ~1024 workgroups, >= 256 rows each
+        rows = (-(-L // want) + 31) // 32 * 32                # a multiple of 32 rows per chunk
         nch = -(-L // rows)
         part = torch.empty((nch, Ma, Nb), dtype=torch.float32, device=x.device)
         lib = _lib.load(required=True)
@@ -206,10 +213,73 @@ def _mm_tn(a, b, out):
     return out
 
 
-def _epi(fwd, A, B, bias, spec, prec="fp32"):
-    """The fused epilogue pass in place on A; returns ``(A, op)`` with ``op`` the :class:`_Op` of
-    the result viewed ``[S*N, W]`` - in the bf16 families its hi (/ lo) copies are written by the
-    same pass instead of a separate conversion."""
+def _fused(X, ws, precision):
+    """The GEMM-epilogue path (the layer jet inside the hand-written kernels, bf16 families)."""
+    import os
+    return (X.is_cuda and precision in ("bf16", "bf16x3") and _hip_gemm() and X.shape[1] <= 8
+            and os.environ.get("TDQ_LAY_FUSED", "1") != "0" and all(K.shape[1] % 4 == 0 for K, _ in ws[:-1]))
+
+
+EPI_FWD, EPI_BWD, EPI_BWD0 = 0, 1, 2   # csrc/lay_gemm.hip lay_epilogue modes
+
+
+def _spec_c(spec):
+    return (ctypes.c_int * len(spec))(*spec)
+
+
+def _nnj(mode, prec, spec, S, N, a, bt, bias=None, H=None, part=None, X=None):
+    """One NN GEMM with the layer jet in its epilogue (csrc/lay_gemm.hip ``lay_nnj_kernel``): ``a``
+    the :class:`_Op` of the layer input planes [S*N, K], ``bt`` the fp32 B^T [Nout, K].  Returns the
+    (hi, lo) bf16 output planes: EPI_FWD the layer's post-activations (lo always - it is the saved
+    activation's residual), EPI_BWD its ZB (lo in bf16x3 only; ``part`` the bias partials),
+    EPI_BWD0 nothing (``part`` the input layer's gradient partials, ``X`` its coordinates)."""
+    ah, al = _planes(a)
+    bo = _Op(bt.contiguous(), prec)
+    bh, bl = _planes(bo)
+    Nout, K = bt.shape
+    dev = ah.device
+    oh = ol = None
+    if mode != EPI_BWD0:
+        oh = torch.empty((S * N, Nout), dtype=torch.bfloat16, device=dev)
+        if mode == EPI_FWD or prec == "bf16x3":
+            ol = torch.empty_like(oh)
+    hh, hl = H if H is not None else (None, None)
+    lib = _lib.load(required=True)
+    rc = lib.tdq_lay_nnj(_PREC[prec], mode, S, _spec_c(spec), _lib.ptr(ah), _lib.ptr(al), _lib.ptr(bh), _lib.ptr(bl),
+                         N, K, Nout, _lib.ptr(bias), _lib.ptr(hh), _lib.ptr(hl), _lib.ptr(oh), _lib.ptr(ol),
+                         _lib.ptr(part), _lib.ptr(X), 0 if X is None else X.shape[1], _lib.stream_ptr(dev))
+    _lib.check(rc, "tdq_lay_nnj")
+    return oh, ol
+
+
+def _parts(S, N, W, q, dev):
+    """Per-tile partials of a jet epilogue: one row per tile row (128 // S points) x q x W."""
+    return torch.empty((-(-N // (128 // S)), q, W), dtype=torch.float32, device=dev)
+
+
+def _xtz(Xm, out, Z=None, H=None, rows=32):
+    """``out[f][j] = sum_n X[n][j] Z[n][f]`` (``out`` [W, d], may be a transposed view) for fp32
+    ``Xm`` [R, d] and Z [R, W] (fp32, or the (hi, lo) bf16 planes ``H``): chunked partials of the
+    FMA kernel (csrc/lay_gemm.hip ``lay_xtz_kernel``, <= 8 columns per launch), fixed-order sum."""
+    lib = _lib.load(required=True)
+    R = Xm.shape[0]
+    W = out.shape[0]
+    zh, zl = H if H is not None else (None, None)
+    for j0 in range(0, Xm.shape[1], 8):
+        xj = Xm[:, j0:j0 + 8].contiguous()
+        part = torch.empty((-(-R // rows), xj.shape[1], W), dtype=torch.float32, device=Xm.device)
+        _lib.check(lib.tdq_lay_xtz2(_lib.ptr(xj), xj.shape[1], _lib.ptr(Z), _lib.ptr(zh), _lib.ptr(zl), R, W,
+                                    _lib.ptr(part), rows, _lib.stream_ptr(Xm.device)), "tdq_lay_xtz2")
+        out[:, j0:j0 + xj.shape[1]].copy_(part.sum(dim=0).t())
+    return out
+
+
+def _epi(fwd, A, B, bias, spec, prec="fp32", keep_lo=False, H=None):
+    """The standalone epilogue pass in place on A; returns ``(A, op)`` with ``op`` the :class:`_Op`
+    of the result viewed ``[S*N, W]`` - in the bf16 families its hi (/ lo) copies are written by
+    the same pass instead of a separate conversion (``keep_lo``: the lo plane in bf16 too, the
+    post-activation residual of the GEMM-epilogue path; then ``op.l_saved`` holds it).  Backward
+    with ``B=None``: the post-activations come as the (hi, lo) bf16 planes ``H``."""
     S, N, W = A.shape
     if A.is_cuda:
         lib = _lib.load(required=True)
@@ -217,13 +287,19 @@ def _epi(fwd, A, B, bias, spec, prec="fp32"):
         hi = lo = None
         if prec in ("bf16", "bf16x3"):
             hi = torch.empty((S * N, W), dtype=torch.bfloat16, device=A.device)
-            if prec == "bf16x3":
+            if prec == "bf16x3" or keep_lo:
                 lo = torch.empty_like(hi)
+        hh, hl = H if H is not None else (None, None)
         rc = lib.tdq_layered_epi(1 if fwd else 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(bias), N, W, S, c,
-                                 _lib.ptr(hi), _lib.ptr(lo), _lib.stream_ptr(A.device))
+                                 _lib.ptr(hi), _lib.ptr(lo), _lib.ptr(hh), _lib.ptr(hl), _lib.stream_ptr(A.device))
         _lib.check(rc, "tdq_layered_epi")
-        op = _Op.parts(prec, hi, lo) if hi is not None else _Op(A.view(S * N, W), prec)
+        if hi is None:
+            return A, _Op(A.view(S * N, W), prec)
+        op = _Op.parts(prec, hi, lo if prec == "bf16x3" else None)
+        op.l_saved = lo
         return A, op
+    if H is not None:
+        B = (H[0].float() + H[1].float()).view(S, N, W)
     A = _epi_fwd_torch(A, bias, spec) if fwd else _epi_bwd_torch(A, B, spec)
     return A, _Op(A.view(S * N, W), prec)
 
@@ -235,8 +311,27 @@ def forward_raw(X, P, net, plan, precision="fp32"):
     spec = _spec(plan)
     ws = net.weights(P)
     S, N = plan.S, X.shape[0]
+    fused = _fused(X, ws, precision)
     K0, b0 = ws[0]
     W0 = K0.shape[1]
+    if fused:
+        # input layer: X K0 (d_in exact fp32 FMAs) + jet in one pass, the hidden layers' NN GEMMs with
+        # the jet in their epilogues; activations only as (hi, lo) bf16 planes
+        hi = torch.empty((S * N, W0), dtype=torch.bfloat16, device=X.device)
+        lo = torch.empty_like(hi)
+        lib = _lib.load(required=True)
+        _lib.check(lib.tdq_lay_in_fwd(S, _spec_c(spec), _lib.ptr(X), X.shape[1], _lib.ptr(K0.contiguous()),
+                                      _lib.ptr(b0.contiguous()), N, W0, _lib.ptr(hi), _lib.ptr(lo),
+                                      _lib.stream_ptr(X.device)), "tdq_lay_in_fwd")
+        Hs, Ho = [(hi, lo)], [_Op.parts(precision, hi, lo if precision == "bf16x3" else None)]
+        for K, b in ws[1:-1]:
+            hi, lo = _nnj(EPI_FWD, precision, spec, S, N, Ho[-1], K.t(), bias=b)
+            Hs.append((hi, lo))
+            Ho.append(_Op.parts(precision, hi, lo if precision == "bf16x3" else None))
+        Ko, bo = ws[-1]
+        J = _mm_w(Ho[-1], Ko, precision).view(S, N, Ko.shape[1])
+        J[0] += bo
+        return J, ("layered", X, P, net, spec, Hs, Ho, precision, fused)
     Z = torch.zeros((S, N, W0), dtype=P.dtype, device=X.device)
     if X.is_cuda:   # layer 0: the input is exact fp32, d_in <= 8 columns - FMAs, not a GEMM
         torch.mul(X[:, :1], K0[0], out=Z[0])
@@ -257,13 +352,13 @@ def forward_raw(X, P, net, plan, precision="fp32"):
     Ko, bo = ws[-1]
     J = _mm_w(Ho[-1], Ko, precision).view(S, N, Ko.shape[1])
     J[0] += bo
-    return J, ("layered", X, P, net, spec, Hs, Ho, precision)
+    return J, ("layered", X, P, net, spec, Hs, Ho, precision, fused)
 
 
 @torch.no_grad()
 def backward_raw(saved, dJ, grad=None):
     """Flat parameter gradient of ``<dJ, J>`` (Keras layer order, like the fused kernels)."""
-    _, X, P, net, spec, Hs, Ho, prec = saved
+    _, X, P, net, spec, Hs, Ho, prec, fused = saved
     if grad is None:
         grad = torch.empty_like(P)
     gw = net.weights(grad)
@@ -272,36 +367,83 @@ def backward_raw(saved, dJ, grad=None):
     dJ = dJ.contiguous()
     Ko, _ = ws[-1]
     dJo = _Op(dJ.view(S * N, dJ.shape[2]), prec)
-    _mm_tn(Ho[-1], dJo, gw[-1][0])
-    torch.sum(dJ[0], dim=0, out=gw[-1][1])
-    if dJ.shape[2] == 1:  # an outer product: a K = 1 GEMM ran 10x slower than this broadcast
-        HB = (dJ.view(S * N, 1) * Ko.view(1, -1)).view(S, N, Ko.shape[0])
+    last = len(ws) - 2
+    if fused and dJ.shape[2] <= 64:   # dKo = H^T dJ, a few columns: FMA partials on exact dJ, H = hi + lo
+        _xtz(dJ.view(S * N, dJ.shape[2]), gw[-1][0], H=Hs[last], rows=64)
     else:
-        HB = _mm_bt(dJo, Ko, prec).view(S, N, Ko.shape[0])
-    for i in range(len(ws) - 2, 0, -1):
-        K, _ = ws[i]
-        ZB, ZBo = _epi(False, HB, Hs[i], None, spec, prec)
-        _mm_tn(Ho[i - 1], ZBo, gw[i][0])
-        torch.sum(ZB[0], dim=0, out=gw[i][1])
-        # HB = ZB K^T: K itself is the transposed operand [W_in, W_out] of the NN GEMM (library path:
-        # K^T materialized - its transposed-B kernels ran ~4x slower, profiles/r3_ag_*)
-        HB = _mm_bt(ZBo, K, prec).view(S, N, K.shape[0])
-    ZB0, _ = _epi(False, HB, Hs[0], None, spec)
-    dK0, db0 = gw[0]
-    if X.is_cuda and _hip_gemm():   # X^T ZB0: d_in rows of exact fp32 - chunked FMA partials
-        rows = 32   # many short row chunks: the kernel is latency-bound (one 16-byte Z load per row)
+        _mm_tn(Ho[-1], dJo, gw[-1][0])
+    torch.sum(dJ[0], dim=0, out=gw[-1][1])
+    HB = None
+    if not fused or dJ.shape[2] > 4:   # (the fused path forms HB = dJ Ko^T inside lay_out_bwd_kernel)
+        if dJ.shape[2] == 1:  # an outer product: a K = 1 GEMM ran 10x slower than this broadcast
+            HB = (dJ.view(S * N, 1) * Ko.view(1, -1)).view(S, N, Ko.shape[0])
+        else:
+            HB = _mm_bt(dJo, Ko, prec).view(S, N, Ko.shape[0])
+    part0 = ZB0 = None
+    if fused:
+        d_in, d_out = X.shape[1], dJ.shape[2]
         lib = _lib.load(required=True)
-        z0 = ZB0[0].contiguous()
-        for j0 in range(0, X.shape[1], 8):   # (the kernel takes up to 8 input columns per launch)
-            xj = X[:, j0:j0 + 8].contiguous()
-            part = torch.empty((-(-N // rows), xj.shape[1], dK0.shape[1]), dtype=torch.float32, device=X.device)
-            _lib.check(lib.tdq_lay_xtz(_lib.ptr(xj), xj.shape[1], _lib.ptr(z0), N, z0.shape[1], _lib.ptr(part), rows,
-                                       _lib.stream_ptr(X.device)), "tdq_lay_xtz")
-            torch.sum(part, dim=0, out=dK0[j0:j0 + xj.shape[1]])
+        W = Ko.shape[0]
+        ZBo = db = None
+        if d_out <= 4:   # the last hidden layer's adjoint with HB = dJ Ko^T formed in the kernel
+            mode = EPI_BWD if last > 0 else EPI_BWD0
+            oh = ol = None
+            if last > 0:
+                db = _parts(S, N, W, 1, X.device)
+                oh = torch.empty((S * N, W), dtype=torch.bfloat16, device=X.device)
+                ol = torch.empty_like(oh) if prec == "bf16x3" else None
+            else:
+                part0 = db = _parts(S, N, W, S + d_in, X.device)
+            _lib.check(lib.tdq_lay_out_bwd(mode, S, _spec_c(spec), _lib.ptr(dJ), d_out, _lib.ptr(Ko.contiguous()),
+                                           _lib.ptr(Hs[last][0]), _lib.ptr(Hs[last][1]), N, W, _lib.ptr(oh),
+                                           _lib.ptr(ol), _lib.ptr(db), _lib.ptr(X if last == 0 else None),
+                                           d_in, _lib.stream_ptr(X.device)), "tdq_lay_out_bwd")
+            if last > 0:
+                ZBo = _Op.parts(prec, oh, ol)
+        else:            # (wide outputs: HB from the NN GEMM, then the standalone pass)
+            ZB, ZBo = _epi(False, HB, None, None, spec, prec if last > 0 else "fp32", H=Hs[last])
+            db = ZB[0].unsqueeze(0)
+            if last == 0:
+                ZB0 = ZB
+        for i in range(last, 0, -1):
+            K, _ = ws[i]
+            _mm_tn(Ho[i - 1], ZBo, gw[i][0])
+            torch.sum(db.reshape(-1, db.shape[-1]), dim=0, out=gw[i][1])
+            # HB_{i-1} = ZB_i K_i^T with layer i-1's adjoint jet in the GEMM epilogue (K is the B^T
+            # operand); the input layer's comes out as gradient partials only
+            W = K.shape[0]
+            if i - 1 > 0:
+                db = _parts(S, N, W, 1, X.device)
+                hi, lo = _nnj(EPI_BWD, prec, spec, S, N, ZBo, K, H=Hs[i - 1], part=db)
+                ZBo = _Op.parts(prec, hi, lo)
+            else:
+                part0 = _parts(S, N, W, S + d_in, X.device)
+                _nnj(EPI_BWD0, prec, spec, S, N, ZBo, K, H=Hs[0], part=part0, X=X)
+    dK0, gb0 = gw[0]
+    if part0 is not None:
+        tot = part0.sum(dim=0)                       # [S + d_in, W0]: stream sums, then X^T zb
+        dK0.copy_(tot[S:])
+        for s in range(1, S):
+            if spec[3 * s] == 1:
+                dK0[spec[3 * s + 1]] += tot[s]
+        gb0.copy_(tot[0])
+        return grad
+    if ZB0 is None:
+        for i in range(last, 0, -1):
+            K, _ = ws[i]
+            ZB, ZBo = _epi(False, HB, Hs[i], None, spec, prec)
+            _mm_tn(Ho[i - 1], ZBo, gw[i][0])
+            torch.sum(ZB[0], dim=0, out=gw[i][1])
+            # HB = ZB K^T: K itself is the transposed operand [W_in, W_out] of the NN GEMM (library path:
+            # K^T materialized - its transposed-B kernels ran ~4x slower, profiles/r3_ag_*)
+            HB = _mm_bt(ZBo, K, prec).view(S, N, K.shape[0])
+        ZB0, _ = _epi(False, HB, Hs[0], None, spec)
+    if X.is_cuda and _hip_gemm():   # X^T ZB0: d_in rows of exact fp32 - chunked FMA partials
+        _xtz(X, dK0.t(), Z=ZB0[0].contiguous())
     else:
         torch.mm(X.t(), ZB0[0], out=dK0)
     for s in range(1, S):
         if spec[3 * s] == 1:
             dK0[spec[3 * s + 1]] += ZB0[s].sum(dim=0)
-    torch.sum(ZB0[0], dim=0, out=db0)
+    torch.sum(ZB0[0], dim=0, out=gb0)
     return grad

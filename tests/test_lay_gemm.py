@@ -59,3 +59,51 @@ def test_layer0_xtz_matches_fp64():
     out = part.sum(0)
     ref = X.double().t() @ Z.double()
     assert ((out.double() - ref).norm() / ref.norm()).item() < 1e-6
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("sizes,reqs,N", [
+    ([2, 256, 256, 256, 1], [(0,), (1,), (0, 0)], 1000),
+    ([3, 132, 64, 1], [(0,), (1,), (2,), (0, 0), (1, 1), (0, 1)], 333),   # S = 7: 18-point tiles
+    ([2, 512, 512, 1], [(0,), (1,)], 130),                              # S = 3: 42-point tiles
+    ([2, 96, 1], [(0, 0)], 77),                                         # one hidden layer
+])
+def test_gemm_epilogue_path_matches_standalone_pass(sizes, reqs, N, prec, monkeypatch):
+    """The GEMM-epilogue path (the layer jet inside tdq_lay_in_fwd / tdq_lay_nnj / tdq_lay_out_bwd,
+    activations kept only as hi / lo bf16 planes, the input layer's gradient as tile partials)
+    against the GEMM + standalone epilogue pass, both compared to the float64 jet + autograd: the
+    epilogue path is no less accurate, and within 1e-5 of the standalone path in bf16x3.  (Not
+    bitwise: the input layer's X K0 is summed in another order, the adjoint reads H = hi + lo -
+    relative 2^-16 - and the output layer's dKo comes from exact-fp32 FMA partials.)"""
+    from tensordiffeq_amd.jet import JetPlan, jet_forward
+    from tensordiffeq_amd.models.networks import TanhMLP
+    from tensordiffeq_amd.ops import jet_layered
+    torch.manual_seed(3)
+    net = TanhMLP(sizes, device="cuda")
+    with torch.no_grad():
+        net.flat.add_(0.05 * torch.randn_like(net.flat))
+    X = torch.rand(N, sizes[0], device="cuda") * 2 - 1
+    plan = JetPlan(reqs, sizes[0])
+    P = net.flat.detach()
+    G = torch.randn(plan.S, N, sizes[-1], device="cuda")
+    p64 = P.double().clone().requires_grad_(True)
+    Jr = jet_forward(X.double(), net.weights(p64), plan)
+    (Jr * G.double()).sum().backward()
+    gr, Jr = p64.grad, Jr.detach()
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TDQ_LAY_FUSED", fused)
+        J, saved = jet_layered.forward_raw(X, P, net, plan, prec)
+        assert saved[-1] == (fused == "1")
+        out[fused] = (J.clone(), jet_layered.backward_raw(saved, G).double())
+    (J1, g1), (J0, g0) = out["1"], out["0"]
+    scale = Jr.abs().amax(dim=(1, 2), keepdim=True).clamp_min(1e-3)
+    f1, f0 = (((J.double() - Jr).abs() / scale).max().item() for J in (J1, J0))
+    e1, e0 = ((g1 - gr).norm() / gr.norm()).item(), ((g0 - gr).norm() / gr.norm()).item()
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    print(f"LAY_NNJ {prec} {sizes} S={plan.S} vs fp64: fwd {f1:.2e} (standalone {f0:.2e}), grad {e1:.2e} "
+          f"(standalone {e0:.2e}); grads between {rel:.2e}")
+    assert f1 <= 1.2 * f0 + 1e-6, (f1, f0)
+    assert e1 <= 1.1 * e0 + 1e-6, (e1, e0)
+    if prec == "bf16x3":
+        assert rel < 1e-5, rel

@@ -10,9 +10,10 @@ timeout -k 10 400 python -u -m pytest tests/test_lay_gemm.py tests/test_layered_
 grep -E "LAY_|KERNEL_ERR|passed" $O/pytest.log | cut -c1-200
 for cfg in "bf16:2,512,512,512,512,1" "bf16x3:2,256,256,256,256,1"; do
   pr=${cfg%%:*}; ly=${cfg#*:}
-  for g in 1 0; do
-    TDQ_LAY_GEMM=$g timeout -k 10 300 python bench.py --steps 40 --warmup 5 --no-l2 --precision $pr --layers $ly > $O/b_${pr}_$g.json 2>> $O/err.log || { tail -20 $O/err.log; exit 1; }
-    python -c "import json;d=json.loads(open('$O/b_${pr}_$g.json').read().splitlines()[-1]);print('$pr $ly LAY_GEMM=$g', round(d['ms_per_step'],4))"
+  for gf in 1:1 1:0 0:0; do
+    g=${gf%%:*}; f=${gf#*:}
+    TDQ_LAY_GEMM=$g TDQ_LAY_FUSED=$f timeout -k 10 300 python bench.py --steps 40 --warmup 5 --no-l2 --precision $pr --layers $ly > $O/b_${pr}_$g$f.json 2>> $O/err.log || { tail -20 $O/err.log; exit 1; }
+    python -c "import json;d=json.loads(open('$O/b_${pr}_$g$f.json').read().splitlines()[-1]);print('$pr $ly LAY_GEMM=$g LAY_FUSED=$f', round(d['ms_per_step'],4))"
   done
 done
 cd /tmp && export TMPDIR=/tmp
