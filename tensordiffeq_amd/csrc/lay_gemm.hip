@@ -276,6 +276,42 @@ __device__ __forceinline__ bf16x8 ldr8(const __bf16* __restrict__ base, long lon
   return r;
 }
 
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+// 8 fp32 at element offset off + k of a row (zero when !ok or past K)
+__device__ __forceinline__ f32x8 ldr8(const float* __restrict__ base, long long off, bool ok, int k, int K, bool vec) {
+  f32x8 r;
+  if (ok) {
+    const float* p = base + off + k;
+    if (vec && k + 8 <= K) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r[j] = x0[j];
+        r[4 + j] = x1[j];
+      }
+      return r;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (k + j < K) ? p[j] : 0.f;
+    return r;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = 0.f;
+  return r;
+}
+
+template <class T>
+struct Vec8;
+template <>
+struct Vec8<__bf16> {
+  using V = bf16x8;
+};
+template <>
+struct Vec8<float> {
+  using V = f32x8;
+};
+
 // 8 bf16 of (row, k..k+7) of a row-major [nrows][ld] matrix, zero outside
 __device__ __forceinline__ bf16x8 ldg8(const __bf16* __restrict__ base, long long ld, int row, int nrows, int k, int K,
                                        bool vec) {
@@ -283,18 +319,22 @@ __device__ __forceinline__ bf16x8 ldg8(const __bf16* __restrict__ base, long lon
 }
 
 // k-depth of a staged step: 64 in bf16 (fewer barriers per MFMA), 32 in bf16x3 (two planes per
-// operand - the 64-deep double buffer would need 144 KB of LDS, one workgroup per CU)
+// operand - the 64-deep double buffer would need 144 KB of LDS, one workgroup per CU) and fp32
 template <int P>
 constexpr int nn_bk() {
-  return P == 1 ? 32 : 64;
+  return P == 0 ? 64 : 32;
+}
+template <int P>
+constexpr int nn_lk() {  // LDS row stride (elements): 40 / 72 bf16, 36 fp32 - conflict-free fragment reads
+  return nn_bk<P>() + (P == 2 ? 4 : 8);
 }
 template <int P>
 constexpr int nn_rows_per_thread() {  // rows of the 128-row tiles one thread stages (8 k-values each)
   return 128 * (nn_bk<P>() / 8) / 256;
 }
 template <int P>
-constexpr int nn_stage_bytes() {  // {A, B} x 2 buffers x planes x 128 rows x (BK + 8) bf16
-  return 2 * 2 * (P == 1 ? 2 : 1) * 128 * (nn_bk<P>() + 8) * 2;
+constexpr int nn_stage_bytes() {  // {A, B} x 2 buffers x planes x 128 rows x LK elements
+  return 2 * 2 * (P == 1 ? 2 : 1) * 128 * nn_lk<P>() * (P == 2 ? 4 : 2);
 }
 
 // the A and B rows a thread stages (element offsets of row starts, validity): row c is tile row
@@ -310,21 +350,25 @@ __device__ __forceinline__ int nn_row(int c) {
 }
 
 // The main loop of a 128 x 128 tile: acc[i][j] = the wave's (i, j) 16 x 16 block of A B over K.
-// LDS rows of BK k-values padded by 8 (row strides of 40 / 72 bf16: the 16 rows of a fragment read
-// land on distinct banks).
+// bf16 families: one v_mfma_f32_16x16x32_bf16 per block and 32-deep substep (x3 in bf16x3); fp32:
+// eight v_mfma_f32_16x16x4_f32 on the same 8-value fragments (MFMA kk takes k = 8 g + kk of lane
+// group g in both operands, so the permuted order sums the same products).
 template <int P>
-__device__ __forceinline__ void nn_loop(__bf16* smem, const __bf16* __restrict__ Ah, const __bf16* __restrict__ Al,
-                                        const __bf16* __restrict__ Bh, const __bf16* __restrict__ Bl,
-                                        const NnRows& R, int K, bool v, f32x4 (&acc)[4][4]) {
+__device__ __forceinline__ void nn_loop(typename Op<P>::T* smem, const typename Op<P>::T* __restrict__ Ah,
+                                        const typename Op<P>::T* __restrict__ Al,
+                                        const typename Op<P>::T* __restrict__ Bh,
+                                        const typename Op<P>::T* __restrict__ Bl, const NnRows& R, int K, bool v,
+                                        f32x4 (&acc)[4][4]) {
+  using V = typename Vec8<typename Op<P>::T>::V;
   constexpr int NB = P == 1 ? 2 : 1;
-  constexpr int BK = nn_bk<P>(), LK = BK + 8, NR = nn_rows_per_thread<P>(), CPR = BK / 8;
+  constexpr int BK = nn_bk<P>(), LK = nn_lk<P>(), NR = nn_rows_per_thread<P>(), CPR = BK / 8;
   constexpr int SZ = 128 * LK;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, p = l & 15, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
   const int sk = (tid % CPR) * 8;
   auto sA = [&](int buf, int b) { return smem + (buf * NB + b) * SZ; };
   auto sB = [&](int buf, int b) { return smem + (2 * NB + buf * NB + b) * SZ; };
-  bf16x8 ra[NR][NB], rb[NR][NB];
+  V ra[NR][NB], rb[NR][NB];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int b = 0; b < NB; ++b)
@@ -340,8 +384,8 @@ __device__ __forceinline__ void nn_loop(__bf16* smem, const __bf16* __restrict__
 #pragma unroll
       for (int c = 0; c < NR; ++c) {
         const int r = nn_row<P>(c);
-        *reinterpret_cast<bf16x8*>(sA(buf, b) + r * LK + sk) = ra[c][b];
-        *reinterpret_cast<bf16x8*>(sB(buf, b) + r * LK + sk) = rb[c][b];
+        *reinterpret_cast<V*>(sA(buf, b) + r * LK + sk) = ra[c][b];
+        *reinterpret_cast<V*>(sB(buf, b) + r * LK + sk) = rb[c][b];
       }
   };
 #pragma unroll
@@ -357,23 +401,29 @@ __device__ __forceinline__ void nn_loop(__bf16* smem, const __bf16* __restrict__
     if (more) gload(k0 + BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
-      bf16x8 a[4][NB], b[4][NB];
+      V a[4][NB], b[4][NB];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          a[i][q] = *reinterpret_cast<const bf16x8*>(sA(buf, q) + (wm * 64 + 16 * i + p) * LK + kk + 8 * g);
-          b[i][q] = *reinterpret_cast<const bf16x8*>(sB(buf, q) + (wn * 64 + 16 * i + p) * LK + kk + 8 * g);
+          a[i][q] = *reinterpret_cast<const V*>(sA(buf, q) + (wm * 64 + 16 * i + p) * LK + kk + 8 * g);
+          b[i][q] = *reinterpret_cast<const V*>(sB(buf, q) + (wn * 64 + 16 * i + p) * LK + kk + 8 * g);
         }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if constexpr (P == 1) {
-            acc[i][j] = mfma_bf(a[i][1], b[j][0], acc[i][j]);
-            acc[i][j] = mfma_bf(a[i][0], b[j][1], acc[i][j]);
+          if constexpr (P == 2) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][0][e], b[j][0][e], acc[i][j], 0, 0, 0);
+          } else {
+            if constexpr (P == 1) {
+              acc[i][j] = mfma_bf(a[i][1], b[j][0], acc[i][j]);
+              acc[i][j] = mfma_bf(a[i][0], b[j][1], acc[i][j]);
+            }
+            acc[i][j] = mfma_bf(a[i][0], b[j][0], acc[i][j]);
           }
-          acc[i][j] = mfma_bf(a[i][0], b[j][0], acc[i][j]);
         }
     }
     if (more) {
@@ -397,7 +447,7 @@ __global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__
                                                       const __bf16* __restrict__ Bl, long long ldb,
                                                       float* __restrict__ C, long long ldc, int M, int N, int K,
                                                       int vec) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[nn_stage_bytes<P>() / 2];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[nn_stage_bytes<P>() / 2];  // (bf16 families only)
   const int gx = (N + 127) / 128;
   const int T = xcd_tile(blockIdx.x, gridDim.x);
   const int m0 = (T / gx) * 128, n0 = (T % gx) * 128;
@@ -447,6 +497,8 @@ struct EpiArgs {
   const float* bias;         // EPI_FWD: [Nout]
   const __bf16 *Hh, *Hl;     // EPI_BWD*: the layer's saved post-activations [S * Npts][Nout]
   __bf16 *Oh, *Ol;           // EPI_FWD / EPI_BWD outputs [S * Npts][Nout] (Ol nullable in EPI_BWD)
+  const float* H32;          // fp32 engine (F32): the saved post-activations, one fp32 plane
+  float* O32;                // fp32 engine: the output plane
   float* part;               // EPI_BWD* partials (nullable in EPI_BWD)
   const float* X;            // EPI_BWD0: [Npts][d_in]
   LSpec sp;
@@ -454,8 +506,9 @@ struct EpiArgs {
 
 // src(s, t) -> the f32x4 input (Z or HB) of stream s, tile point t, this thread's feature quad.
 // red: LDS scratch of 4 x (S + TDQ_MAXD) x 128 floats (may alias the source tile: a barrier
-// precedes its first write).  Every thread of the block must call this.
-template <int S, int MODE, class Src>
+// precedes its first write).  Every thread of the block must call this.  F32: the fp32 engine -
+// activations / adjoints are single fp32 planes (H32 / O32) instead of bf16 hi / lo pairs.
+template <int S, int MODE, bool F32, class Src>
 __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, Src src, float* red) {
   constexpr int PT = 128 / S;
   constexpr int NS = MODE == EPI_BWD0 ? S : 1;
@@ -492,9 +545,15 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const long long o = ((long long)s * e.Npts + n) * e.Nout + col;
-        const bf16x4 hh = *reinterpret_cast<const bf16x4*>(e.Hh + o), hl = *reinterpret_cast<const bf16x4*>(e.Hl + o);
+        if constexpr (F32) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(e.H32 + o);
 #pragma unroll
-        for (int v = 0; v < 4; ++v) h[s][v] = (float)hh[v] + (float)hl[v];
+          for (int v = 0; v < 4; ++v) h[s][v] = q[v];
+        } else {
+          const bf16x4 hh = *reinterpret_cast<const bf16x4*>(e.Hh + o), hl = *reinterpret_cast<const bf16x4*>(e.Hl + o);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) h[s][v] = (float)hh[v] + (float)hl[v];
+        }
       }
       lay_jet_bwd<S, 4>(h, x, e.sp, y);
 #pragma unroll
@@ -516,14 +575,18 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const long long o = ((long long)s * e.Npts + n) * e.Nout + col;
-        bf16x4 hv, lv;
+        if constexpr (F32) {
+          *reinterpret_cast<f32x4*>(e.O32 + o) = f32x4{y[s][0], y[s][1], y[s][2], y[s][3]};
+        } else {
+          bf16x4 hv, lv;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          hv[v] = (__bf16)y[s][v];
-          lv[v] = (__bf16)(y[s][v] - (float)hv[v]);
+          for (int v = 0; v < 4; ++v) {
+            hv[v] = (__bf16)y[s][v];
+            lv[v] = (__bf16)(y[s][v] - (float)hv[v]);
+          }
+          *reinterpret_cast<bf16x4*>(e.Oh + o) = hv;
+          if (e.Ol != nullptr) *reinterpret_cast<bf16x4*>(e.Ol + o) = lv;
         }
-        *reinterpret_cast<bf16x4*>(e.Oh + o) = hv;
-        if (e.Ol != nullptr) *reinterpret_cast<bf16x4*>(e.Ol + o) = lv;
       }
     }
   };
@@ -566,7 +629,7 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
 constexpr int EPI_CS = 132;  // LDS row stride of the fp32 tile: the 4 row groups of a store land 16 banks apart
 
 struct NnjArgs {
-  const __bf16 *Ah, *Al, *Bh, *Bl;  // A planes [S * Npts][K]; B^T [Nout][K]
+  const void *Ah, *Al, *Bh, *Bl;  // A planes [S * Npts][K]; B^T [Nout][K] (bf16, or fp32 when P == 2)
   int K, vec;
   EpiArgs e;
 };
@@ -577,7 +640,8 @@ __global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
   constexpr int STG = nn_stage_bytes<P>();
   constexpr int EPI = 128 * EPI_CS * 4;
   static_assert(4 * (TDQ_MAXS + TDQ_MAXD) * 128 * 4 <= EPI, "partials scratch fits the tile");
-  __shared__ __attribute__((aligned(16))) __bf16 smem[(STG > EPI ? STG : EPI) / 2];
+  using E = typename Op<P>::T;
+  __shared__ __attribute__((aligned(16))) E smem[(STG > EPI ? STG : EPI) / sizeof(E)];
   const int gx = (a.e.Nout + 127) / 128;
   const int T = xcd_tile(blockIdx.x, gridDim.x);
   const int ty = T / gx, n0 = (T % gx) * 128, pt0 = ty * PT;
@@ -593,7 +657,7 @@ __global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
     R.vb[c] = n0 + r < a.e.Nout;
   }
   f32x4 acc[4][4];
-  nn_loop<P>(smem, a.Ah, a.Al, a.Bh, a.Bl, R, a.K, a.vec != 0, acc);
+  nn_loop<P>(smem, (const E*)a.Ah, (const E*)a.Al, (const E*)a.Bh, (const E*)a.Bl, R, a.K, a.vec != 0, acc);
   __syncthreads();  // every wave is done with the staging buffers
   float* sC = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -604,14 +668,14 @@ __global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
       for (int r = 0; r < 4; ++r) sC[(wm * 64 + 16 * i + 4 * g + r) * EPI_CS + wn * 64 + 16 * j + p] = acc[i][j][r];
   __syncthreads();
   const int f4 = (tid & 31) * 4;
-  lay_epilogue<S, MODE>(a.e, ty, n0, [&](int s, int t) {
+  lay_epilogue<S, MODE, P == 2>(a.e, ty, n0, [&](int s, int t) {
     return *reinterpret_cast<const f32x4*>(&sC[(s * PT + t) * EPI_CS + f4]);
   }, sC);
 }
 
 // The input layer forward without a GEMM: Z = X K0 (d_in <= 8 exact fp32 columns), the first-order
 // streams' Z = the K0 row of their coordinate, second-order streams 0 - straight into the jet.
-template <int S>
+template <int S, bool F32>
 __global__ void __launch_bounds__(256) lay_in_fwd_kernel(EpiArgs e, const float* __restrict__ X,
                                                          const float* __restrict__ K0) {
   __shared__ float red[4];  // (EPI_FWD: no partials)
@@ -624,7 +688,7 @@ __global__ void __launch_bounds__(256) lay_in_fwd_kernel(EpiArgs e, const float*
   for (int j = 0; j < TDQ_MAXD; ++j)
 #pragma unroll
     for (int v = 0; v < 4; ++v) k[j][v] = (cok && j < e.d_in) ? K0[(long long)j * e.Nout + col + v] : 0.f;
-  lay_epilogue<S, EPI_FWD>(e, ty, n0, [&](int s, int t) {
+  lay_epilogue<S, EPI_FWD, F32>(e, ty, n0, [&](int s, int t) {
     f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s == 0) {
       const int n = pt0 + t;
@@ -650,7 +714,7 @@ __global__ void __launch_bounds__(256) lay_in_fwd_kernel(EpiArgs e, const float*
 // The last hidden layer's adjoint without materializing HB = dJ Ko^T (the output layer, d_out <= 4
 // columns): hb computed per (point, feature quad) from dJ and the thread's Ko rows.  MODE EPI_BWD,
 // or EPI_BWD0 when the last hidden layer is the input layer.
-template <int S, int MODE>
+template <int S, int MODE, bool F32>
 __global__ void __launch_bounds__(256) lay_out_bwd_kernel(EpiArgs e, const float* __restrict__ dJ,
                                                           const float* __restrict__ Ko, int d_out) {
   __shared__ __attribute__((aligned(16))) float red[4 * (TDQ_MAXS + TDQ_MAXD) * 128];
@@ -663,7 +727,7 @@ __global__ void __launch_bounds__(256) lay_out_bwd_kernel(EpiArgs e, const float
   for (int q = 0; q < TDQ_MAXO; ++q)
 #pragma unroll
     for (int v = 0; v < 4; ++v) ko[q][v] = (cok && q < d_out) ? Ko[(long long)(col + v) * d_out + q] : 0.f;
-  lay_epilogue<S, MODE>(e, ty, n0, [&](int s, int t) {
+  lay_epilogue<S, MODE, F32>(e, ty, n0, [&](int s, int t) {
     const float* dj = dJ + ((long long)s * e.Npts + pt0 + t) * d_out;
     f32x4 hb = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -891,67 +955,86 @@ int tdq_lay_xtz(const float* X, int d_in, const float* Z, int N, int W, float* C
 }
 
 // Host side of the layer-jet kernels: EpiArgs from the common arguments; false when invalid.
-static bool epi_args(EpiArgs& e, int S, const int* spec, int Npts, int Nout, int d_in) {
+// f32: the fp32 engine - Hh is the fp32 H plane and Oh the fp32 output plane (Hl / Ol unused).
+static bool epi_args(EpiArgs& e, int S, const int* spec, int Npts, int Nout, int d_in, bool f32, const void* Hh,
+                     const void* Hl, void* Oh, void* Ol) {
   if (Npts <= 0 || Nout <= 0 || Nout % 4 != 0 || d_in < 0 || d_in > TDQ_MAXD) return false;
   if (!lspec_parse(spec, S, e.sp)) return false;
   for (int s = 0; s < S; ++s)
     if (e.sp.stype[s] == 1 && (spec[3 * s + 1] < 0 || spec[3 * s + 1] >= TDQ_MAXD)) return false;
+  const uintptr_t al = f32 ? 15 : 7;  // 16-byte fp32 / 8-byte bf16 quads
+  if (((reinterpret_cast<uintptr_t>(Hh) | reinterpret_cast<uintptr_t>(Oh)) & al) != 0 ||
+      (!f32 && ((reinterpret_cast<uintptr_t>(Hl) | reinterpret_cast<uintptr_t>(Ol)) & 7) != 0))
+    return false;
   e.Npts = Npts;
   e.Nout = Nout;
   e.d_in = d_in;
   e.bias = nullptr;
-  e.Hh = e.Hl = nullptr;
-  e.Oh = e.Ol = nullptr;
   e.part = nullptr;
   e.X = nullptr;
+  e.Hh = f32 ? nullptr : (const __bf16*)Hh;
+  e.Hl = f32 ? nullptr : (const __bf16*)Hl;
+  e.Oh = f32 ? nullptr : (__bf16*)Oh;
+  e.Ol = f32 ? nullptr : (__bf16*)Ol;
+  e.H32 = f32 ? (const float*)Hh : nullptr;
+  e.O32 = f32 ? (float*)Oh : nullptr;
   return true;
 }
 
-static bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
+static long long epi_tiles(int S, int Npts, int Nout) {
+  return (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+}
 
-// mode: EPI_FWD (bias, Oh, Ol), EPI_BWD (Hh, Hl, Oh, Ol nullable, part nullable [tiles_y][1][Nout]),
-// EPI_BWD0 (Hh, Hl, part [tiles_y][S + d_in][Nout], X [Npts][d_in]); tiles_y = ceil(Npts / (128 / S)).
+// prec 0 bf16 / 1 bf16x3 / 2 fp32; mode: EPI_FWD (bias, Oh, Ol), EPI_BWD (Hh, Hl, Oh, Ol nullable,
+// part nullable [tiles_y][1][Nout]), EPI_BWD0 (Hh, Hl, part [tiles_y][S + d_in][Nout], X [Npts][d_in]);
+// tiles_y = ceil(Npts / (128 / S)).  fp32: A / B fp32, Hh / Oh single fp32 planes, Hl / Ol unused.
 // Planes are contiguous: A [S * Npts][K], B^T [Nout][K], H / outputs [S * Npts][Nout].
 int tdq_lay_nnj(int prec, int mode, int S, const int* spec, const void* Ah, const void* Al, const void* Bh,
                 const void* Bl, int Npts, int K, int Nout, const float* bias, const void* Hh, const void* Hl, void* Oh,
                 void* Ol, float* part, const float* X, int d_in, void* stream) {
   NnjArgs a;
-  if (!epi_args(a.e, S, spec, Npts, Nout, mode == EPI_BWD0 ? d_in : 0) || K <= 0 || prec < 0 || prec > 1 ||
-      (prec == 1 && (Al == nullptr || Bl == nullptr)) || Ah == nullptr || Bh == nullptr || mode < 0 || mode > 2)
+  const bool f32 = prec == 2;
+  if (prec < 0 || prec > 2 || mode < 0 || mode > 2 || K <= 0 || Ah == nullptr || Bh == nullptr ||
+      (prec == 1 && (Al == nullptr || Bl == nullptr)) ||
+      !epi_args(a.e, S, spec, Npts, Nout, mode == EPI_BWD0 ? d_in : 0, f32, Hh, Hl, Oh, Ol))
     return (int)hipErrorInvalidValue;
-  if (mode == EPI_FWD ? (bias == nullptr || Oh == nullptr || Ol == nullptr)
-                      : (Hh == nullptr || Hl == nullptr ||
+  if (mode == EPI_FWD ? (bias == nullptr || Oh == nullptr || (!f32 && Ol == nullptr))
+                      : (Hh == nullptr || (!f32 && Hl == nullptr) ||
                          (mode == EPI_BWD ? Oh == nullptr : (part == nullptr || X == nullptr || d_in < 1))))
     return (int)hipErrorInvalidValue;
-  if (!aligned8(Oh) || !aligned8(Ol) || !aligned8(Hh) || !aligned8(Hl)) return (int)hipErrorInvalidValue;
-  a.e.bias = bias; a.e.Hh = (const __bf16*)Hh; a.e.Hl = (const __bf16*)Hl;
-  a.e.Oh = (__bf16*)Oh; a.e.Ol = (__bf16*)Ol; a.e.part = part; a.e.X = X;
-  a.Ah = (const __bf16*)Ah; a.Al = (const __bf16*)Al; a.Bh = (const __bf16*)Bh; a.Bl = (const __bf16*)Bl;
+  a.e.bias = bias;
+  a.e.part = part;
+  a.e.X = X;
+  a.Ah = Ah; a.Al = Al; a.Bh = Bh; a.Bl = Bl;
   a.K = K;
-  a.vec = aligned16<__bf16>(Ah, K) && aligned16<__bf16>(Bh, K) &&
-          (prec == 0 || (aligned16<__bf16>(Al, K) && aligned16<__bf16>(Bl, K)));
-  const long long tiles = (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+  a.vec = f32 ? (aligned16<float>(Ah, K) && aligned16<float>(Bh, K))
+              : (aligned16<__bf16>(Ah, K) && aligned16<__bf16>(Bh, K) &&
+                 (prec == 0 || (aligned16<__bf16>(Al, K) && aligned16<__bf16>(Bl, K))));
+  const long long tiles = epi_tiles(S, Npts, Nout);
   if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)tiles);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define TDQ_NNJ_M(P_, S_, M_) hipLaunchKernelGGL((lay_nnj_kernel<P_, S_, M_>), grid, dim3(256), 0, st, a)
-#define TDQ_NNJ(P_, S_)                                 \
-  case S_:                                              \
-    if (mode == EPI_FWD) TDQ_NNJ_M(P_, S_, EPI_FWD);    \
+#define TDQ_NNJ(P_, S_)                                   \
+  case S_:                                                \
+    if (mode == EPI_FWD) TDQ_NNJ_M(P_, S_, EPI_FWD);      \
     else if (mode == EPI_BWD) TDQ_NNJ_M(P_, S_, EPI_BWD); \
-    else TDQ_NNJ_M(P_, S_, EPI_BWD0);                   \
+    else TDQ_NNJ_M(P_, S_, EPI_BWD0);                     \
     break;
-  if (prec == 0) {
-    switch (S) {
-      TDQ_NNJ(0, 1) TDQ_NNJ(0, 2) TDQ_NNJ(0, 3) TDQ_NNJ(0, 4) TDQ_NNJ(0, 5) TDQ_NNJ(0, 6) TDQ_NNJ(0, 7) TDQ_NNJ(0, 8)
-      default: return (int)hipErrorInvalidValue;
-    }
-  } else {
-    switch (S) {
-      TDQ_NNJ(1, 1) TDQ_NNJ(1, 2) TDQ_NNJ(1, 3) TDQ_NNJ(1, 4) TDQ_NNJ(1, 5) TDQ_NNJ(1, 6) TDQ_NNJ(1, 7) TDQ_NNJ(1, 8)
-      default: return (int)hipErrorInvalidValue;
-    }
+#define TDQ_NNJ_P(P_)                                                                                         \
+  switch (S) {                                                                                                \
+    TDQ_NNJ(P_, 1) TDQ_NNJ(P_, 2) TDQ_NNJ(P_, 3) TDQ_NNJ(P_, 4) TDQ_NNJ(P_, 5) TDQ_NNJ(P_, 6) TDQ_NNJ(P_, 7) \
+    TDQ_NNJ(P_, 8)                                                                                            \
+    default: return (int)hipErrorInvalidValue;                                                                \
   }
+  if (prec == 0) {
+    TDQ_NNJ_P(0)
+  } else if (prec == 1) {
+    TDQ_NNJ_P(1)
+  } else {
+    TDQ_NNJ_P(2)
+  }
+#undef TDQ_NNJ_P
 #undef TDQ_NNJ
 #undef TDQ_NNJ_M
   TDQ_CHECK_LAUNCH();
@@ -959,23 +1042,26 @@ int tdq_lay_nnj(int prec, int mode, int S, const int* spec, const void* Ah, cons
 }
 
 // The input layer forward (lay_in_fwd_kernel): X [Npts][d_in] fp32, K0 [d_in][Nout], bias [Nout] ->
-// the layer's post-activations as hi / lo bf16 planes [S * Npts][Nout].
-int tdq_lay_in_fwd(int S, const int* spec, const float* X, int d_in, const float* K0, const float* bias, int Npts,
-                   int Nout, void* Oh, void* Ol, void* stream) {
+// the layer's post-activations as hi / lo bf16 planes [S * Npts][Nout] (f32: one fp32 plane Oh).
+int tdq_lay_in_fwd(int f32, int S, const int* spec, const float* X, int d_in, const float* K0, const float* bias,
+                   int Npts, int Nout, void* Oh, void* Ol, void* stream) {
   EpiArgs e;
-  if (!epi_args(e, S, spec, Npts, Nout, d_in) || d_in < 1 || X == nullptr || K0 == nullptr || bias == nullptr ||
-      Oh == nullptr || Ol == nullptr || !aligned8(Oh) || !aligned8(Ol))
+  if (!epi_args(e, S, spec, Npts, Nout, d_in, f32 != 0, nullptr, nullptr, Oh, Ol) || d_in < 1 || X == nullptr ||
+      K0 == nullptr || bias == nullptr || Oh == nullptr || (!f32 && Ol == nullptr))
     return (int)hipErrorInvalidValue;
   for (int s = 0; s < S; ++s)
     if (e.sp.stype[s] == 1 && e.sp.coord[s] >= d_in) return (int)hipErrorInvalidValue;
-  e.bias = bias; e.Oh = (__bf16*)Oh; e.Ol = (__bf16*)Ol;
-  const long long tiles = (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+  e.bias = bias;
+  const long long tiles = epi_tiles(S, Npts, Nout);
   if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)tiles);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (S) {
-#define TDQ_INF(S_) \
-  case S_: hipLaunchKernelGGL((lay_in_fwd_kernel<S_>), grid, dim3(256), 0, st, e, X, K0); break;
+#define TDQ_INF(S_)                                                                                   \
+  case S_:                                                                                            \
+    if (f32) hipLaunchKernelGGL((lay_in_fwd_kernel<S_, true>), grid, dim3(256), 0, st, e, X, K0);   \
+    else hipLaunchKernelGGL((lay_in_fwd_kernel<S_, false>), grid, dim3(256), 0, st, e, X, K0);      \
+    break;
     TDQ_INF(1) TDQ_INF(2) TDQ_INF(3) TDQ_INF(4) TDQ_INF(5) TDQ_INF(6) TDQ_INF(7) TDQ_INF(8)
 #undef TDQ_INF
     default: return (int)hipErrorInvalidValue;
@@ -985,32 +1071,40 @@ int tdq_lay_in_fwd(int S, const int* spec, const float* X, int d_in, const float
 }
 
 // The last hidden layer's adjoint from the output layer (lay_out_bwd_kernel): dJ [S * Npts][d_out]
-// fp32, Ko [Nout][d_out]; mode EPI_BWD / EPI_BWD0 with the outputs of tdq_lay_nnj.
-int tdq_lay_out_bwd(int mode, int S, const int* spec, const float* dJ, int d_out, const float* Ko, const void* Hh,
-                    const void* Hl, int Npts, int Nout, void* Oh, void* Ol, float* part, const float* X, int d_in,
-                    void* stream) {
+// fp32, Ko [Nout][d_out]; mode EPI_BWD / EPI_BWD0 with the outputs of tdq_lay_nnj (f32: fp32 planes).
+int tdq_lay_out_bwd(int f32, int mode, int S, const int* spec, const float* dJ, int d_out, const float* Ko,
+                    const void* Hh, const void* Hl, int Npts, int Nout, void* Oh, void* Ol, float* part, const float* X,
+                    int d_in, void* stream) {
   EpiArgs e;
-  if (!epi_args(e, S, spec, Npts, Nout, mode == EPI_BWD0 ? d_in : 0) || (mode != EPI_BWD && mode != EPI_BWD0) ||
-      d_out < 1 || d_out > TDQ_MAXO || dJ == nullptr || Ko == nullptr || Hh == nullptr || Hl == nullptr ||
-      (mode == EPI_BWD ? Oh == nullptr : (part == nullptr || X == nullptr || d_in < 1)) || !aligned8(Oh) ||
-      !aligned8(Ol) || !aligned8(Hh) || !aligned8(Hl))
+  if ((mode != EPI_BWD && mode != EPI_BWD0) ||
+      !epi_args(e, S, spec, Npts, Nout, mode == EPI_BWD0 ? d_in : 0, f32 != 0, Hh, Hl, Oh, Ol) || d_out < 1 ||
+      d_out > TDQ_MAXO || dJ == nullptr || Ko == nullptr || Hh == nullptr || (!f32 && Hl == nullptr) ||
+      (mode == EPI_BWD ? Oh == nullptr : (part == nullptr || X == nullptr || d_in < 1)))
     return (int)hipErrorInvalidValue;
-  e.Hh = (const __bf16*)Hh; e.Hl = (const __bf16*)Hl; e.Oh = (__bf16*)Oh; e.Ol = (__bf16*)Ol;
-  e.part = part; e.X = X;
-  const long long tiles = (long long)((Nout + 127) / 128) * ((Npts + 128 / S - 1) / (128 / S));
+  e.part = part;
+  e.X = X;
+  const long long tiles = epi_tiles(S, Npts, Nout);
   if (tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)tiles);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  switch (S) {
-#define TDQ_OB(S_)                                                                                          \
-  case S_:                                                                                                  \
-    if (mode == EPI_BWD) hipLaunchKernelGGL((lay_out_bwd_kernel<S_, EPI_BWD>), grid, dim3(256), 0, st, e, dJ, Ko, d_out); \
-    else hipLaunchKernelGGL((lay_out_bwd_kernel<S_, EPI_BWD0>), grid, dim3(256), 0, st, e, dJ, Ko, d_out);   \
+#define TDQ_OB_L(S_, M_, F_) \
+  hipLaunchKernelGGL((lay_out_bwd_kernel<S_, M_, F_>), grid, dim3(256), 0, st, e, dJ, Ko, d_out)
+#define TDQ_OB(S_)                                         \
+  case S_:                                                 \
+    if (mode == EPI_BWD) {                                 \
+      if (f32) TDQ_OB_L(S_, EPI_BWD, true);                \
+      else TDQ_OB_L(S_, EPI_BWD, false);                   \
+    } else {                                               \
+      if (f32) TDQ_OB_L(S_, EPI_BWD0, true);               \
+      else TDQ_OB_L(S_, EPI_BWD0, false);                  \
+    }                                                      \
     break;
+  switch (S) {
     TDQ_OB(1) TDQ_OB(2) TDQ_OB(3) TDQ_OB(4) TDQ_OB(5) TDQ_OB(6) TDQ_OB(7) TDQ_OB(8)
-#undef TDQ_OB
     default: return (int)hipErrorInvalidValue;
   }
+#undef TDQ_OB
+#undef TDQ_OB_L
   TDQ_CHECK_LAUNCH();
   return 0;
 }

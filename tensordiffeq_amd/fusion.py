@@ -482,8 +482,51 @@ def _build(prog, lambdas):
     lam_ids = {k: i for i, k in enumerate(fl.lam_slots)}
     for gr, g in gs:
         gr.program = compile_graph(g, gr.outputs, stream_index, fl.n_streams, val_ids, lam_ids, scal_id)
+        gr.graph = g
         fl.groups.append(gr)
+    fl.compile_ctx = (stream_index, fl.n_streams, val_ids, lam_ids, scal_id)
     return fl
+
+
+def split_by_streams(fl, gr, n_lo):
+    """``(P_lo, P_hi)``: the group's outputs that read only J rows ``< n_lo`` (the main plan's
+    streams) and those that read only rows ``>= n_lo`` (a mixed program's high-order streams),
+    each compiled on its own - a term is a sum of per-output squares, so the two programs together
+    are the group's loss.  ``None`` when an output reads both kinds or one side is empty."""
+    g = getattr(gr, "graph", None)
+    ctx = getattr(fl, "compile_ctx", None)
+    if g is None or ctx is None:
+        return None
+    stream_index = ctx[0]
+
+    def rows(i):
+        seen, stack, out = set(), [i], set()
+        while stack:
+            j = stack.pop()
+            if j in seen:
+                continue
+            seen.add(j)
+            k = g.nodes[j]
+            if k[0] == "stream":
+                out.add(stream_index[k[2]])
+            elif k[0] in ("add", "sub", "mul", "div"):
+                stack += [k[1], k[2]]
+            elif k[0] in ("powi", "powf") or k[0] in UNARY:
+                stack.append(k[1])
+        return out
+
+    lo, hi = [], []
+    for o in gr.outputs:
+        r = rows(o[0]) | rows(o[1])
+        if all(x < n_lo for x in r):
+            lo.append(o)
+        elif all(x >= n_lo for x in r):
+            hi.append(o)
+        else:
+            return None
+    if not lo or not hi:
+        return None
+    return compile_graph(g, lo, *ctx), compile_graph(g, hi, *ctx)
 
 
 def _extra_syms(g, extra, scal_id, fl):

@@ -231,12 +231,13 @@ def ineligible(prog, fop):
     for gr in fl.groups:
         if any(s >= cfg["S"] for (_, s) in gr.program.stream_regs) and not _mixed(prog):
             return "a loss group reads streams outside the jet plan"
-    if _mixed(prog) and os.environ.get("TDQ_FUSED_STEP_MIXED", "0") != "1":
-        # AC-baseline (order-4 periodic streams): the residual fused beside the high-order boundary
-        # chain measured 0.253 ms/step vs 0.211-0.217 on the point-range path (gpurun_out/r5f1):
-        # the jet_hi chain no longer overlaps a second range's backward
-        return "high-order boundary streams (TDQ_FUSED_STEP_MIXED=1 runs the residual fused)"
-    if _mixed(prog):
+    mode = _mixed_mode(prog)
+    if mode == "0":
+        return "high-order boundary streams (TDQ_FUSED_STEP_MIXED=0)"
+    if mode == "split":
+        sp = _split_groups(prog, fop, cfg["S"])
+        return sp if isinstance(sp, str) else None
+    if mode == "1":
         # high-order boundary points (jet_hi.hip streams): only the residual group runs fused
         last = len(prog.segments) - 1
         gr = fl.groups[-1]
@@ -256,6 +257,35 @@ def _mixed(prog):
     return getattr(prog, "hi_op", None) is not None
 
 
+def _mixed_mode(prog):
+    """Layout of a mixed program (order-3/4 boundary streams from jet_hi.hip), ``TDQ_FUSED_STEP_MIXED``:
+    ``split`` (default) - every loss output on main-plan streams runs in the fused launch (the
+    boundary groups' low-order outputs included), only the high-order outputs' chain (jet_hi
+    forward, their loss blocks, jet_hi adjoint) on a side stream; ``1`` - only the residual group
+    fused, the whole boundary chain on the side stream; ``0`` - the point-range path.  MI355X,
+    AC-baseline 50k: split 0.207 ms/step, residual 0.251, point ranges 0.219-0.226 (AC-SA 0.168;
+    profiles/r5split3_*, r5acb_*).  None: not mixed."""
+    if not _mixed(prog):
+        return None
+    return os.environ.get("TDQ_FUSED_STEP_MIXED", "split")
+
+
+def _split_groups(prog, fop, S):
+    """``[(group, fused program, side program or None)]`` of the split layout, or the reason it
+    does not apply (an output reading main-plan and high-order streams together)."""
+    from .. import fusion
+    out = []
+    for gr in fop.fl.groups:
+        if all(s < S for (_, s) in gr.program.stream_regs):
+            out.append((gr, gr.program, None))
+            continue
+        sp = fusion.split_by_streams(fop.fl, gr, S)
+        if sp is None:
+            return "a loss output reads main-plan and high-order streams together"
+        out.append((gr, sp[0], sp[1]))
+    return out
+
+
 class FusedStepOp:
     """The fused training step of a :class:`~tensordiffeq_amd.models.loss.LossProgram` (built by
     :func:`for_program`).
@@ -263,9 +293,12 @@ class FusedStepOp:
     Single-plan programs: EVERY loss group runs in the one launch - the points re-laid out once
     into a fused point set (each group's instances contiguous, a periodic group's two segments
     interleaved pair by pair), so a step is the fused launch + the two-launch step tail.  Mixed
-    programs (order-3/4 boundary streams from jet_hi.hip): the residual group runs fused over its
-    own segment, the boundary chain (high-order streams, saved-activation forward, loss blocks,
-    backward) on a side stream beside it."""
+    programs (order-3/4 boundary streams from jet_hi.hip, :func:`_mixed_mode`): split layout -
+    every loss output on main-plan streams in the fused launch, the high-order outputs (their own
+    loss op, :func:`fusion.split_by_streams`) with the jet_hi forward / adjoint on a side stream
+    beside it; residual layout - the residual group fused over its own segment, the whole boundary
+    chain (high-order streams, saved-activation forward, loss blocks, backward) on the side
+    stream."""
 
     def __init__(self, prog, fop, wlo=False):
         lib = _lib.load(required=True)
@@ -284,15 +317,19 @@ class FusedStepOp:
         N = prog.X_all.shape[0]
         dev = prog.device
         self.mixed = _mixed(prog)
-        if not self.mixed:
-            # the fused point set: groups in program order, pair groups on even offsets
+        self.layout = "plain" if not self.mixed else ("split" if _mixed_mode(prog) == "split" else "residual")
+        self.fop2 = None
+        if self.layout != "residual":
+            # the fused point set: groups in program order, pair groups on even offsets (split
+            # layout: the boundary groups with their main-plan outputs only)
+            groups = [(gr, gr.program, None) for gr in fl.groups] if not self.mixed else _split_groups(prog, fop, S)
             layout, idx, pos = [], [], 0
-            for gr in fl.groups:
+            for gr, P_f, _ in groups:
                 ns = len(gr.segs)
                 if ns == 2 and pos % 2:
                     idx.append(-1)
                     pos += 1
-                layout.append((gr.program, pos, ns, gr.n))
+                layout.append((P_f, pos, ns, gr.n))
                 offs = [prog.segments[sg].offset for sg in gr.segs]
                 for k in range(gr.n):
                     idx.extend(o + k for o in offs)
@@ -302,6 +339,22 @@ class FusedStepOp:
             X_f[ix < 0] = 0.0
             self.X = X_f.contiguous()
             self.N, self.p_lo, self.srow, self.b_res, self.p_bc, self.seg_lo = pos, 0, 0, 0, 0, 0
+            if self.layout == "split":
+                # the high-order outputs: a loss op of their own (same term / value / lambda / scalar
+                # slots - its pointer table is the main op's), its block rows ahead of the fused rows
+                import copy
+                from ..fusion import Group
+                from .loss_fused import FusedLossOp
+                fl2 = copy.copy(fl)
+                fl2.groups = []
+                for gr, _, P_s in groups:
+                    if P_s is not None:
+                        g2 = Group(list(gr.segs), gr.n)
+                        g2.program = P_s
+                        fl2.groups.append(g2)
+                self.fop2 = FusedLossOp(fl2, prog, fop.lams, fop.scalars, fl.lam_offsets)
+                self.fop2.ptrs = fop.ptrs
+                self.b_res = self.fop2.n_blocks
         else:
             self.seg_lo = prog.segments[-1].offset
             layout = [(fl.groups[-1].program, self.seg_lo, 1, fl.groups[-1].n)]
@@ -318,10 +371,14 @@ class FusedStepOp:
         ntiles = -(-(self.N - self.p_lo) // 32)
         cus = max(1, lib.tdq_device_cus())
         rounds = -(-ntiles // cus)
+        if self.fop2 is not None:
+            # split layout: one round more leaves ~57 CUs to the jet_hi side chain - AC-baseline
+            # 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*
+            rounds += int(os.environ.get("TDQ_FS_SPLIT_ROUNDS", "1"))
         # the fewest workgroups with the same tiles per workgroup (AC-SA 50k: 1592 tiles, 228 x 7):
         # in the mixed layout the CUs left over run the boundary chain beside the fused launch
         self.G = -(-ntiles // rounds)
-        if self.mixed:   # the fused rows follow the boundary loss blocks' rows in fop.partials
+        if self.layout == "residual":   # the fused rows follow the boundary loss blocks' rows in fop.partials
             self.G = min(self.G, fop.n_blocks - self.b_res)
         self.rows = self.srow + self.G
         need = lib.tdq_slab_floats_rows(self.rows, cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"])
@@ -331,7 +388,9 @@ class FusedStepOp:
         # loss partials: the boundary loss blocks' rows (mixed) then one row per fused workgroup
         self.n_lblocks = self.b_res + self.G
         self.lpart = torch.zeros(max(1, self.n_lblocks * self.nacc), dtype=torch.float32, device=dev)
-        self._side = torch.cuda.Stream(device=dev) if self.p_bc > 0 else None
+        if self.fop2 is not None:   # the side chain's loss blocks write rows [0, b_res) of the same buffer
+            self.fop2.partials = self.lpart[:self.b_res * self.nacc]
+        self._side = torch.cuda.Stream(device=dev) if (self.p_bc > 0 or self.fop2 is not None) else None
 
     def run(self, saved, J, work, flat, pack=True):
         """The step's gradient slabs and loss partials (the fused launch; mixed programs: plus the
@@ -347,9 +406,14 @@ class FusedStepOp:
         X, _, scratch, _, spec, S = saved
         spec_arr = (ctypes.c_int * len(spec))(*spec)
         Xf = self.X if self.X is not None else X
-        lpart = fop.partials if self.mixed else self.lpart
+        lpart = fop.partials if self.layout == "residual" else self.lpart
 
         def boundary():
+            if self.fop2 is not None:   # split layout: only the high-order outputs' chain
+                hop.forward(J, flat)
+                self.fop2.run_range(J, 0, self.fop2.n_blocks)
+                hop.backward(self.fop2.dJ, flat)
+                return
             hop.forward(J, flat)
             jet_hip.forward_range(saved, J, 0, self.p_bc)
             if self.b_res > 0:
@@ -369,6 +433,19 @@ class FusedStepOp:
 
         if side is None:
             fused()
+            return
+        if self.fop2 is not None and os.environ.get("TDQ_FS_SPLIT_ORDER", "side_first") == "side_first":
+            # split layout: the jet_hi forward goes first - launched beside a running fused kernel it
+            # only gets the CUs the persistent workgroups leave free (143 us instead of 18,
+            # profiles/r5split_*); ahead of it, its ~100 workgroups finish while the fused
+            # kernel's fill the rest of the GPU
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                boundary()
+            fused()
+            cur.wait_stream(side)
             return
         # the fused launch is the graph's first node and the boundary branch forks from before it:
         # MI355X, AC-SA (side chain layout): 0.1697 vs 0.1813 ms/step with the branch captured
@@ -390,7 +467,7 @@ class FusedStepOp:
     def tail_kw(self):
         """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows (the
         weight-lo objective: ``dp_tail_a`` only, its slab rows are fp32)."""
-        kw = {"rows": self.rows, "lpart": self.fop.partials if self.mixed else self.lpart,
+        kw = {"rows": self.rows, "lpart": self.fop.partials if self.layout == "residual" else self.lpart,
               "n_lblocks": self.n_lblocks}
         if self.wlo:
             kw["half"] = False

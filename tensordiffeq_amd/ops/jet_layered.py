@@ -12,12 +12,14 @@ whole layer stack, which bounds the hidden width at 128.  The reference accepts 
   ``csrc/lay_gemm.hip`` (``TDQ_LAY_GEMM=0``: the library GEMMs through ``torch.mm``, the A/B
   reference);
 * the bias, the tanh jet (value, first-, second-order streams) and its adjoint (``csrc/lay_jet.h``)
-  run in the EPILOGUE of the hidden layers' NN GEMMs in the bf16 families (``tdq_lay_nnj``: a
-  GEMM tile holds all S streams of its points, so the jet runs on the accumulators; the layer's
+  run in the EPILOGUE of the hidden layers' NN GEMMs (``tdq_lay_nnj``: a GEMM tile holds all S
+  streams of its points, so the jet runs on the accumulators); in the bf16 families the layer's
   output leaves the kernel only as the next GEMMs' bf16 operands, whose hi + lo sum is also the
-  saved post-activation of the adjoint - no fp32 Z / H round trips through HBM).  The input layer,
-  the output layer's adjoint, fp32 and the library path use the standalone memory-bound epilogue
-  pass (``tdq_layered_epi``), the adjoint from the saved post-activations only (no tanh recompute).
+  saved post-activation of the adjoint (fp32: one fp32 plane) - no Z / HB round trips through HBM.
+  The input layer is one ``X K0`` + jet kernel, the last hidden layer's adjoint forms ``dJ Ko^T``
+  in-kernel, and the input layer's gradient leaves as tile partials.  The library path
+  (``TDQ_LAY_GEMM=0``), ``TDQ_LAY_FUSED=0`` and CPU use the standalone memory-bound epilogue pass
+  (``tdq_layered_epi``) between plain GEMMs.
 
 Orders <= 2 (like the fused kernels).  On CPU the same engine runs with torch epilogues (the
 numerics oracle of the HIP pass, tests/test_layered_jet.py).  Same contract as
@@ -216,7 +218,7 @@ def _mm_tn(a, b, out):
 def _fused(X, ws, precision):
     """The GEMM-epilogue path (the layer jet inside the hand-written kernels, bf16 families)."""
     import os
-    return (X.is_cuda and precision in ("bf16", "bf16x3") and _hip_gemm() and X.shape[1] <= 8
+    return (X.is_cuda and precision in ("bf16", "bf16x3", "fp32") and _hip_gemm() and X.shape[1] <= 8
             and os.environ.get("TDQ_LAY_FUSED", "1") != "0" and all(K.shape[1] % 4 == 0 for K, _ in ws[:-1]))
 
 
@@ -227,23 +229,31 @@ def _spec_c(spec):
     return (ctypes.c_int * len(spec))(*spec)
 
 
+def _hl(H):
+    """(hi, lo) device planes of a saved activation: a bf16 pair, or one fp32 plane (fp32 engine)."""
+    if H is None:
+        return None, None
+    return H if isinstance(H, tuple) else (H, None)
+
+
 def _nnj(mode, prec, spec, S, N, a, bt, bias=None, H=None, part=None, X=None):
     """One NN GEMM with the layer jet in its epilogue (csrc/lay_gemm.hip ``lay_nnj_kernel``): ``a``
     the :class:`_Op` of the layer input planes [S*N, K], ``bt`` the fp32 B^T [Nout, K].  Returns the
     (hi, lo) bf16 output planes: EPI_FWD the layer's post-activations (lo always - it is the saved
     activation's residual), EPI_BWD its ZB (lo in bf16x3 only; ``part`` the bias partials),
-    EPI_BWD0 nothing (``part`` the input layer's gradient partials, ``X`` its coordinates)."""
+    EPI_BWD0 nothing (``part`` the input layer's gradient partials, ``X`` its coordinates).  fp32:
+    one fp32 output plane as ``(plane, None)``, ``H`` the fp32 plane."""
     ah, al = _planes(a)
-    bo = _Op(bt.contiguous(), prec)
-    bh, bl = _planes(bo)
+    bo = _Op(bt.contiguous(), prec) if prec != "fp32" else None
+    bh, bl = _planes(bo) if bo is not None else (bt.contiguous(), None)
     Nout, K = bt.shape
     dev = ah.device
     oh = ol = None
     if mode != EPI_BWD0:
-        oh = torch.empty((S * N, Nout), dtype=torch.bfloat16, device=dev)
-        if mode == EPI_FWD or prec == "bf16x3":
+        oh = torch.empty((S * N, Nout), dtype=torch.float32 if prec == "fp32" else torch.bfloat16, device=dev)
+        if prec != "fp32" and (mode == EPI_FWD or prec == "bf16x3"):
             ol = torch.empty_like(oh)
-    hh, hl = H if H is not None else (None, None)
+    hh, hl = _hl(H)
     lib = _lib.load(required=True)
     rc = lib.tdq_lay_nnj(_PREC[prec], mode, S, _spec_c(spec), _lib.ptr(ah), _lib.ptr(al), _lib.ptr(bh), _lib.ptr(bl),
                          N, K, Nout, _lib.ptr(bias), _lib.ptr(hh), _lib.ptr(hl), _lib.ptr(oh), _lib.ptr(ol),
@@ -317,17 +327,25 @@ def forward_raw(X, P, net, plan, precision="fp32"):
     if fused:
         # input layer: X K0 (d_in exact fp32 FMAs) + jet in one pass, the hidden layers' NN GEMMs with
         # the jet in their epilogues; activations only as (hi, lo) bf16 planes
-        hi = torch.empty((S * N, W0), dtype=torch.bfloat16, device=X.device)
-        lo = torch.empty_like(hi)
+        f32 = precision == "fp32"
+        hi = torch.empty((S * N, W0), dtype=torch.float32 if f32 else torch.bfloat16, device=X.device)
+        lo = None if f32 else torch.empty_like(hi)
         lib = _lib.load(required=True)
-        _lib.check(lib.tdq_lay_in_fwd(S, _spec_c(spec), _lib.ptr(X), X.shape[1], _lib.ptr(K0.contiguous()),
+        _lib.check(lib.tdq_lay_in_fwd(int(f32), S, _spec_c(spec), _lib.ptr(X), X.shape[1], _lib.ptr(K0.contiguous()),
                                       _lib.ptr(b0.contiguous()), N, W0, _lib.ptr(hi), _lib.ptr(lo),
                                       _lib.stream_ptr(X.device)), "tdq_lay_in_fwd")
-        Hs, Ho = [(hi, lo)], [_Op.parts(precision, hi, lo if precision == "bf16x3" else None)]
+
+        def saved(hi, lo):   # (saved activation, GEMM operand)
+            if f32:
+                return hi, _Op(hi, "fp32")
+            return (hi, lo), _Op.parts(precision, hi, lo if precision == "bf16x3" else None)
+
+        h, o = saved(hi, lo)
+        Hs, Ho = [h], [o]
         for K, b in ws[1:-1]:
-            hi, lo = _nnj(EPI_FWD, precision, spec, S, N, Ho[-1], K.t(), bias=b)
-            Hs.append((hi, lo))
-            Ho.append(_Op.parts(precision, hi, lo if precision == "bf16x3" else None))
+            h, o = saved(*_nnj(EPI_FWD, precision, spec, S, N, Ho[-1], K.t(), bias=b))
+            Hs.append(h)
+            Ho.append(o)
         Ko, bo = ws[-1]
         J = _mm_w(Ho[-1], Ko, precision).view(S, N, Ko.shape[1])
         J[0] += bo
@@ -369,7 +387,10 @@ def backward_raw(saved, dJ, grad=None):
     dJo = _Op(dJ.view(S * N, dJ.shape[2]), prec)
     last = len(ws) - 2
     if fused and dJ.shape[2] <= 64:   # dKo = H^T dJ, a few columns: FMA partials on exact dJ, H = hi + lo
-        _xtz(dJ.view(S * N, dJ.shape[2]), gw[-1][0], H=Hs[last], rows=64)
+        if prec == "fp32":
+            _xtz(dJ.view(S * N, dJ.shape[2]), gw[-1][0], Z=Hs[last], rows=64)
+        else:
+            _xtz(dJ.view(S * N, dJ.shape[2]), gw[-1][0], H=Hs[last], rows=64)
     else:
         _mm_tn(Ho[-1], dJo, gw[-1][0])
     torch.sum(dJ[0], dim=0, out=gw[-1][1])
@@ -385,22 +406,29 @@ def backward_raw(saved, dJ, grad=None):
         lib = _lib.load(required=True)
         W = Ko.shape[0]
         ZBo = db = None
+        f32 = prec == "fp32"
         if d_out <= 4:   # the last hidden layer's adjoint with HB = dJ Ko^T formed in the kernel
             mode = EPI_BWD if last > 0 else EPI_BWD0
             oh = ol = None
             if last > 0:
                 db = _parts(S, N, W, 1, X.device)
-                oh = torch.empty((S * N, W), dtype=torch.bfloat16, device=X.device)
+                oh = torch.empty((S * N, W), dtype=torch.float32 if f32 else torch.bfloat16, device=X.device)
                 ol = torch.empty_like(oh) if prec == "bf16x3" else None
             else:
                 part0 = db = _parts(S, N, W, S + d_in, X.device)
-            _lib.check(lib.tdq_lay_out_bwd(mode, S, _spec_c(spec), _lib.ptr(dJ), d_out, _lib.ptr(Ko.contiguous()),
-                                           _lib.ptr(Hs[last][0]), _lib.ptr(Hs[last][1]), N, W, _lib.ptr(oh),
+            hh, hl = _hl(Hs[last])
+            _lib.check(lib.tdq_lay_out_bwd(int(f32), mode, S, _spec_c(spec), _lib.ptr(dJ), d_out,
+                                           _lib.ptr(Ko.contiguous()), _lib.ptr(hh), _lib.ptr(hl), N, W, _lib.ptr(oh),
                                            _lib.ptr(ol), _lib.ptr(db), _lib.ptr(X if last == 0 else None),
                                            d_in, _lib.stream_ptr(X.device)), "tdq_lay_out_bwd")
             if last > 0:
-                ZBo = _Op.parts(prec, oh, ol)
-        else:            # (wide outputs: HB from the NN GEMM, then the standalone pass)
+                ZBo = _Op(oh, "fp32") if f32 else _Op.parts(prec, oh, ol)
+        elif f32:        # (wide outputs: HB from the NN GEMM, then the standalone pass)
+            ZB, ZBo = _epi(False, HB, Hs[last], None, spec, "fp32")
+            db = ZB[0].unsqueeze(0)
+            if last == 0:
+                ZB0 = ZB
+        else:
             ZB, ZBo = _epi(False, HB, None, None, spec, prec if last > 0 else "fp32", H=Hs[last])
             db = ZB[0].unsqueeze(0)
             if last == 0:
@@ -415,7 +443,7 @@ def backward_raw(saved, dJ, grad=None):
             if i - 1 > 0:
                 db = _parts(S, N, W, 1, X.device)
                 hi, lo = _nnj(EPI_BWD, prec, spec, S, N, ZBo, K, H=Hs[i - 1], part=db)
-                ZBo = _Op.parts(prec, hi, lo)
+                ZBo = _Op(hi, "fp32") if f32 else _Op.parts(prec, hi, lo)
             else:
                 part0 = _parts(S, N, W, S + d_in, X.device)
                 _nnj(EPI_BWD0, prec, spec, S, N, ZBo, K, H=Hs[0], part=part0, X=X)

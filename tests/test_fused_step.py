@@ -95,13 +95,15 @@ def _acsa(n_f, seed=0, problem="ac-sa"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("problem,n_f", [("ac-sa", 50000), ("ac-sa", 3001), ("ac-baseline", 20000)])
-def test_fused_step_matches_separate_launches(problem, n_f, monkeypatch):
+@pytest.mark.parametrize("problem,n_f,mixed", [("ac-sa", 50000, "split"), ("ac-sa", 3001, "split"),
+                                               ("ac-baseline", 20000, "split"), ("ac-baseline", 20000, "1")])
+def test_fused_step_matches_separate_launches(problem, n_f, mixed, monkeypatch):
     """One evaluation: every loss term, the theta gradient and the SA-weight gradients of the fused
     step vs the separate launches (saved-activation kernels + specialized loss kernel).  AC-SA runs
     every group in the fused launch (IC with SA weights, the periodic pairs, the residual);
-    AC-baseline (order-4 periodic streams, opt-in) its residual only."""
-    monkeypatch.setenv("TDQ_FUSED_STEP_MIXED", "1")
+    AC-baseline (order-4 periodic streams): split layout - every main-plan output fused, the
+    u_xxx / u_xxxx outputs on the jet_hi side chain; layout "1" - the residual only."""
+    monkeypatch.setenv("TDQ_FUSED_STEP_MIXED", mixed)
     from tensordiffeq_amd.fit import LossGradEngine
     from tensordiffeq_amd.ops import fused_step
     out = {}
@@ -114,6 +116,8 @@ def test_fused_step_matches_separate_launches(problem, n_f, monkeypatch):
         if flag == "1":
             assert fs is not None, prog.fused_step_reason
             assert fs.mixed == (problem == "ac-baseline")
+            if fs.mixed:
+                assert fs.layout == ("split" if mixed == "split" else "residual")
         else:
             assert fs is None
         eng = LossGradEngine(m, prog, m.lambdas)

@@ -8,7 +8,7 @@ O=gpurun_out/${TAG:-r5lay}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_lay_gemm.py tests/test_layered_jet.py -m gpu -q -x -s --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { grep -E "^E |FAILED|passed|failed|Error|LAY_|KERNEL_ERR" $O/pytest.log | head -30; exit 1; }
 grep -E "LAY_|KERNEL_ERR|passed" $O/pytest.log | cut -c1-200
-for cfg in "bf16:2,512,512,512,512,1" "bf16x3:2,256,256,256,256,1"; do
+for cfg in "bf16:2,512,512,512,512,1" "bf16x3:2,256,256,256,256,1" "fp32:2,256,256,256,256,1"; do
   pr=${cfg%%:*}; ly=${cfg#*:}
   for gf in 1:1 1:0 0:0; do
     g=${gf%%:*}; f=${gf#*:}
