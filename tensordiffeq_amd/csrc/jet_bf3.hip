@@ -664,7 +664,7 @@ int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_
 // workgroups, gradient-slab rows srow.., loss-partial rows prow.. (nacc floats each)
 int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* work, int N, int d_in, const int* widths,
                           int d_out, int n_hidden, int S, const int* spec, int p_lo, int srow, int G, const void* lptrs,
-                          float* lpart, int prow, int nacc, int seg_lo, void* stream) {
+                          float* lpart, int prow, int nacc, int seg_lo, int* tctr, void* stream) {
   if (func == nullptr || N <= 0 || p_lo < 0 || p_lo >= N || G < 1 || srow < 0 || prow < 0 || nacc < 1)
     return (int)hipErrorInvalidValue;
   NetDims d;
@@ -693,6 +693,7 @@ int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* wor
   P.prow = prow;
   P.nacc = nacc;
   P.seg_lo = seg_lo;
+  P.tctr = tctr;  // (the dynamic-queue kernels only; nullable otherwise)
   void* args[] = {(void*)&P};
   return (int)hipModuleLaunchKernel((hipFunction_t)func, (unsigned)G, 1, 1, 64 * FZ_WAVES, 1, 1, 0,
                                     reinterpret_cast<hipStream_t>(stream), args, nullptr);

@@ -284,6 +284,9 @@ struct FzParams {
   const FzLossPtrs* lptrs;
   float* lpart;         // loss / scalar-gradient partials, row prow + blockIdx.x, nacc floats each
   int prow, nacc, seg_lo;  // (seg_lo: unused by the generated loss)
+  // MODE 2 with the dynamic tile queue (DYN): [0] next tile, [1] finished workgroups; zero at
+  // launch, re-armed by the last workgroup to finish
+  int* tctr;
 };
 
 // MODE 0 / 1 builds: no loss code.  The MODE 2 interface (ops/fused_step.py generates it):
@@ -311,7 +314,24 @@ struct FzNoLoss {
 // wave w computes column tile q = w >> 2 (16 points) of feature tiles 2 (w & 3).. (OPW of them) in
 // every GEMM / epilogue, and owns an NR x NC block of each hidden layer's dK tiles.
 // WLO (MODE 2, the L-BFGS objective "bf16w"): weight lo parts in every GEMM and fp32 slab rows
-template <int WT, int S, int NSO, int LM, int MODE, class LossF, bool WLO = false>
+// LDS slots of the dynamic tile queue (allocated only by DYN instantiations)
+template <bool DYN>
+struct FzTileQ {
+  __device__ static int* slots() { return nullptr; }
+};
+template <>
+struct FzTileQ<true> {
+  __device__ static int* slots() {
+    __shared__ int q[2];
+    return q;
+  }
+};
+
+// DYN (MODE 2): tiles come from an atomic counter instead of a fixed contiguous range, so
+// workgroups that start late (CUs still held by a side-stream kernel) simply take fewer tiles.  The
+// counter is read two tiles ahead (the returned index is parked in LDS at the end of the tile), so
+// no wave waits on the atomic.
+template <int WT, int S, int NSO, int LM, int MODE, class LossF, bool WLO = false, bool DYN = false>
 __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   const float* __restrict__ X = P.X;
   const float* __restrict__ aux_g = P.aux;
@@ -396,19 +416,34 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       upre = (n < N && qo < d.d_out) ? dJ[((size_t)s * N + n) * d.d_out + qo] : 0.f;
     }
   };
-  if (t0 < t1) fetch(t0);
+  int* fz_tq = FzTileQ<DYN>::slots();  // DYN: [0] first tile, [1] the tile after the next one
+  int t = t0, tend = t1, tn = 0;
+  if constexpr (DYN) {
+    if (tid == 0) {
+      fz_tq[0] = atomicAdd(P.tctr, 1);
+      fz_tq[1] = atomicAdd(P.tctr, 1);
+    }
+    __syncthreads();
+    t = fz_tq[0];
+    tend = ntiles;
+  }
+  if (t < tend) fetch(t);
   TDQ_TS(0);
-  for (int t = t0; t < t1; ++t) {
+  while (t < tend) {
     const int pb = P.p_lo + t * FZ_PT;
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
     __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
+    if constexpr (DYN) tn = fz_tq[1];
+    else tn = t + 1;
     if (tid < FZ_PT * TDQ_MAXD) xs[tid] = xpre;
     if (MODE == 1 && tid < S * FZ_PT * 4) ubs[tid] = upre;
     if constexpr (MODE == 2) {
 #pragma unroll
       for (int k = 0; k < LossF::NPRE; ++k) lpre[k] = lnext[k];
     }
-    if (t + 1 < t1) fetch(t + 1);
+    if (tn < tend) fetch(tn);
+    int tq = 0;
+    if (DYN && tid == 0) tq = atomicAdd(P.tctr, 1);  // the tile after tn (parked at the tile's end)
     __syncthreads();
     FZ_TS(1);
 
@@ -654,8 +689,16 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
         FZ_TS(tb + 4);
       }
     }
+    if (DYN && tid == 0) fz_tq[1] = tq;  // read after the next tile's first barrier
+    t = tn;
   }
   TDQ_TS(62);
+  if constexpr (DYN) {  // the last workgroup out re-arms the queue for the next launch
+    if (tid == 0 && atomicAdd(P.tctr + 1, 1) == (int)gridDim.x - 1) {
+      P.tctr[0] = 0;
+      P.tctr[1] = 0;
+    }
+  }
 
   if constexpr (MODE >= 1) {
     // ---- this workgroup's gradient-slab row (bf16; WLO: fp32) --------------------------------

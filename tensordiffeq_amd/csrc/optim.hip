@@ -83,7 +83,7 @@ __global__ void step_book_kernel(float* __restrict__ loss, const float* __restri
 
 extern "C" {
 
-int tdq_abi_version() { return 26; }
+int tdq_abi_version() { return 27; }
 
 int tdq_step_book(float* loss, const float* terms, int n_terms, int sum_terms, float* hist, int64_t hist_rows,
                   int64_t* epoch, float* best_loss, int64_t* best_epoch, int* improved, double* const* counters,

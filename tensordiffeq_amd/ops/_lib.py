@@ -19,7 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "csrc", "libtdq_hip.so")
-ABI_VERSION = 26
+ABI_VERSION = 27
 
 _lock = threading.Lock()
 _lib = None
@@ -59,7 +59,7 @@ def _declare(lib):
         "tdq_jet_fused_active": (I, [I, P, I, I, I, I]),
         "tdq_jet_fused_rows": (I, [I]),
         "tdq_jet_fused_override": (I, [I]),
-        "tdq_fused_step_launch": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, I, P, P, I, I, I, P]),
+        "tdq_fused_step_launch": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, I, P, P, I, I, I, P, P]),
         "tdq_fused_params_size": (I, []),
         "tdq_jet_fused_lds": (I, [I, P, I, I, I, I]),
         "tdq_device_cus": (I, []),

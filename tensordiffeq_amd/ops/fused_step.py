@@ -176,12 +176,13 @@ def gen_loss(groups, n_terms, nacc, S):
     return "\n".join(L)
 
 
-def kernel_source(S, nso, LM, lds, gen, wlo=False):
+def kernel_source(S, nso, LM, lds, gen, wlo=False, dyn=False):
     return (header_source() + "\n" + gen + "\n"
             'extern "C" __global__ void __launch_bounds__(64 * FZ_WAVES) '
             "__attribute__((amdgpu_waves_per_eu(2, 2))) tdq_fused_step(FzParams P) {\n"
             f"  __shared__ __attribute__((aligned(16))) char lds[{lds}];\n"
-            f"  fz_body<8, {S}, {nso}, {LM}, 2, GenLoss, {'true' if wlo else 'false'}>(P, lds);\n"
+            f"  fz_body<8, {S}, {nso}, {LM}, 2, GenLoss, {'true' if wlo else 'false'}, "
+            f"{'true' if dyn else 'false'}>(P, lds);\n"
             "}\n")
 
 
@@ -366,18 +367,28 @@ class FusedStepOp:
             pts_b = jet_hip.slab_geometry(cfg, N)[0]
             self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
             self.srow = -(-self.p_bc // pts_b)
-        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), wlo=self.wlo)
+        # dynamic tile queue (fz_body DYN, ``TDQ_FS_DYNAMIC=1``): workgroups that start late take
+        # fewer tiles.  Measured on the split layout (AC-baseline, profiles/r5split_dyn_*): every CU
+        # taken 0.2106 ms (the side chain then waits for the launch to end), 32 CUs left to the side
+        # chain 0.2098 (it overlaps; the join before the tail costs ~10 us) vs 0.2065 with static
+        # ranges and one round more; AC-SA 0.1751 vs 0.1673 static - off by default
+        self.dyn = os.environ.get("TDQ_FS_DYNAMIC", "0") == "1"
+        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), wlo=self.wlo,
+                                    dyn=self.dyn)
         self.module, self.func = _compile(self.source)
         ntiles = -(-(self.N - self.p_lo) // 32)
         cus = max(1, lib.tdq_device_cus())
         rounds = -(-ntiles // cus)
-        if self.fop2 is not None:
-            # split layout: one round more leaves ~57 CUs to the jet_hi side chain - AC-baseline
-            # 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*
+        if self.fop2 is not None and not self.dyn:
+            # split layout, static ranges: one round more leaves ~57 CUs to the jet_hi side chain -
+            # AC-baseline 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*
             rounds += int(os.environ.get("TDQ_FS_SPLIT_ROUNDS", "1"))
-        # the fewest workgroups with the same tiles per workgroup (AC-SA 50k: 1592 tiles, 228 x 7):
-        # in the mixed layout the CUs left over run the boundary chain beside the fused launch
-        self.G = -(-ntiles // rounds)
+        # static ranges: the fewest workgroups with the same tiles per workgroup (AC-SA 50k: 1592
+        # tiles, 228 x 7); dynamic queue: one workgroup per CU but the ones the split layout's side
+        # chain needs (with every CU taken its kernels waited for the fused launch to end)
+        reserve = int(os.environ.get("TDQ_FS_DYN_RESERVE", "32")) if self.fop2 is not None else 0
+        self.G = max(1, min(cus - reserve, ntiles)) if self.dyn else -(-ntiles // rounds)
+        self.tctr = torch.zeros(2, dtype=torch.int32, device=dev)
         if self.layout == "residual":   # the fused rows follow the boundary loss blocks' rows in fop.partials
             self.G = min(self.G, fop.n_blocks - self.b_res)
         self.rows = self.srow + self.G
@@ -428,6 +439,7 @@ class FusedStepOp:
                                            cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S,
                                            spec_arr, self.p_lo, self.srow, self.G, _lib.ptr(fop.ptrs),
                                            _lib.ptr(lpart), self.b_res, self.nacc, self.seg_lo,
+                                           _lib.ptr(self.tctr) if self.dyn else None,
                                            _lib.stream_ptr(flat.device))
             _lib.check(rc, "tdq_fused_step_launch")
 

@@ -77,6 +77,8 @@ def test_fused_step_source_compiles(problem, layers):
     if problem == "ac":   # the periodic pair group reads its partner point
         assert "t + 1" in gen
     _compile_ok(fused_step.kernel_source(cfg["S"], nso, cfg["n_hidden"] - 1, lds, gen))
+    if problem == "ac":   # the dynamic tile queue variant (split layout of mixed programs)
+        _compile_ok(fused_step.kernel_source(cfg["S"], nso, cfg["n_hidden"] - 1, lds, gen, dyn=True))
 
 
 def test_fused_step_not_on_cpu():
@@ -95,15 +97,19 @@ def _acsa(n_f, seed=0, problem="ac-sa"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("problem,n_f,mixed", [("ac-sa", 50000, "split"), ("ac-sa", 3001, "split"),
-                                               ("ac-baseline", 20000, "split"), ("ac-baseline", 20000, "1")])
-def test_fused_step_matches_separate_launches(problem, n_f, mixed, monkeypatch):
+@pytest.mark.parametrize("problem,n_f,mixed,dyn", [("ac-sa", 50000, "split", "0"), ("ac-sa", 3001, "split", "0"),
+                                                   ("ac-sa", 50000, "split", "1"),
+                                                   ("ac-baseline", 20000, "split", "1"),
+                                                   ("ac-baseline", 20000, "split", "0"),
+                                                   ("ac-baseline", 20000, "1", "0")])
+def test_fused_step_matches_separate_launches(problem, n_f, mixed, dyn, monkeypatch):
     """One evaluation: every loss term, the theta gradient and the SA-weight gradients of the fused
     step vs the separate launches (saved-activation kernels + specialized loss kernel).  AC-SA runs
     every group in the fused launch (IC with SA weights, the periodic pairs, the residual);
     AC-baseline (order-4 periodic streams): split layout - every main-plan output fused, the
     u_xxx / u_xxxx outputs on the jet_hi side chain; layout "1" - the residual only."""
     monkeypatch.setenv("TDQ_FUSED_STEP_MIXED", mixed)
+    monkeypatch.setenv("TDQ_FS_DYNAMIC", dyn)   # the dynamic tile queue (opt-in)
     from tensordiffeq_amd.fit import LossGradEngine
     from tensordiffeq_amd.ops import fused_step
     out = {}
@@ -118,6 +124,7 @@ def test_fused_step_matches_separate_launches(problem, n_f, mixed, monkeypatch):
             assert fs.mixed == (problem == "ac-baseline")
             if fs.mixed:
                 assert fs.layout == ("split" if mixed == "split" else "residual")
+            assert fs.dyn == (dyn == "1")
         else:
             assert fs is None
         eng = LossGradEngine(m, prog, m.lambdas)
