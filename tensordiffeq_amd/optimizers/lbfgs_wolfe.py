@@ -16,8 +16,12 @@ GPU and one L-BFGS iteration is a handful of graph replays:
 * **update** (one graph): shift the history, insert ``s = x1 - x0``, ``y = g1 - g0``, ``rho``.
 
 The line search is the strong-Wolfe bracketing / zoom of Nocedal & Wright (Alg. 3.5 / 3.6,
-``c1 = 1e-4``, ``c2 = 0.9``) with safeguarded cubic interpolation; it runs on the host on the two
-scalars of each trial.  Stops: ``max_iterations``, ``max|g| <= tolerance``, a line search that finds
+``c1 = 1e-4``, ``c2 = 0.9``) with safeguarded cubic interpolation, plus the approximate Wolfe
+conditions of Hager & Zhang (TFP's default line search; ``delta = 0.1``, ``sigma = 0.9``,
+``epsilon = 1e-6``): near the minimum the loss changes only at its rounding level, where the
+sufficient-decrease test is noise - a trial within ``epsilon |f0|`` of ``f0`` whose slope satisfies
+``sigma g0.d <= g.d <= (2 delta - 1) g0.d`` is accepted.  It runs on the host on the two scalars of
+each trial.  Stops: ``max_iterations``, ``max|g| <= tolerance``, a line search that finds
 no decrease, or an unchanged loss (TFP's zero x / f tolerances).
 
 On a CPU (or without graphs) the same operations run eagerly; that path is the oracle of the tests
@@ -32,6 +36,7 @@ import torch
 from ..graphs import capture_graph
 
 C1, C2 = 1e-4, 0.9
+HZ_DELTA, HZ_SIGMA, HZ_EPS = 0.1, 0.9, 1e-6   # approximate Wolfe (Hager & Zhang 2005, TFP's defaults)
 
 
 def _cubic(x1, f1, g1, x2, f2, g2, lo, hi):
@@ -199,6 +204,10 @@ class WolfeLBFGS:
         tp, fp, gp = 0.0, f0, gtd0
         bracket = None
         n = 0
+
+        def approx_wolfe(f, gtd):
+            return f <= f0 + HZ_EPS * abs(f0) and HZ_SIGMA * gtd0 <= gtd <= (2.0 * HZ_DELTA - 1.0) * gtd0
+
         while n < self.max_ls:
             f, gtd = self._trial(t)
             n += 1
@@ -206,6 +215,9 @@ class WolfeLBFGS:
                 bracket = ((tp, fp, gp), (t, math.inf, math.nan))
                 break
             if f > f0 + C1 * t * gtd0 or (n > 1 and f >= fp):
+                if approx_wolfe(f, gtd):
+                    self._keep()
+                    return (t, f, gtd)
                 bracket = ((tp, fp, gp), (t, f, gtd))
                 break
             self._keep()
@@ -234,6 +246,9 @@ class WolfeLBFGS:
             f, gtd = self._trial(t)
             n += 1
             if not math.isfinite(f) or f > f0 + C1 * t * gtd0 or f >= fl:
+                if math.isfinite(f) and approx_wolfe(f, gtd):
+                    self._keep()
+                    return (t, f, gtd)
                 th, fh, gh = t, (f if math.isfinite(f) else math.inf), gtd
                 continue
             self._keep()
