@@ -23,7 +23,7 @@
 // The layer jet (lay_jet.h) runs in the GEMM epilogues (lay_nnj_kernel) and in two elementwise end-layer
 // kernels (lay_in_fwd_kernel: X K0 + jet; lay_out_bwd_kernel: dJ Ko^T + adjoint jet), so no fp32
 // activation / adjoint plane of a hidden layer ever goes through HBM.  Measured on MI355X (AC
-// [2, W x 4, 1], 50k points, one Adam step, profiles/r5lay4_*): bf16 width 512 2.81 ms and bf16x3
+// [2, W x 4, 1], 50k points, one Adam step, profiles/r5lay4_*): bf16 width 512 2.71 ms and bf16x3
 // width 256 1.79 ms per step, vs 4.75 / 5.69 ms on the library GEMMs (hipBLASLt) + standalone pass.
 // Reference: tensordiffeq/networks.py:10-20 (any layer list), the reference's tape GEMMs.
 #include "jet_bf3.h"
@@ -755,8 +755,10 @@ __global__ void __launch_bounds__(256) lay_tn2_kernel(const __bf16* __restrict__
                                                       float* __restrict__ Cp, int L, int Ma, int Nb,
                                                       int rows_per_chunk, int vec) {
   constexpr int NB = P == 1 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) __bf16 sA[2][NB][32 * TS];
-  __shared__ __attribute__((aligned(16))) __bf16 sB[2][NB][32 * TS];
+  constexpr int RK = P == 1 ? 32 : 64;  // rows per staged step (bf16x3: two planes, 32)
+  constexpr int NRS = RK / 16;          // rows one thread stages per step
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][NB][RK * TS];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][NB][RK * TS];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
   // XCD-aware order (xcd_tile): the tiles of one row chunk run on one XCD, so its A / B rows are read
@@ -766,8 +768,8 @@ __global__ void __launch_bounds__(256) lay_tn2_kernel(const __bf16* __restrict__
   const int bz = T / (gx * gy), i0 = ((T / gx) % gy) * 128, j0 = (T % gx) * 128;
   const int r_lo = bz * rows_per_chunk, r_hi = min(L, r_lo + rows_per_chunk);
   const bool v = vec != 0;
-  // staging: chunks t, t + 256 of the 512 8-feature chunks of a 32-row x 128-feature tile
-  const int rr0 = tid >> 4, rr1 = rr0 + 16, fc = (tid & 15) * 8;
+  // staging: thread t stages feature chunk (t & 15) of rows (t >> 4) + 16 c of an RK-row step
+  const int rr = tid >> 4, fc = (tid & 15) * 8;
   // transposed-read address of this lane: row 8g + q, column 4p (+ the tile's first column)
   const int trq = (l & 15) >> 2, trp = l & 3;
   const int ta = (8 * g + trq) * TS + 4 * trp, tb = ta + 4 * TS;
@@ -776,25 +778,25 @@ __global__ void __launch_bounds__(256) lay_tn2_kernel(const __bf16* __restrict__
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // double-buffered: the next 32-row step's global loads are in flight during this step's MFMAs
-  bf16x8 ra[2][NB], rb[2][NB];
+  // double-buffered: the next step's global loads are in flight during this step's MFMAs
+  bf16x8 ra[NRS][NB], rb[NRS][NB];
   auto gload = [&](int r0) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      ra[0][q] = ldg8(q ? Al : Ah, lda, r0 + rr0, r_hi, i0 + fc, Ma, v);
-      ra[1][q] = ldg8(q ? Al : Ah, lda, r0 + rr1, r_hi, i0 + fc, Ma, v);
-      rb[0][q] = ldg8(q ? Bl : Bh, ldb, r0 + rr0, r_hi, j0 + fc, Nb, v);
-      rb[1][q] = ldg8(q ? Bl : Bh, ldb, r0 + rr1, r_hi, j0 + fc, Nb, v);
-    }
+    for (int q = 0; q < NB; ++q)
+#pragma unroll
+      for (int c = 0; c < NRS; ++c) {
+        ra[c][q] = ldg8(q ? Al : Ah, lda, r0 + rr + 16 * c, r_hi, i0 + fc, Ma, v);
+        rb[c][q] = ldg8(q ? Bl : Bh, ldb, r0 + rr + 16 * c, r_hi, j0 + fc, Nb, v);
+      }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      *reinterpret_cast<bf16x8*>(&sA[buf][q][rr0 * TS + fc]) = ra[0][q];
-      *reinterpret_cast<bf16x8*>(&sA[buf][q][rr1 * TS + fc]) = ra[1][q];
-      *reinterpret_cast<bf16x8*>(&sB[buf][q][rr0 * TS + fc]) = rb[0][q];
-      *reinterpret_cast<bf16x8*>(&sB[buf][q][rr1 * TS + fc]) = rb[1][q];
-    }
+    for (int q = 0; q < NB; ++q)
+#pragma unroll
+      for (int c = 0; c < NRS; ++c) {
+        *reinterpret_cast<bf16x8*>(&sA[buf][q][(rr + 16 * c) * TS + fc]) = ra[c][q];
+        *reinterpret_cast<bf16x8*>(&sB[buf][q][(rr + 16 * c) * TS + fc]) = rb[c][q];
+      }
   };
   if (r_lo < r_hi) {
     gload(r_lo);
@@ -802,28 +804,31 @@ __global__ void __launch_bounds__(256) lay_tn2_kernel(const __bf16* __restrict__
   }
   __syncthreads();
   int buf = 0;
-  for (int r0 = r_lo; r0 < r_hi; r0 += 32) {
-    const bool more = r0 + 32 < r_hi;
-    if (more) gload(r0 + 32);
-    bf16x8 a[4][NB], b[4][NB];
+  for (int r0 = r_lo; r0 < r_hi; r0 += RK) {
+    const bool more = r0 + RK < r_hi;
+    if (more) gload(r0 + RK);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int kk = 0; kk < RK; kk += 32) {
+      bf16x8 a[4][NB], b[4][NB];
 #pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int ca = wm * 64 + 16 * i, cb = wn * 64 + 16 * i;
-        a[i][q] = cat8(tr_read(&sA[buf][q][ta + ca]), tr_read(&sA[buf][q][tb + ca]));
-        b[i][q] = cat8(tr_read(&sB[buf][q][ta + cb]), tr_read(&sB[buf][q][tb + cb]));
-      }
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (P == 1) {
-          acc[i][j] = mfma_bf(a[i][1], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_bf(a[i][0], b[j][1], acc[i][j]);
+        for (int q = 0; q < NB; ++q) {
+          const int ca = kk * TS + wm * 64 + 16 * i, cb = kk * TS + wn * 64 + 16 * i;
+          a[i][q] = cat8(tr_read(&sA[buf][q][ta + ca]), tr_read(&sA[buf][q][tb + ca]));
+          b[i][q] = cat8(tr_read(&sB[buf][q][ta + cb]), tr_read(&sB[buf][q][tb + cb]));
         }
-        acc[i][j] = mfma_bf(a[i][0], b[j][0], acc[i][j]);
-      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (P == 1) {
+            acc[i][j] = mfma_bf(a[i][1], b[j][0], acc[i][j]);
+            acc[i][j] = mfma_bf(a[i][0], b[j][1], acc[i][j]);
+          }
+          acc[i][j] = mfma_bf(a[i][0], b[j][0], acc[i][j]);
+        }
+    }
     if (more) {
       sstore(buf ^ 1);
       __syncthreads();
