@@ -23,7 +23,7 @@
 // The layer jet (lay_jet.h) runs in the GEMM epilogues (lay_nnj_kernel) and in two elementwise end-layer
 // kernels (lay_in_fwd_kernel: X K0 + jet; lay_out_bwd_kernel: dJ Ko^T + adjoint jet), so no fp32
 // activation / adjoint plane of a hidden layer ever goes through HBM.  Measured on MI355X (AC
-// [2, W x 4, 1], 50k points, one Adam step, profiles/r5lay4_*): bf16 width 512 2.71 ms and bf16x3
+// [2, W x 4, 1], 50k points, one Adam step, profiles/r5lay4_*): bf16 width 512 2.59 ms and bf16x3
 // width 256 1.79 ms per step, vs 4.75 / 5.69 ms on the library GEMMs (hipBLASLt) + standalone pass.
 // Reference: tensordiffeq/networks.py:10-20 (any layer list), the reference's tape GEMMs.
 #include "jet_bf3.h"
@@ -318,23 +318,19 @@ __device__ __forceinline__ bf16x8 ldg8(const __bf16* __restrict__ base, long lon
   return ldr8(base, (long long)row * ld, row < nrows, k, K, vec);
 }
 
-// k-depth of a staged step: 64 in bf16 (fewer barriers per MFMA), 32 in bf16x3 (two planes per
-// operand - the 64-deep double buffer would need 144 KB of LDS, one workgroup per CU) and fp32
-template <int P>
-constexpr int nn_bk() {
-  return P == 0 ? 64 : 32;
-}
-template <int P>
+// Staged k-depth BK (template): 32 in general (bf16: 40 KB of staging, so with the half-tile
+// epilogue 3-4 workgroups fit a CU), 64 where the LDS holds two workgroups per CU anyway.
+template <int P, int BK>
 constexpr int nn_lk() {  // LDS row stride (elements): 40 / 72 bf16, 36 fp32 - conflict-free fragment reads
-  return nn_bk<P>() + (P == 2 ? 4 : 8);
+  return BK + (P == 2 ? 4 : 8);
 }
-template <int P>
+template <int BK>
 constexpr int nn_rows_per_thread() {  // rows of the 128-row tiles one thread stages (8 k-values each)
-  return 128 * (nn_bk<P>() / 8) / 256;
+  return 128 * (BK / 8) / 256;
 }
-template <int P>
+template <int P, int BK>
 constexpr int nn_stage_bytes() {  // {A, B} x 2 buffers x planes x 128 rows x LK elements
-  return 2 * 2 * (P == 1 ? 2 : 1) * 128 * nn_lk<P>() * (P == 2 ? 4 : 2);
+  return 2 * 2 * (P == 1 ? 2 : 1) * 128 * nn_lk<P, BK>() * (P == 2 ? 4 : 2);
 }
 
 // the A and B rows a thread stages (element offsets of row starts, validity): row c is tile row
@@ -343,9 +339,9 @@ struct NnRows {
   long long a[4], b[4];
   bool va[4], vb[4];
 };
-template <int P>
+template <int BK>
 __device__ __forceinline__ int nn_row(int c) {
-  constexpr int CPR = nn_bk<P>() / 8;
+  constexpr int CPR = BK / 8;
   return (int)threadIdx.x / CPR + c * (256 / CPR);
 }
 
@@ -353,7 +349,7 @@ __device__ __forceinline__ int nn_row(int c) {
 // bf16 families: one v_mfma_f32_16x16x32_bf16 per block and 32-deep substep (x3 in bf16x3); fp32:
 // eight v_mfma_f32_16x16x4_f32 on the same 8-value fragments (MFMA kk takes k = 8 g + kk of lane
 // group g in both operands, so the permuted order sums the same products).
-template <int P>
+template <int P, int BK>
 __device__ __forceinline__ void nn_loop(typename Op<P>::T* smem, const typename Op<P>::T* __restrict__ Ah,
                                         const typename Op<P>::T* __restrict__ Al,
                                         const typename Op<P>::T* __restrict__ Bh,
@@ -361,7 +357,7 @@ __device__ __forceinline__ void nn_loop(typename Op<P>::T* smem, const typename 
                                         f32x4 (&acc)[4][4]) {
   using V = typename Vec8<typename Op<P>::T>::V;
   constexpr int NB = P == 1 ? 2 : 1;
-  constexpr int BK = nn_bk<P>(), LK = nn_lk<P>(), NR = nn_rows_per_thread<P>(), CPR = BK / 8;
+  constexpr int LK = nn_lk<P, BK>(), NR = nn_rows_per_thread<BK>(), CPR = BK / 8;
   constexpr int SZ = 128 * LK;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, p = l & 15, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
@@ -383,7 +379,7 @@ __device__ __forceinline__ void nn_loop(typename Op<P>::T* smem, const typename 
     for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int c = 0; c < NR; ++c) {
-        const int r = nn_row<P>(c);
+        const int r = nn_row<BK>(c);
         *reinterpret_cast<V*>(sA(buf, b) + r * LK + sk) = ra[c][b];
         *reinterpret_cast<V*>(sB(buf, b) + r * LK + sk) = rb[c][b];
       }
@@ -447,7 +443,8 @@ __global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__
                                                       const __bf16* __restrict__ Bl, long long ldb,
                                                       float* __restrict__ C, long long ldc, int M, int N, int K,
                                                       int vec) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[nn_stage_bytes<P>() / 2];  // (bf16 families only)
+  constexpr int BK = 32;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[nn_stage_bytes<P, BK>() / 2];  // (bf16 families only)
   const int gx = (N + 127) / 128;
   const int T = xcd_tile(blockIdx.x, gridDim.x);
   const int m0 = (T / gx) * 128, n0 = (T % gx) * 128;
@@ -455,15 +452,15 @@ __global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__
   const int wm = w >> 1, wn = w & 1;
   NnRows R;
 #pragma unroll
-  for (int c = 0; c < nn_rows_per_thread<P>(); ++c) {
-    const int r = nn_row<P>(c);
+  for (int c = 0; c < nn_rows_per_thread<BK>(); ++c) {
+    const int r = nn_row<BK>(c);
     R.a[c] = (long long)(m0 + r) * lda;
     R.b[c] = (long long)(n0 + r) * ldb;
     R.va[c] = m0 + r < M;
     R.vb[c] = n0 + r < N;
   }
   f32x4 acc[4][4];
-  nn_loop<P>(smem, Ah, Al, Bh, Bl, R, K, vec != 0, acc);
+  nn_loop<P, BK>(smem, Ah, Al, Bh, Bl, R, K, vec != 0, acc);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -508,13 +505,16 @@ struct EpiArgs {
 // red: LDS scratch of 4 x (S + TDQ_MAXD) x 128 floats (may alias the source tile: a barrier
 // precedes its first write).  Every thread of the block must call this.  F32: the fp32 engine -
 // activations / adjoints are single fp32 planes (H32 / O32) instead of bf16 hi / lo pairs.
-template <int S, int MODE, bool F32, class Src>
+// CW: feature columns per call (128, or 64 when a GEMM tile's epilogue runs in two column halves
+// to halve its LDS tile); CW / 4 threads cover a row, 1024 / CW rows per pass.
+template <int S, int MODE, bool F32, int CW = 128, class Src>
 __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, Src src, float* red) {
   constexpr int PT = 128 / S;
   constexpr int NS = MODE == EPI_BWD0 ? S : 1;
   constexpr int NX = MODE == EPI_BWD0 ? TDQ_MAXD : 1;
+  constexpr int QL = CW / 4, RP = 256 / QL;  // threads per row, rows per pass
   const int tid = threadIdx.x, pt0 = ty * PT;
-  const int f4 = (tid & 31) * 4, col = n0 + f4;
+  const int f4 = (tid % QL) * 4, col = n0 + f4;
   const bool cok = col < e.Nout;  // (Nout % 4 == 0: a quad is all in or all out)
   float bb[4] = {0.f, 0.f, 0.f, 0.f}, ps[NS][4], px[NX][4];
 #pragma unroll
@@ -592,14 +592,14 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
   };
   if constexpr (MODE == EPI_BWD0) {  // (rolled: the partial accumulators already hold 4 (S + 8) registers)
 #pragma unroll 1
-    for (int t = tid >> 5; t < PT; t += 8) point(t);
+    for (int t = tid / QL; t < PT; t += RP) point(t);
   } else {
-    for (int t = tid >> 5; t < PT; t += 8) point(t);
+    for (int t = tid / QL; t < PT; t += RP) point(t);
   }
   if constexpr (MODE != EPI_FWD) {
     if (e.part == nullptr) return;  // (uniform)
     const int NP = MODE == EPI_BWD ? 1 : S + e.d_in;
-    // lanes l and l ^ 32 hold the same features: combine them, then the 4 waves through LDS
+    // the lanes of a wave with the same features (lane % QL) combined, then the 4 waves via LDS
     const int w = tid >> 6;
     __syncthreads();  // red may alias the source tile
 #pragma unroll
@@ -608,16 +608,17 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         float a = q < NS ? ps[q < NS ? q : 0][v] : px[q >= NS ? q - NS : 0][v];
-        a += __shfl_xor(a, 32, 64);
-        if ((tid & 32) == 0) red[(w * NP + q) * 128 + f4 + v] = a;
+#pragma unroll
+        for (int m = QL; m < 64; m <<= 1) a += __shfl_xor(a, m, 64);
+        if ((tid & 63) < QL) red[(w * NP + q) * CW + f4 + v] = a;
       }
     }
     __syncthreads();
-    for (int i = tid; i < NP * 128; i += 256) {
-      const int q = i >> 7, c = i & 127;
+    for (int i = tid; i < NP * CW; i += 256) {
+      const int q = i / CW, c = i % CW;
       if (n0 + c >= e.Nout) continue;
-      const float a = red[q * 128 + c] + red[(NP + q) * 128 + c] + red[(2 * NP + q) * 128 + c] +
-                      red[(3 * NP + q) * 128 + c];
+      const float a = red[q * CW + c] + red[(NP + q) * CW + c] + red[(2 * NP + q) * CW + c] +
+                      red[(3 * NP + q) * CW + c];
       e.part[((long long)ty * NP + q) * e.Nout + n0 + c] = a;
     }
   }
@@ -626,7 +627,8 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
 // NN GEMM + layer jet: the 128 tile rows are S streams x PT points (row s PT + t = stream s of point
 // pt0 + t, global row s Npts + pt0 + t of the stream-major planes), so one tile holds every stream of
 // its points; the accumulators go through LDS (a 128 x 132 fp32 tile) into lay_epilogue.
-constexpr int EPI_CS = 132;  // LDS row stride of the fp32 tile: the 4 row groups of a store land 16 banks apart
+// LDS row strides of the fp32 C tile (whole: 132, half: 68): the 4 row groups of a store land 16
+// banks apart
 
 struct NnjArgs {
   const void *Ah, *Al, *Bh, *Bl;  // A planes [S * Npts][K]; B^T [Nout][K] (bf16, or fp32 when P == 2)
@@ -637,9 +639,17 @@ struct NnjArgs {
 template <int P, int S, int MODE>
 __global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
   constexpr int PT = 128 / S;
-  constexpr int STG = nn_stage_bytes<P>();
-  constexpr int EPI = 128 * EPI_CS * 4;
-  static_assert(4 * (TDQ_MAXS + TDQ_MAXD) * 128 * 4 <= EPI, "partials scratch fits the tile");
+  // k-depth of a staged step: 32, except the bf16 input-layer adjoint (whole C tile, 2 workgroups
+  // per CU either way: 64-deep steps halve its barriers, 286 vs 328 us at W512)
+  constexpr int BK = (P == 0 && MODE == EPI_BWD0) ? 64 : 32;
+  constexpr int STG = nn_stage_bytes<P, BK>();
+  // bf16 forward / hidden adjoint: the C tile through LDS in two 64-column halves (40 KB of LDS in
+  // all, so 3-4 workgroups per CU instead of 2: forward 238 vs 278 us at W512); the other modes and
+  // precisions keep the whole tile (two halves measured slower there: profiles/r5lay7_*)
+  constexpr bool HALF = P == 0 && MODE != EPI_BWD0;
+  constexpr int CW = HALF ? 64 : 128, CS = CW + 4;
+  constexpr int EPI = 128 * CS * 4;
+  static_assert(4 * (TDQ_MAXS + TDQ_MAXD) * CW * 4 <= EPI, "partials scratch fits the C tile");
   using E = typename Op<P>::T;
   __shared__ __attribute__((aligned(16))) E smem[(STG > EPI ? STG : EPI) / sizeof(E)];
   const int gx = (a.e.Nout + 127) / 128;
@@ -649,28 +659,34 @@ __global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
   const int wm = w >> 1, wn = w & 1;
   NnRows R;
 #pragma unroll
-  for (int c = 0; c < nn_rows_per_thread<P>(); ++c) {
-    const int r = nn_row<P>(c), rs = r / PT, rt = r % PT;
+  for (int c = 0; c < nn_rows_per_thread<BK>(); ++c) {
+    const int r = nn_row<BK>(c), rs = r / PT, rt = r % PT;
     R.va[c] = rs < S && pt0 + rt < a.e.Npts;
     R.a[c] = ((long long)rs * a.e.Npts + pt0 + rt) * a.K;
     R.b[c] = (long long)(n0 + r) * a.K;
     R.vb[c] = n0 + r < a.e.Nout;
   }
   f32x4 acc[4][4];
-  nn_loop<P>(smem, (const E*)a.Ah, (const E*)a.Al, (const E*)a.Bh, (const E*)a.Bl, R, a.K, a.vec != 0, acc);
-  __syncthreads();  // every wave is done with the staging buffers
+  nn_loop<P, BK>(smem, (const E*)a.Ah, (const E*)a.Al, (const E*)a.Bh, (const E*)a.Bl, R, a.K, a.vec != 0, acc);
   float* sC = reinterpret_cast<float*>(smem);
+  const int f4 = (tid % (CW / 4)) * 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int hh = 0; hh < (HALF ? 2 : 1); ++hh) {
+    __syncthreads();  // staging buffers (first pass) / the previous half's readers are done
+    if (!HALF || wn == hh) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sC[(wm * 64 + 16 * i + 4 * g + r) * EPI_CS + wn * 64 + 16 * j + p] = acc[i][j][r];
-  __syncthreads();
-  const int f4 = (tid & 31) * 4;
-  lay_epilogue<S, MODE, P == 2>(a.e, ty, n0, [&](int s, int t) {
-    return *reinterpret_cast<const f32x4*>(&sC[(s * PT + t) * EPI_CS + f4]);
-  }, sC);
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sC[(wm * 64 + 16 * i + 4 * g + r) * CS + (HALF ? 0 : wn * 64) + 16 * j + p] = acc[i][j][r];
+    }
+    __syncthreads();
+    lay_epilogue<S, MODE, P == 2, CW>(a.e, ty, n0 + 64 * hh, [&](int s, int t) {
+      return *reinterpret_cast<const f32x4*>(&sC[(s * PT + t) * CS + f4]);
+    }, sC);
+  }
 }
 
 // The input layer forward without a GEMM: Z = X K0 (d_in <= 8 exact fp32 columns), the first-order

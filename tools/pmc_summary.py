@@ -12,9 +12,10 @@ def main():
     root = sys.argv[1]
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.defaultdict(int)
-    for f in sorted(glob.glob(f"{root}/pmc*/*/*counter_collection.csv")):
+    for f in sorted(glob.glob(f"{root}/pmc*/**/*counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0][:40]
+            k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+            k = k.split("(")[0][:48]
             key = (k, r["Counter_Name"])
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             cnt[key] += 1
