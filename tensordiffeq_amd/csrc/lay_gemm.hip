@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(256) lay_nn2_kernel(const __bf16* __restrict__
 //             first-order streams' dK0 rows) and X^T zb (dK0 = X^T ZB0 over the d_in <= 8 exact
 //             fp32 coordinates)
 // Partials: part[tile_y][q][Nout], q < 1 (EPI_BWD) or S + d_in (EPI_BWD0), summed by the caller.
-enum { EPI_FWD = 0, EPI_BWD = 1, EPI_BWD0 = 2 };
+enum { EPI_FWD = 0, EPI_BWD = 1, EPI_BWD0 = 2, EPI_FWDJ = 3 };  // FWDJ: EPI_FWD + the output layer's J dots
 
 struct EpiArgs {
   int Npts, Nout, d_in;
@@ -496,6 +496,11 @@ struct EpiArgs {
   __bf16 *Oh, *Ol;           // EPI_FWD / EPI_BWD outputs [S * Npts][Nout] (Ol nullable in EPI_BWD)
   const float* H32;          // fp32 engine (F32): the saved post-activations, one fp32 plane
   float* O32;                // fp32 engine: the output plane
+  // EPI_FWD of the last hidden layer (nullable): the output layer's J = H Ko fused in - per
+  // 64-column group partial dots jpart[col / 64][s][n][q] (the caller sums the groups, adds bo)
+  const float* Ko;           // [Nout][d_out]
+  float* jpart;
+  int d_out;
   float* part;               // EPI_BWD* partials (nullable in EPI_BWD)
   const float* X;            // EPI_BWD0: [Npts][d_in]
   LSpec sp;
@@ -507,8 +512,10 @@ struct EpiArgs {
 // activations / adjoints are single fp32 planes (H32 / O32) instead of bf16 hi / lo pairs.
 // CW: feature columns per call (128, or 64 when a GEMM tile's epilogue runs in two column halves
 // to halve its LDS tile); CW / 4 threads cover a row, 1024 / CW rows per pass.
-template <int S, int MODE, bool F32, int CW = 128, class Src>
+template <int S, int MODE_, bool F32, int CW = 128, class Src>
 __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, Src src, float* red) {
+  constexpr bool JDOT = MODE_ == EPI_FWDJ;
+  constexpr int MODE = JDOT ? (int)EPI_FWD : MODE_;
   constexpr int PT = 128 / S;
   constexpr int NS = MODE == EPI_BWD0 ? S : 1;
   constexpr int NX = MODE == EPI_BWD0 ? TDQ_MAXD : 1;
@@ -528,10 +535,21 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
 #pragma unroll
     for (int v = 0; v < 4; ++v) bb[v] = e.bias[col + v];
   }
+  float ko[JDOT ? TDQ_MAXO : 1][4];
+#pragma unroll
+  for (int q = 0; q < (JDOT ? TDQ_MAXO : 1); ++q)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) ko[q][v] = (JDOT && cok && q < e.d_out) ? e.Ko[(long long)(col + v) * e.d_out + q] : 0.f;
   auto point = [&](int t) {
     const int n = pt0 + t;
-    if (!cok || n >= e.Npts) return;
-    float x[S][4], y[S][4];
+    const bool ok = cok && n < e.Npts;
+    float y[S][4];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) y[s][v] = 0.f;
+    if (ok) {
+    float x[S][4];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const f32x4 q = src(s, t);
@@ -586,6 +604,23 @@ __device__ __forceinline__ void lay_epilogue(const EpiArgs& e, int ty, int n0, S
           }
           *reinterpret_cast<bf16x4*>(e.Oh + o) = hv;
           if (e.Ol != nullptr) *reinterpret_cast<bf16x4*>(e.Ol + o) = lv;
+        }
+      }
+    }
+    }  // ok
+    if constexpr (JDOT) {
+      {  // J partials of this row's 64-column group: a 16-lane reduction (whole groups share t)
+#pragma unroll
+        for (int q = 0; q < TDQ_MAXO; ++q) {
+          if (q >= e.d_out) break;
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            float a = y[s][0] * ko[q][0] + y[s][1] * ko[q][1] + y[s][2] * ko[q][2] + y[s][3] * ko[q][3];
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) a += __shfl_xor(a, m, 64);
+            if ((tid & 15) == 0 && n < e.Npts && col < e.Nout)
+              e.jpart[(((long long)(col >> 6) * S + s) * e.Npts + n) * e.d_out + q] = a;
+          }
         }
       }
     }
@@ -646,7 +681,7 @@ __global__ void __launch_bounds__(256) lay_nnj_kernel(NnjArgs a) {
   // bf16 forward / hidden adjoint: the C tile through LDS in two 64-column halves (40 KB of LDS in
   // all, so 3-4 workgroups per CU instead of 2: forward 238 vs 278 us at W512); the other modes and
   // precisions keep the whole tile (two halves measured slower there: profiles/r5lay7_*)
-  constexpr bool HALF = P == 0 && MODE != EPI_BWD0;
+  constexpr bool HALF = P == 0 && MODE != EPI_BWD0;  // (EPI_FWDJ included)
   constexpr int CW = HALF ? 64 : 128, CS = CW + 4;
   constexpr int EPI = 128 * CS * 4;
   static_assert(4 * (TDQ_MAXS + TDQ_MAXD) * CW * 4 <= EPI, "partials scratch fits the C tile");
@@ -999,6 +1034,9 @@ static bool epi_args(EpiArgs& e, int S, const int* spec, int Npts, int Nout, int
   e.Ol = f32 ? nullptr : (__bf16*)Ol;
   e.H32 = f32 ? (const float*)Hh : nullptr;
   e.O32 = f32 ? (float*)Oh : nullptr;
+  e.Ko = nullptr;
+  e.jpart = nullptr;
+  e.d_out = 0;
   return true;
 }
 
@@ -1009,10 +1047,13 @@ static long long epi_tiles(int S, int Npts, int Nout) {
 // prec 0 bf16 / 1 bf16x3 / 2 fp32; mode: EPI_FWD (bias, Oh, Ol), EPI_BWD (Hh, Hl, Oh, Ol nullable,
 // part nullable [tiles_y][1][Nout]), EPI_BWD0 (Hh, Hl, part [tiles_y][S + d_in][Nout], X [Npts][d_in]);
 // tiles_y = ceil(Npts / (128 / S)).  fp32: A / B fp32, Hh / Oh single fp32 planes, Hl / Ol unused.
+// EPI_FWD with jpart: the output layer's J partials (Ko [Nout][d_out], d_out <= 4; jpart
+// [ceil(Nout / 64)][S][Npts][d_out]).
 // Planes are contiguous: A [S * Npts][K], B^T [Nout][K], H / outputs [S * Npts][Nout].
 int tdq_lay_nnj(int prec, int mode, int S, const int* spec, const void* Ah, const void* Al, const void* Bh,
                 const void* Bl, int Npts, int K, int Nout, const float* bias, const void* Hh, const void* Hl, void* Oh,
-                void* Ol, float* part, const float* X, int d_in, void* stream) {
+                void* Ol, float* part, const float* X, int d_in, const float* Ko, float* jpart, int d_out,
+                void* stream) {
   NnjArgs a;
   const bool f32 = prec == 2;
   if (prec < 0 || prec > 2 || mode < 0 || mode > 2 || K <= 0 || Ah == nullptr || Bh == nullptr ||
@@ -1026,6 +1067,12 @@ int tdq_lay_nnj(int prec, int mode, int S, const int* spec, const void* Ah, cons
   a.e.bias = bias;
   a.e.part = part;
   a.e.X = X;
+  if (jpart != nullptr && (mode != EPI_FWD || Ko == nullptr || d_out < 1 || d_out > TDQ_MAXO))
+    return (int)hipErrorInvalidValue;
+  const int kmode = (mode == EPI_FWD && jpart != nullptr) ? (int)EPI_FWDJ : mode;
+  a.e.Ko = Ko;
+  a.e.jpart = jpart;
+  a.e.d_out = d_out;
   a.Ah = Ah; a.Al = Al; a.Bh = Bh; a.Bl = Bl;
   a.K = K;
   a.vec = f32 ? (aligned16<float>(Ah, K) && aligned16<float>(Bh, K))
@@ -1036,11 +1083,12 @@ int tdq_lay_nnj(int prec, int mode, int S, const int* spec, const void* Ah, cons
   const dim3 grid((unsigned)tiles);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define TDQ_NNJ_M(P_, S_, M_) hipLaunchKernelGGL((lay_nnj_kernel<P_, S_, M_>), grid, dim3(256), 0, st, a)
-#define TDQ_NNJ(P_, S_)                                   \
-  case S_:                                                \
-    if (mode == EPI_FWD) TDQ_NNJ_M(P_, S_, EPI_FWD);      \
-    else if (mode == EPI_BWD) TDQ_NNJ_M(P_, S_, EPI_BWD); \
-    else TDQ_NNJ_M(P_, S_, EPI_BWD0);                     \
+#define TDQ_NNJ(P_, S_)                                    \
+  case S_:                                                 \
+    if (kmode == EPI_FWD) TDQ_NNJ_M(P_, S_, EPI_FWD);      \
+    else if (kmode == EPI_FWDJ) TDQ_NNJ_M(P_, S_, EPI_FWDJ); \
+    else if (kmode == EPI_BWD) TDQ_NNJ_M(P_, S_, EPI_BWD); \
+    else TDQ_NNJ_M(P_, S_, EPI_BWD0);                      \
     break;
 #define TDQ_NNJ_P(P_)                                                                                         \
   switch (S) {                                                                                                \

@@ -69,7 +69,7 @@ def _declare(lib):
         "tdq_lay_tn": (I, [I, P, P, L, P, P, L, P, I, I, I, I, P]),
         "tdq_lay_xtz": (I, [P, I, P, I, I, P, I, P]),
         "tdq_lay_xtz2": (I, [P, I, P, P, P, I, I, P, I, P]),
-        "tdq_lay_nnj": (I, [I, I, I, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, I, P]),
+        "tdq_lay_nnj": (I, [I, I, I, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, I, P, P, I, P]),
         "tdq_lay_in_fwd": (I, [I, I, P, P, I, P, P, I, I, P, P, P]),
         "tdq_lay_out_bwd": (I, [I, I, I, P, P, I, P, P, P, I, I, P, P, P, P, I, P]),
         "tdq_adam_multi": (I, [P, I, P, P, P]),

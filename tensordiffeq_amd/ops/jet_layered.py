@@ -236,13 +236,15 @@ def _hl(H):
     return H if isinstance(H, tuple) else (H, None)
 
 
-def _nnj(mode, prec, spec, S, N, a, bt, bias=None, H=None, part=None, X=None):
+def _nnj(mode, prec, spec, S, N, a, bt, bias=None, H=None, part=None, X=None, ko=None, jpart=None):
     """One NN GEMM with the layer jet in its epilogue (csrc/lay_gemm.hip ``lay_nnj_kernel``): ``a``
     the :class:`_Op` of the layer input planes [S*N, K], ``bt`` the fp32 B^T [Nout, K].  Returns the
     (hi, lo) bf16 output planes: EPI_FWD the layer's post-activations (lo always - it is the saved
     activation's residual), EPI_BWD its ZB (lo in bf16x3 only; ``part`` the bias partials),
     EPI_BWD0 nothing (``part`` the input layer's gradient partials, ``X`` its coordinates).  fp32:
-    one fp32 output plane as ``(plane, None)``, ``H`` the fp32 plane."""
+    one fp32 output plane as ``(plane, None)``, ``H`` the fp32 plane.  EPI_FWD of the last hidden
+    layer may also take the output layer (``ko`` [Nout, d_out], ``jpart`` [ceil(Nout / 64), S, N,
+    d_out]): J's partial dots per 64-column group come out of the same epilogue."""
     ah, al = _planes(a)
     bo = _Op(bt.contiguous(), prec) if prec != "fp32" else None
     bh, bl = _planes(bo) if bo is not None else (bt.contiguous(), None)
@@ -257,7 +259,8 @@ def _nnj(mode, prec, spec, S, N, a, bt, bias=None, H=None, part=None, X=None):
     lib = _lib.load(required=True)
     rc = lib.tdq_lay_nnj(_PREC[prec], mode, S, _spec_c(spec), _lib.ptr(ah), _lib.ptr(al), _lib.ptr(bh), _lib.ptr(bl),
                          N, K, Nout, _lib.ptr(bias), _lib.ptr(hh), _lib.ptr(hl), _lib.ptr(oh), _lib.ptr(ol),
-                         _lib.ptr(part), _lib.ptr(X), 0 if X is None else X.shape[1], _lib.stream_ptr(dev))
+                         _lib.ptr(part), _lib.ptr(X), 0 if X is None else X.shape[1], _lib.ptr(ko), _lib.ptr(jpart),
+                         0 if ko is None else ko.shape[1], _lib.stream_ptr(dev))
     _lib.check(rc, "tdq_lay_nnj")
     return oh, ol
 
@@ -342,12 +345,21 @@ def forward_raw(X, P, net, plan, precision="fp32"):
 
         h, o = saved(hi, lo)
         Hs, Ho = [h], [o]
-        for K, b in ws[1:-1]:
-            h, o = saved(*_nnj(EPI_FWD, precision, spec, S, N, Ho[-1], K.t(), bias=b))
+        Ko, bo = ws[-1]
+        d_out = Ko.shape[1]
+        jpart = None
+        for i, (K, b) in enumerate(ws[1:-1]):
+            kw = {}
+            if i == len(ws) - 3 and d_out <= 4:   # the last hidden layer also forms J = H Ko
+                jpart = torch.empty((-(-K.shape[1] // 64), S, N, d_out), dtype=torch.float32, device=X.device)
+                kw = {"ko": Ko.contiguous(), "jpart": jpart}
+            h, o = saved(*_nnj(EPI_FWD, precision, spec, S, N, Ho[-1], K.t(), bias=b, **kw))
             Hs.append(h)
             Ho.append(o)
-        Ko, bo = ws[-1]
-        J = _mm_w(Ho[-1], Ko, precision).view(S, N, Ko.shape[1])
+        if jpart is not None:
+            J = jpart.sum(dim=0)
+        else:
+            J = _mm_w(Ho[-1], Ko, precision).view(S, N, d_out)
         J[0] += bo
         return J, ("layered", X, P, net, spec, Hs, Ho, precision, fused)
     Z = torch.zeros((S, N, W0), dtype=P.dtype, device=X.device)
