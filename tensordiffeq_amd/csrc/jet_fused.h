@@ -558,8 +558,13 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       if constexpr (MODE == 2) {
         // ---- J of the tile's points: the wave-ordered sums of the partial dots, in place of wave
         // 0's (each (stream, point) entry read and written by one thread) ----------------------
-        if (tid < S * FZ_PT) {
-          const int s = tid / FZ_PT, pt = tid - s * FZ_PT;
+        // (the thread index goes through an opaque copy here and at the loss call: the addresses
+        // derived from it would otherwise be hoisted out of the tile loop and, at 256 VGPRs,
+        // spilled - a scratch reload + full vmcnt wait per address on the loss's critical path)
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+        if (tl < S * FZ_PT) {
+          const int s = tl / FZ_PT, pt = tl - s * FZ_PT;
           float a = outp[((0 * S + s) * FZ_PT + pt) * OQ];
 #pragma unroll
           for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * OQ];
@@ -569,7 +574,9 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
         // ---- the per-point loss (generated code: every loss group of the program - residual, SA
         // weighting, boundary terms with the two points of a periodic pair side by side - and its
         // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
-        if (tid < FZ_PT) LossF::template eval<S, OQ>(outp, xs, tid, pb + tid, N, *P.lptrs, lpre, ubs, lacc);
+        tl = tid;
+        asm volatile("" : "+v"(tl));
+        if (tl < FZ_PT) LossF::template eval<S, OQ>(outp, xs, tl, pb + tl, N, *P.lptrs, lpre, ubs, lacc);
         __syncthreads();
         FZ_TS(9);
         // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
