@@ -609,10 +609,12 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
         }
         __syncthreads();
       }
-      if (w == 0 && l < 4) {  // dbo (ubs is complete since the tile's first barriers)
+      int ll = l;
+      asm volatile("" : "+v"(ll));  // (its addresses recomputed per tile, not hoisted and spilled)
+      if (w == 0 && ll < 4) {  // dbo (ubs is complete since the tile's first barriers)
         float a = 0.f;
-        for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + l];
-        accBo[l] += a;
+        for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + ll];
+        accBo[ll] += a;
       }
       // ---- hidden layers LM..1: dK_l, hb_{l-1} = K_l zb_l, adjoint of tanh layer l-1 --------
 #pragma unroll
