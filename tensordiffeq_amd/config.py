@@ -8,12 +8,7 @@ field                  env var                     meaning
 backend                TDQ_BACKEND                 auto | hip | jet | autograd
 precision              TDQ_PRECISION               bf16x3 (split-bf16 MFMA) | bf16 (bf16 MFMA operands,
                                                    fp32 accumulate / jets / master weights) | fp32
-newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision;
-                                                   "bf16w": bf16 activations with the weights' hi + lo
-                                                   parts, on the fused step - ops/fused_step.py;
-                                                   gradient 4e-4 vs fp64 (bf16 3e-3, bf16x3 8e-6), but
-                                                   the fixed-step L-BFGS diverges on AC-SA with it:
-                                                   profiles/r5wlo2_bf16w_lbfgs.json - experimental)
+newton_precision       TDQ_NEWTON_PRECISION        jet precision of the L-BFGS phase (default: precision)
 newton_schedule        TDQ_NEWTON_SCHEDULE         leading L-BFGS phases "prec:iters,..." before the
                                                    newton_precision phase (e.g. "bf16:7000")
 seed                   TDQ_SEED                    global seed applied at compile
@@ -31,7 +26,9 @@ force_dp               TDQ_FORCE_DP=1              DP machinery (process group, 
                                                    even at world 1 (parallel/dist.py)
 dp_graph               TDQ_DP_GRAPH=0 disables     RCCL all-reduce captured inside the step graph
 nan_check              TDQ_NAN_CHECK=0 disables    device loss-history NaN/Inf scan (fit.py)
-(split)                TDQ_SPLIT                   auto (cut at 0.45 for bf16, 0.35 for bf16x3) | off | cut
+(fused_step)           TDQ_FUSED_STEP=0 disables   one-launch forward -> loss -> backward (bf16 Adam
+                                                   step, bf16x3 L-BFGS objective; ops/fused_step.py)
+(split)                TDQ_SPLIT                   auto (cut at 0.38 for bf16, 0.35 for bf16x3) | off | cut
                                                    fraction: two point ranges on concurrent graph
                                                    branches (fit.point_ranges)
 (lbfgs_fused)          TDQ_LBFGS_FUSED=0           five-launch L-BFGS update instead of two
@@ -107,7 +104,7 @@ class SolverConfig:
             raise ValueError(f"backend {self.backend!r}")
         if self.precision not in ("bf16x3", "bf16", "fp32"):
             raise ValueError(f"precision {self.precision!r}")
-        if self.newton_precision not in (None, "bf16x3", "bf16", "bf16w", "fp32"):
+        if self.newton_precision not in (None, "bf16x3", "bf16", "fp32"):
             raise ValueError(f"newton_precision {self.newton_precision!r}")
         parse_newton_schedule(self.newton_schedule)
         if self.log_every < 1:
@@ -131,7 +128,7 @@ def parse_newton_schedule(spec):
     out = []
     for part in str(spec).split(","):
         prec, _, n = part.strip().partition(":")
-        if prec not in ("bf16x3", "bf16", "bf16w", "fp32") or not n.strip().isdigit():
+        if prec not in ("bf16x3", "bf16", "fp32") or not n.strip().isdigit():
             raise ValueError(f"newton_schedule entry {part!r}: want precision:iterations")
         out.append((prec, int(n)))
     return out

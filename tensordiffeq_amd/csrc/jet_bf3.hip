@@ -13,7 +13,7 @@
 //                 weights snapshot, and the next step's weight images: every updated weight is
 //                 scattered straight into its forward / backward A-image (bf16 hi + lo) or aux
 //                 slot, so the next forward runs without a pack launch.
-#include "jet_fused.h"
+#include "jet_fused3.h"
 #include "optim_common.h"
 
 // A-operand images: img[layer-1][o][kb][hl][lane] = 8 bf16 (hl 0 = hi, 1 = lo)
@@ -279,7 +279,6 @@ int64_t stage_floats(int N, int WT, int S, int lo) {  // the wide bf16x3 plans' 
 
 // gradient-slab rows of a backward over N points
 int bf3_rows(int N, const NetDims& d, int WT, int S, int lo) {
-  if (fz_active(d, WT, S, lo)) return fz_rows(N);
   const int pts_b = 16 * bwd_waves(WT, lo != 0, S);
   return (N + pts_b - 1) / pts_b;
 }
@@ -317,8 +316,7 @@ int dispatch(bool fwd, int WT, int S, int nso, const Bf3Args& a) {
 extern "C" {
 
 // scratch = forward A image | backward A image | aux image | (wide bf16x3 plans) the global
-// fragment stage | saved post-activations Hs (none when the persistent kernels of jet_fused.h
-// serve the plan: they keep every activation on chip) - floats; -1: unsupported.  The forward
+// fragment stage | saved post-activations Hs - floats; -1: unsupported.  The forward
 // packs all three images in one launch; the backward reuses them.
 int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, const int* widths, int n_hidden, int S, int lo) {
   NetDims d;
@@ -326,19 +324,21 @@ int64_t tdq_jet_bf3_scratch_floats(int N, int d_in, const int* widths, int n_hid
   const int WT = width_tiles(d.width);
   if (WT < 2) return -1;
   const int64_t nwg = (N + 63) / 64;
-  const int64_t hs = fz_active(d, WT, S, lo) ? 0 : (int64_t)n_hidden * nwg * S * 4 * WT * 256;
+  const int64_t hs = (int64_t)n_hidden * nwg * S * 4 * WT * 256;
   return hs + 2 * img_floats(WT, n_hidden) + aux_alloc(d_in, n_hidden, 16 * WT) + stage_floats(N, WT, S, lo);
 }
 
 // per-workgroup gradient slabs + reduction partials, in floats (rows: the saved-activation
-// backward's 64-point workgroups or the persistent kernels' workgroups, whichever is more)
+// backward's 64-point workgroups or the fused step's workgroups, whichever is more)
 int64_t tdq_jet_bf3_slab_floats(int N, int d_in, const int* widths, int d_out, int n_hidden) {
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return -1;
   const int WT = width_tiles(d.width);
   if (WT < 2) return -1;
   int nwg = (N + 63) / 64;
-  if (fz_rows(N) > nwg) nwg = fz_rows(N);
+  // the fused step's rows: at most one workgroup per CU, at most one per 16-point tile
+  const int fz = (N + 15) / 16 < fz_cus() ? (N + 15) / 16 : fz_cus();
+  if (fz > nwg) nwg = fz;
   const int64_t P = slab_stride(param_count(d));
   return ((int64_t)nwg + slab_chunks(nwg)) * P;
 }
@@ -390,8 +390,6 @@ int tdq_jet_fwd_bf3_range(const float* X, const float* P, float* J, float* scrat
   const int nso = spec_nso(S, spec);
   if (nso < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const bool fz = fz_active(d, WT, S, lo);
-  if (fz && (p_lo != 0 || p_hi != N)) return (int)hipErrorInvalidValue;  // one launch over every point
   float* Hs = scratch_hs(scratch, N, d_in, n_hidden, S, WT, lo);
   float *img, *bimg, *aux;
   scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
@@ -399,9 +397,6 @@ int tdq_jet_fwd_bf3_range(const float* X, const float* P, float* J, float* scrat
     int rc = launch_pack(P, reinterpret_cast<bf16x8*>(img), reinterpret_cast<bf16x8*>(bimg), aux, d, WT, st);
     if (rc) return rc;
   }
-  if (fz)
-    return fz_launch(0, X, aux, reinterpret_cast<const bf16x8*>(img), reinterpret_cast<const bf16x8*>(bimg), nullptr, J,
-                     nullptr, N, 0, d, sp, S, nso, st);
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(img), nullptr, J, Hs, nullptr, N, 0, d, sp, st, lo,
             scratch_stage(scratch, N, d_in, n_hidden, S, WT, lo), p_lo, p_hi};
   return dispatch(true, WT, S, nso, a);
@@ -452,11 +447,6 @@ int tdq_jet_bwd_bf3_range(const float* X, const float* dJ, const float* Hs, floa
   float* scr = const_cast<float*>(Hs);
   float *img, *bimg, *aux;
   scratch_images(scr, n_hidden, WT, &img, &bimg, &aux);
-  if (fz_active(d, WT, S, lo)) {  // recompute backward: activations rebuilt on chip, tile by tile
-    if (p_lo != 0 || p_hi != N) return (int)hipErrorInvalidValue;
-    return fz_launch(1, X, aux, reinterpret_cast<const bf16x8*>(img), reinterpret_cast<const bf16x8*>(bimg), dJ,
-                     nullptr, work, N, slab_stride(Ptot), d, sp, S, nso, st);
-  }
   // slab rows use the 16-byte aligned stride that tdq_slab_reduce's float4 passes assume
   Bf3Args a{X, aux, reinterpret_cast<const bf16x8*>(bimg), dJ, nullptr, scratch_hs(scr, N, d_in, n_hidden, S, WT, lo),
             work, N, slab_stride(Ptot), d, sp, st, lo, scratch_stage(scr, N, d_in, n_hidden, S, WT, lo), p_lo, p_hi};
@@ -577,7 +567,7 @@ int tdq_dp_tail_a_bf3(float* work, float* grad, int N, int d_in, const int* widt
   tb.losses = losses;
   tb.dscal = dscal;
   tb.total = total;
-  const int half = half_ovr >= 0 ? (half_ovr != 0) : (int)slab_half(lo != 0);  // (fused step bf16w: fp32 rows)
+  const int half = half_ovr >= 0 ? (half_ovr != 0) : (int)slab_half(lo != 0);
   const int nqb = (Pst / (half ? 8 : 4) + 255) / 256, nq2 = (Pst / 4 + 255) / 256;
   hipLaunchKernelGGL(tail_reduce1_kernel, dim3(nqb + 1, chunks - c_first), dim3(256), 0, st, work, part, nwg_b, Pst,
                      chunks, nqb, half, c_first, tb);
@@ -594,8 +584,7 @@ int tdq_bf3_slab_geometry(int N, int d_in, const int* widths, int d_out, int n_h
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
   if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || N < 1) return (int)hipErrorInvalidValue;
-  const bool fz = fz_active(d, WT, S, lo);
-  const int pts_b = fz ? N : 16 * bwd_waves(WT, lo != 0, S), nwg_b = bf3_rows(N, d, WT, S, lo),
+  const int pts_b = 16 * bwd_waves(WT, lo != 0, S), nwg_b = bf3_rows(N, d, WT, S, lo),
             chunks = slab_chunks(nwg_b);
   out[0] = pts_b;
   out[1] = nwg_b;
@@ -659,18 +648,25 @@ int tdq_dp_tail_b_bf3(float* scratch, int N, int d_in, const int* widths, int d_
   return 0;
 }
 
-// One launch of a run-time compiled fused training step (csrc/jet_fused.h MODE 2, ops/fused_step.py):
-// forward -> the residual group's loss -> recompute backward over the points [p_lo, N), G
-// workgroups, gradient-slab rows srow.., loss-partial rows prow.. (nacc floats each)
+// One launch of a run-time compiled fused training step (ops/fused_step.py; lo = 0: the bf16 step of
+// csrc/jet_fused.h, 32-point tiles; lo = 1: the bf16x3 objective of csrc/jet_fused3.h, 16-point
+// tiles): forward -> loss -> backward over the points [p_lo, N), G workgroups, gradient-slab rows
+// srow.., loss-partial rows prow.. (nacc floats each)
 int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* work, int N, int d_in, const int* widths,
                           int d_out, int n_hidden, int S, const int* spec, int p_lo, int srow, int G, const void* lptrs,
-                          float* lpart, int prow, int nacc, int seg_lo, int* tctr, void* stream) {
-  if (func == nullptr || N <= 0 || p_lo < 0 || p_lo >= N || G < 1 || srow < 0 || prow < 0 || nacc < 1)
+                          float* lpart, int prow, int nacc, int lo, void* stream) {
+  if (func == nullptr || N <= 0 || p_lo < 0 || p_lo >= N || G < 1 || srow < 0 || prow < 0 || nacc < 1 || lo < 0 ||
+      lo > 1)
     return (int)hipErrorInvalidValue;
   NetDims d;
   if (!make_dims(d, d_in, widths, 0, d_out, n_hidden)) return (int)hipErrorInvalidValue;
   const int WT = width_tiles(d.width);
-  if (!bf3_ok(WT, S, d_in, d_out, n_hidden)) return (int)hipErrorInvalidValue;
+  // the kernels' geometry (also what the LDS size was computed for): width 128, 2-3 MFMA layers
+  if (!bf3_ok(WT, S, d_in, d_out, n_hidden) || tdq_jet_fused_lds(d_in, widths, d_out, n_hidden, S, lo) < 0)
+    return (int)hipErrorInvalidValue;
+  const int PT = lo ? FZ3_PT : FZ_PT;
+  // at most one workgroup per tile: every workgroup owns at least one tile
+  if (G > (N - p_lo + PT - 1) / PT) return (int)hipErrorInvalidValue;
   JetSpec sp;
   if (spec_nso(S, spec) < 0 || !make_spec(S, spec, sp)) return (int)hipErrorInvalidValue;
   float *img, *bimg, *aux;
@@ -683,7 +679,7 @@ int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* wor
   P.slab = work;
   P.N = N;
   P.Pst = slab_stride(param_count(d));
-  P.ntiles = (N - p_lo + FZ_PT - 1) / FZ_PT;
+  P.ntiles = (N - p_lo + PT - 1) / PT;
   P.p_lo = p_lo;
   P.srow = srow;
   P.d = d;
@@ -692,8 +688,6 @@ int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* wor
   P.lpart = lpart;
   P.prow = prow;
   P.nacc = nacc;
-  P.seg_lo = seg_lo;
-  P.tctr = tctr;  // (the dynamic-queue kernels only; nullable otherwise)
   void* args[] = {(void*)&P};
   return (int)hipModuleLaunchKernel((hipFunction_t)func, (unsigned)G, 1, 1, 64 * FZ_WAVES, 1, 1, 0,
                                     reinterpret_cast<hipStream_t>(stream), args, nullptr);

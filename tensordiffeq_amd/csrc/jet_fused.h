@@ -1,36 +1,41 @@
-// Persistent point-tile jet kernels for precision "bf16" (gfx950 / MI355X): the forward of a
-// whole point set, and the RECOMPUTE backward - forward of a 32-point tile with every activation
-// kept on chip (LDS images + registers), then the reverse sweep through the same tile - with the
-// weight gradient dK of every hidden layer accumulated in MFMA accumulator registers across all
-// of a workgroup's tiles.
+// One-launch training step for precision "bf16" (gfx950 / MI355X): a persistent point-tile kernel
+// that runs, per 32-point tile, the Taylor-jet forward of the network with every activation kept on
+// chip (LDS images + registers), the per-point loss of the traced loss program (generated C++,
+// compiled with hipRTC: ops/fused_step.py) and its reverse sweep, and the recompute-free backward -
+// with the weight gradient dK of every hidden layer accumulated in MFMA accumulator registers
+// across all of a workgroup's tiles.
 //
 // Why (profiles/r3_roofline_bf16.txt): the saved-activation design streams
 // 4.35 KB per point out of the forward and back into the backward (223 + 268 MB per 50k-point
 // step) at 2-4 TB/s, with the backward at 12 % MFMA busy and two wave rounds per launch.  Here:
-//   * one workgroup (4 waves, one per SIMD, the 512-entry register file each) per CU, a static
-//     contiguous share of 32-point tiles per workgroup (deterministic summation order);
+//   * one workgroup (8 waves, two per SIMD) per CU, a static contiguous share of 32-point tiles per
+//     workgroup (deterministic summation order);
 //   * per tile, the forward writes each layer's post-activation streams into [point][feature]
 //     bf16 LDS images - the B operand of the next layer's GEMM (two ds_read_b64 per fragment in
 //     the permuted k order of the weight images) and, read transposed (ds_read_b64_tr_b16), the
 //     A operand of the backward's dK = sum_points sum_streams h_{l-1} zb_l^T;
 //   * the value stream keeps a bf16 "lo" image beside its hi image (hi + lo ~ 2^-17 relative) for
-//     the tanh-jet adjoint's s1 = 1 - h^2; the top layer stays in registers (fp32);
+//     the tanh-jet adjoint's s1 = 1 - h^2;
 //   * the reverse sweep writes each zb_l in place of h_l once every wave's dK_{l+1} has read
 //     h_l; layer 0 (input -> width, VALU) is rebuilt from x instead of being kept;
-//   * dK_l (l = 1..LM) lives in AGPR-able accumulators for the whole launch (WT = 8: 192 per
-//     lane); vector-parameter partials (biases, first / output layer) accumulate in LDS; one
-//     bf16 gradient-slab row per workgroup at the end (256 rows instead of 391 for 50k points),
-//     reduced by the existing fused step tail.
-// No saved-activation traffic at all: the backward reads x, dJ and the (L2-resident) weight images.
-// Numerics: the forward is statement-for-statement the saved-activation forward (same bf16
-// operands, same MFMA k order, same tanh jet), so J is bitwise the same; dK sums in another order.
+//   * dK_l (l = 1..LM) lives in accumulators for the whole launch; vector-parameter partials
+//     (biases, first / output layer) accumulate in LDS; one bf16 gradient-slab row and one loss-
+//     partial row per workgroup at the end, reduced by the fused step tail (jet_bf3.hip).
+// No activation or jet traffic through HBM: the kernel reads x, the loss inputs and the
+// (L2-resident) weight images.
+// Removed after measurement (tools/patches/fused_step_experiments_REMOVED.patch, A/B notes there):
+// the MODE 0 / 1 forward-only and backward-only persistent launches (TDQ_FUSED=1), the dynamic
+// tile queue (TDQ_FS_DYNAMIC), the loss inputs prefetched a tile ahead (TDQ_FS_PREFETCH), the
+// cheap tanh in the hidden layers (FZ_CHEAP_TANH) and the weight-lo "bf16w" objective (WLO).
+// The L-BFGS objective in bf16x3 runs the 16-point-tile kernel of jet_fused3.h.
 // Reference behaviour: the nested tf.gradients of the PDE residual and its tape.gradient
 // (tensordiffeq/models.py:116-225, fit.py:125-147).
 #pragma once
 #include "jet_bf3.h"
 
-// Phase stamps (-DTDQ_PHASE_TIMING build, tools/fused_timing.py): the phases of tile t0 + FZ_TS_TILE
-// of every workgroup (0: the first, cold tile; 1: a steady-state one) and the whole tile loop, per wave
+// Phase stamps (-DTDQ_PHASE_TIMING build, tools/fused_step_timing.py): the phases of tile
+// t0 + FZ_TS_TILE of every workgroup (0: the first, cold tile; 1: a steady-state one) and the whole
+// tile loop, per wave
 #ifndef FZ_TS_TILE
 #define FZ_TS_TILE 0
 #endif
@@ -47,77 +52,32 @@ __host__ __device__ constexpr int fz_nslot(int LM) { return LM < 2 ? 2 : LM; }
 __host__ __device__ constexpr int fz_img_elems(int WT, int S, int LM) {
   return (S + 1) * fz_nslot(LM) * FZ_PT * bf3_img_rs(WT);
 }
-// output-layer partial-dot columns per point: d_out <= 4 (MODE 0), 1 (MODE 2: the fused loss is scalar)
-__host__ __device__ constexpr int fz_oq(int mode) { return mode == 2 ? 1 : 4; }
-// float area after the images: aux copy | xs | ubs | (MODE 1, 2) per-column-tile partials (biases
-// of layers 0..LM, K0, Ko), bo | (MODE 0, 2) output-layer partial dots
+// float area after the images: aux copy | xs | ubs | per-column-tile partials (biases of layers
+// 0..LM, K0, Ko), bo | output-layer partial dots
 __host__ __device__ inline int fz_aux_floats(const NetDims& d, int W) { return (aux_floats(d, W) + 3) / 4 * 4; }
-__host__ __device__ inline int fz_fl_floats(const NetDims& d, int WT, int S, int LM, int mode) {
+__host__ __device__ inline int fz_fl_floats(const NetDims& d, int WT, int S, int LM) {
   const int W = 16 * WT;
   const int common = fz_aux_floats(d, W) + FZ_PT * TDQ_MAXD + S * FZ_PT * 4;
-  const int part = mode >= 1 ? 2 * ((LM + 1) * W + d.d_in * W + 4 * W) + 4 : 0;
-  const int outp = mode != 1 ? 4 * S * FZ_PT * fz_oq(mode) : 0;
+  const int part = 2 * ((LM + 1) * W + d.d_in * W + 4 * W) + 4;
+  const int outp = 4 * S * FZ_PT;
   return common + part + outp;
 }
-__host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int LM, int mode) {
-  return fz_img_elems(WT, S, LM) * 2 + fz_fl_floats(d, WT, S, LM, mode) * 4;
+__host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int LM) {
+  return fz_img_elems(WT, S, LM) * 2 + fz_fl_floats(d, WT, S, LM) * 4;
 }
 
-// Precision bf16 forward tanh jet with e = exp(2 min(z, 15)), r = 1 / (1 + e):
-//   tanh z = 1 - 2 r,  s1 = 1 - tanh^2 z = 4 e r^2
-// (exp, rcp and ~6 FMA-class ops instead of the ~12 of tanh_s1's polynomial / select form).  s1 is
-// formed from e, not as 1 - h^2: that cancels for saturated units, whose derivative streams
-// h_a = s1 z_a then carried 4 % error at |z| = 7 (the u_x stream of J moved by 1e-2 against the
-// saved-activation kernels, gpurun_out/r5tanh).  The clamp keeps e finite (tanh(15) = 1 - 2e-13).
-// tanh's own ~6e-8 absolute error near 0 is far below the bf16 rounding every activation takes
-// before the next GEMM.  The epilogue VALU work is as large as the layer's MFMA work at width 128
-// (4 streams: 1 MFMA cycle and ~20 VALU ops per feature x point).
-// Hidden layers: OFF by default - the AC-SA reference schedule with the fused step landed at L2
-// 2.83 / 2.99 / 3.07e-2 (seeds 0-2) with it and 2.41 / 2.29 / 1.86e-2 with the saved-activation
-// kernels' tanh_jet_f, at the same step time (profiles/r5acc_accuracy_ab.jsonl).  Layer 0 (fz_h0):
-// the cheap form stays - seeds 0-5 with it 2.41 / 2.29 / 1.86 / 2.03 / 2.59 / 2.44e-2 (median
-// 2.35e-2, the separate-launch step's 6-seed median), with tanh_s1 there 1.45 / 2.63 / 3.17 / 3.02 /
-// 3.43 / 2.57e-2 (median 2.83e-2) - profiles/r5acc2_l2_six_seeds.jsonl.  (1 - 2r has 6e-8 absolute
-// error near z = 0.)  A/B builds: TDQ_FUSED_STEP_DEFINES="-DFZ_CHEAP_TANH=1" / "-DFZ_CHEAP_H0=0".
-#ifndef FZ_CHEAP_TANH
-#define FZ_CHEAP_TANH 0
-#endif
-#ifndef FZ_CHEAP_H0
-#define FZ_CHEAP_H0 1
-#endif
-template <int S, int NSO>
-__device__ __forceinline__ void fz_tanh_jet_f(const JetSpec& sp, const f32x4 (&z)[S], f32x4 (&h)[S]) {
-  if constexpr (!FZ_CHEAP_TANH) {
-    tanh_jet_f<S, NSO>(sp, z, h);
-    return;
-  }
-  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
-  f32x4 za[S], zb[S];
-#pragma unroll
-  for (int s = SO; s < S; ++s) {
-    za[s] = sel_first<S, S1>(z, sp.ia[s], sp.selA[s]);
-    zb[s] = sel_first<S, S1>(z, sp.ib[s], sp.selB[s]);
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const float e = __builtin_amdgcn_exp2f(fminf(z[0][c], 15.f) * 2.8853900817779268f);
-    const float r = __builtin_amdgcn_rcpf(1.f + e);
-    const float hv = fmaf(-2.f, r, 1.f);
-    const float s1 = (4.f * e) * (r * r);
-    const float s2 = -2.f * hv * s1;
-    h[0][c] = hv;
-#pragma unroll
-    for (int s = 1; s < SO; ++s) h[s][c] = s1 * z[s][c];
-#pragma unroll
-    for (int s = SO; s < S; ++s) h[s][c] = fmaf(s2 * za[s][c], zb[s][c], s1 * z[s][c]);
-  }
-}
-
-// Layer 0 (input -> width, VALU) of feature tile t at one point x (LDS row), in the cheap tanh
-// form of fz_tanh_jet_f - computed three times per tile (forward, the h_0 image rebuild for dK_1,
-// the layer-0 adjoint), always by this function, so every pass sees the same h_0.  Its derivative
-// streams are rows of K0: h_a = s1 K0[a], h_ab = s2 K0[a] K0[b] (z_ab = 0).
-template <int WT, int S, int NSO>
+// Layer 0 (input -> width, VALU) of feature tile t at one point x (LDS row) - computed three times
+// per tile (forward, the h_0 image rebuild for dK_1, the layer-0 adjoint), always by this function,
+// so every pass sees the same h_0.  Its derivative streams are rows of K0: h_a = s1 K0[a],
+// h_ab = s2 K0[a] K0[b] (z_ab = 0).
+// CHEAP (the bf16 step): tanh z = 1 - 2 r, s1 = 4 e r^2 with e = exp(2 min(z, 15)), r = 1 / (1 + e)
+// (exp, rcp and ~6 FMA-class ops; s1 from e, not 1 - h^2, which cancels for saturated units).  On
+// the AC-SA reference schedule seeds 0-5 ended at L2 2.41 / 2.29 / 1.86 / 2.03 / 2.59 / 2.44e-2
+// with it (median 2.35e-2, the separate-launch step's) and 1.45 / 2.63 / 3.17 / 3.02 / 3.43 /
+// 2.57e-2 with tanh_s1 (profiles/r5acc2_l2_six_seeds.jsonl).  In the hidden layers the cheap form
+// cost accuracy (L2 median 2.99e-2, profiles/r5acc_accuracy_ab.jsonl): they use tanh_jet_f.
+// !CHEAP (the bf16x3 objective, jet_fused3.h): tanh_s1, the saved-activation kernels' tanh.
+template <int WT, int S, int NSO, bool CHEAP = true>
 __device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const NetDims& d, const float* xrow, int t,
                                       int g, f32x4 (&h)[S]) {
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
@@ -136,13 +96,13 @@ __device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     float hv, s1;
-    if constexpr (FZ_CHEAP_H0) {
+    if constexpr (CHEAP) {
       const float e = __builtin_amdgcn_exp2f(fminf(z[c], 15.f) * 2.8853900817779268f);
       const float r = __builtin_amdgcn_rcpf(1.f + e);
       hv = fmaf(-2.f, r, 1.f);
       s1 = (4.f * e) * (r * r);
     } else {
-      tanh_s1(z[c], hv, s1);   // the saved-activation kernels' tanh (layer 0 of every tile)
+      tanh_s1(z[c], hv, s1);
     }
     const float s2 = -2.f * hv * s1;
     h[0][c] = hv;
@@ -194,15 +154,14 @@ __device__ __forceinline__ f32x4 fz_bf4(bf16x4 v) {
 // acc[oo][s] = sum_kb A(o0 + oo, kb) B(kb, s) for the 16 points of column tile q: A from a weight
 // image in global memory (hi only, one k-block ahead), B from the LDS image `im` (S stream images of
 // FZ_PT rows; the SIMD's other wave covers the LDS latency).
-// WLO: the weights' bf16 lo parts too (a second MFMA per fragment; the activations stay bf16)
-template <int WT, int S, int OPW, bool WLO = false>
+template <int WT, int S, int OPW>
 __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __restrict__ wimg, int layer, int o0,
                                         const __bf16* im, int q, const FzLane& L, int l) {
   constexpr int KB = WT / 2, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS, NSTEP = WT * KB;
   const Tl Wi = tl_make(wimg + (size_t)(layer - 1) * NSTEP * 128, l);
   bf16x8 a[2][OPW], alo[2][OPW];
 #pragma unroll
-  for (int oo = 0; oo < OPW; ++oo) img_frag<WLO>(Wi, (o0 + oo) * KB, a[0][oo], alo[0][oo]);
+  for (int oo = 0; oo < OPW; ++oo) img_frag<false>(Wi, (o0 + oo) * KB, a[0][oo], alo[0][oo]);
 #pragma unroll
   for (int oo = 0; oo < OPW; ++oo)
 #pragma unroll
@@ -212,7 +171,7 @@ __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __re
     if (kb + 1 < KB) {
 #pragma unroll
       for (int oo = 0; oo < OPW; ++oo)
-        img_frag<WLO>(Wi, (o0 + oo) * KB + kb + 1, a[(kb + 1) & 1][oo], alo[(kb + 1) & 1][oo]);
+        img_frag<false>(Wi, (o0 + oo) * KB + kb + 1, a[(kb + 1) & 1][oo], alo[(kb + 1) & 1][oo]);
     }
     bf16x8 b[S];
 #pragma unroll
@@ -220,19 +179,18 @@ __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __re
 #pragma unroll
     for (int oo = 0; oo < OPW; ++oo)
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        acc[oo][s] = mfma_bf(a[kb & 1][oo], b[s], acc[oo][s]);
-        if constexpr (WLO) acc[oo][s] = mfma_bf(alo[kb & 1][oo], b[s], acc[oo][s]);
-      }
+      for (int s = 0; s < S; ++s) acc[oo][s] = mfma_bf(a[kb & 1][oo], b[s], acc[oo][s]);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // dK[r][c] += sum over the tile's points and streams of H^T Z (transposed LDS reads; the wave's
-// NR x NC block of 16 x 16 output tiles at row tiles r0.., column tiles c0..)
-template <int WT, int S, int NR, int NC, bool SB = true>
+// NR x NC block of 16 x 16 output tiles at row tiles r0.., column tiles c0..).  The k index of
+// each MFMA runs over 32 image rows: 32 points of one stream here (SIMG = FZ_PT * RS); the
+// 16-point-tile kernel of jet_fused3.h passes two streams' 16-row images as one 32-row image.
+template <int WT, int S, int NR, int NC, bool SB = true, int SIMG = FZ_PT * bf3_img_rs(WT)>
 __device__ __forceinline__ void fz_dk(f32x4 (&dk)[NR][NC], const __bf16* H, const __bf16* Z, int r0, int c0, int l) {
-  constexpr int RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
+  constexpr int RS = bf3_img_rs(WT);
   const int g = l >> 4;
   const int tr_row = 8 * g + ((l & 15) >> 2);
   const int swz = (g & 1) << 6;
@@ -272,81 +230,39 @@ struct FzParams {
   const float* aux;
   const bf16x8* fimg;   // forward A image ([out][in] k order)
   const bf16x8* bimg;   // backward A image ([in][out])
-  const float* dJ;      // MODE 1
-  float* J;             // MODE 0
-  float* slab;          // MODE 1, 2: gradient-slab rows srow + blockIdx.x
+  float* slab;          // gradient-slab rows srow + blockIdx.x
   int N, Pst, ntiles;
   int p_lo;             // the tiles cover points [p_lo, N)
   int srow;
   NetDims d;
   JetSpec sp;
-  // MODE 2: the loss program's pointer table (the generated loss maps a point to its group)
+  // the loss program's pointer table (the generated loss maps a point to its group)
   const FzLossPtrs* lptrs;
   float* lpart;         // loss / scalar-gradient partials, row prow + blockIdx.x, nacc floats each
-  int prow, nacc, seg_lo;  // (seg_lo: unused by the generated loss)
-  // MODE 2 with the dynamic tile queue (DYN): [0] next tile, [1] finished workgroups; zero at
-  // launch, re-armed by the last workgroup to finish
-  int* tctr;
+  int prow, nacc;
 };
 
-// MODE 0 / 1 builds: no loss code.  The MODE 2 interface (ops/fused_step.py generates it):
-//   prefetch(ptrs, n, N, pre): the per-point inputs of point n's loss (SA weights, data values,
-//   scalars) into registers, one tile ahead (their global latency hides behind the current tile);
-//   eval<S, OQ>(jv, xs, t, n, N, ptrs, pre, ubs, acc) on the tile's point-thread t (point n of the
-//   fused point set): J of the tile's point k, stream s at jv[(s * FZ_PT + k) * OQ], coordinates
-//   at xs[k * TDQ_MAXD + j]; writes dJ of the points it owns to ubs[(s * FZ_PT + k) * 4] (zero for
-//   points outside every loss group) and adds loss / scalar-gradient sums to acc
-struct FzNoLoss {
-  static constexpr int NACC = 1, NPRE = 1;
-  __device__ static void prefetch(const FzLossPtrs&, int, int, float (&pre)[NPRE]) { pre[0] = 0.f; }
-  template <int S, int OQ>
-  __device__ static void eval(const float*, const float*, int t, int, int, const FzLossPtrs&, const float (&)[NPRE],
-                              float* ubs, float (&)[1]) {
-#pragma unroll
-    for (int s = 0; s < S; ++s) ubs[(s * FZ_PT + t) * 4] = 0.f;
-  }
-};
-
-// MODE 0: forward only (J of every point).  MODE 1: recompute backward (dJ given -> slab rows).
-// MODE 2: forward -> per-point loss (LossF, generated from the traced program and compiled at run
-// time: ops/fused_step.py) -> backward, all in one launch (slab rows + loss partials).
+// The generated loss (ops/fused_step.py gen_loss) has this interface:
+//   NACC: loss / scalar-gradient sums per point-thread;
+//   eval<S>(jv, xs, t, n, N, ptrs, ubs, acc) on the tile's point-thread t (point n of the fused
+//   point set): J of the tile's point k, stream s at jv[s * PT + k], coordinates at
+//   xs[k * TDQ_MAXD + j]; writes dJ of the points it owns to ubs[(s * PT + k) * 4] (zero for points
+//   outside every loss group) and adds loss / scalar-gradient sums to acc.
 // Eight waves (two per SIMD, so one wave's tanh-jet VALU work runs beside the other's MFMAs):
 // wave w computes column tile q = w >> 2 (16 points) of feature tiles 2 (w & 3).. (OPW of them) in
 // every GEMM / epilogue, and owns an NR x NC block of each hidden layer's dK tiles.
-// WLO (MODE 2, the L-BFGS objective "bf16w"): weight lo parts in every GEMM and fp32 slab rows
-// LDS slots of the dynamic tile queue (allocated only by DYN instantiations)
-template <bool DYN>
-struct FzTileQ {
-  __device__ static int* slots() { return nullptr; }
-};
-template <>
-struct FzTileQ<true> {
-  __device__ static int* slots() {
-    __shared__ int q[2];
-    return q;
-  }
-};
-
-// DYN (MODE 2): tiles come from an atomic counter instead of a fixed contiguous range, so
-// workgroups that start late (CUs still held by a side-stream kernel) simply take fewer tiles.  The
-// counter is read two tiles ahead (the returned index is parked in LDS at the end of the tile), so
-// no wave waits on the atomic.
-template <int WT, int S, int NSO, int LM, int MODE, class LossF, bool WLO = false, bool DYN = false>
+template <int WT, int S, int NSO, int LM, class LossF>
 __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   const float* __restrict__ X = P.X;
   const float* __restrict__ aux_g = P.aux;
-  const float* __restrict__ dJ = P.dJ;
-  float* __restrict__ J = P.J;
   const int N = P.N, Pst = P.Pst, ntiles = P.ntiles;
   const NetDims& d = P.d;
   const JetSpec& sp = P.sp;
-  constexpr int W = 16 * WT, KB = WT / 2, OPW = WT / 4, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
+  constexpr int W = 16 * WT, OPW = WT / 4, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
   constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
-  constexpr int ZS = LM == 1 ? 1 : 0;      // slot of zb_LM (h_0's slot once layer 1 has read it)
-  constexpr int S1 = S - 1 - NSO, SO = 1 + S1;
-  constexpr int OQ = fz_oq(MODE);
-  static_assert(OPW >= 1 && OPW * 4 == WT, "fused kernels: WT = 4 or 8");
-  static_assert(MODE != 2 || LM >= 2, "fused-loss mode keeps h_LM in h_0's slot");
+  constexpr int ZS = 0;                    // slot of h_LM / zb_LM (h_0's slot once layer 1 has read it)
+  static_assert(OPW >= 1 && OPW * 4 == WT, "fused step: WT = 4 or 8");
+  static_assert(LM >= 2, "fused step keeps h_LM in h_0's slot");
   __bf16* img = reinterpret_cast<__bf16*>(lds_raw);
   auto slot = [&](int k) { return img + k * (S + 1) * SIMG; };
   float* fl = reinterpret_cast<float*>(img + fz_img_elems(WT, S, LM));
@@ -354,9 +270,9 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   float* aux = fl;                            // the aux image (biases, K0, Ko, bo), copied once
   float* xs = aux + naux;                     // [FZ_PT][TDQ_MAXD]
   float* ubs = xs + FZ_PT * TDQ_MAXD;         // [S][FZ_PT][4] dJ of the tile
-  float* part = ubs + S * FZ_PT * 4;          // MODE 1, 2: [2 column tiles][...] partials
+  float* part = ubs + S * FZ_PT * 4;          // [2 column tiles][...] partials
   const int pq = (LM + 1) * W + d.d_in * W + 4 * W;  // partial floats per column tile
-  float* outp = part + (MODE >= 1 ? 2 * pq + 4 : 0);  // MODE 0, 2: [4][S][FZ_PT][OQ] output-layer dots
+  float* outp = part + 2 * pq + 4;            // [4][S][FZ_PT] output-layer dots
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -378,72 +294,42 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
 
   for (int e = tid; e < naux; e += 64 * FZ_WAVES) aux[e] = e < aux_floats(d, W) ? aux_g[e] : 0.f;
   f32x4 dk[LM][NR][NC];
-  float lacc[LossF::NACC];  // MODE 2: this point-thread's loss / scalar-gradient sums (all tiles)
+  float lacc[LossF::NACC];  // this point-thread's loss / scalar-gradient sums (all tiles)
 #pragma unroll
   for (int k = 0; k < LossF::NACC; ++k) lacc[k] = 0.f;
-  if constexpr (MODE >= 1) {
 #pragma unroll
-    for (int i = 0; i < LM; ++i)
+  for (int i = 0; i < LM; ++i)
 #pragma unroll
-      for (int r = 0; r < NR; ++r)
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) dk[i][r][c] = zero4();
-    for (int e = tid; e < 2 * pq + 4; e += 64 * FZ_WAVES) part[e] = 0.f;
-  }
+      for (int c = 0; c < NC; ++c) dk[i][r][c] = zero4();
+  for (int e = tid; e < 2 * pq + 4; e += 64 * FZ_WAVES) part[e] = 0.f;
   const float* Ko = aux + aux_ko(d, W);
 
   // layer 0 (input -> width, VALU) of feature tile o0 + oo at this lane's point
   auto layer0 = [&](int oo, f32x4(&h)[S]) { fz_h0<WT, S, NSO>(sp, aux, d, xs + row * TDQ_MAXD, o0 + oo, g, h); };
 
-  // this thread's element of a tile's x / dJ (one each: FZ_PT * TDQ_MAXD and S * FZ_PT * 4 are
-  // <= 512), fetched one tile ahead so the global latency hides behind the current tile
-  static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES && S * FZ_PT * 4 <= 64 * FZ_WAVES, "one element per thread");
-  float xpre = 0.f, upre = 0.f;
-  float lnext[LossF::NPRE], lpre[LossF::NPRE];  // MODE 2: the loss inputs of this thread's point
-#pragma unroll
-  for (int k = 0; k < LossF::NPRE; ++k) lnext[k] = lpre[k] = 0.f;
+  // this thread's element of a tile's x (one: FZ_PT * TDQ_MAXD <= 512), fetched one tile ahead so
+  // the global latency hides behind the current tile
+  static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES, "one element per thread");
+  float xpre = 0.f;
   auto fetch = [&](int tt) {
     const int pb = P.p_lo + tt * FZ_PT;
-    if (MODE == 2 && tid < FZ_PT) LossF::prefetch(*P.lptrs, pb + tid, N, lnext);
     if (tid < FZ_PT * TDQ_MAXD) {
       const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
       const int n = min(pb + pt, N - 1);
       xpre = j < d.d_in ? X[(size_t)n * d.d_in + j] : 0.f;
     }
-    if (MODE == 1 && tid < S * FZ_PT * 4) {
-      const int s = tid / (FZ_PT * 4), r = tid - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
-      const int n = pb + pt;
-      upre = (n < N && qo < d.d_out) ? dJ[((size_t)s * N + n) * d.d_out + qo] : 0.f;
-    }
   };
-  int* fz_tq = FzTileQ<DYN>::slots();  // DYN: [0] first tile, [1] the tile after the next one
-  int t = t0, tend = t1, tn = 0;
-  if constexpr (DYN) {
-    if (tid == 0) {
-      fz_tq[0] = atomicAdd(P.tctr, 1);
-      fz_tq[1] = atomicAdd(P.tctr, 1);
-    }
-    __syncthreads();
-    t = fz_tq[0];
-    tend = ntiles;
-  }
-  if (t < tend) fetch(t);
+  int t = t0;
+  if (t < t1) fetch(t);
   TDQ_TS(0);
-  while (t < tend) {
+  while (t < t1) {
     const int pb = P.p_lo + t * FZ_PT;
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
     __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
-    if constexpr (DYN) tn = fz_tq[1];
-    else tn = t + 1;
     if (tid < FZ_PT * TDQ_MAXD) xs[tid] = xpre;
-    if (MODE == 1 && tid < S * FZ_PT * 4) ubs[tid] = upre;
-    if constexpr (MODE == 2) {
-#pragma unroll
-      for (int k = 0; k < LossF::NPRE; ++k) lpre[k] = lnext[k];
-    }
-    if (tn < tend) fetch(tn);
-    int tq = 0;
-    if (DYN && tid == 0) tq = atomicAdd(P.tctr, 1);  // the tile after tn (parked at the tile's end)
+    if (t + 1 < t1) fetch(t + 1);
     __syncthreads();
     FZ_TS(1);
 
@@ -463,9 +349,9 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     for (int ly = 1; ly <= LM; ++ly) {
       const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
       f32x4 acc[OPW][S];
-      fz_gemm<WT, S, OPW, WLO>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
+      fz_gemm<WT, S, OPW>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
       FZ_TS(1 + 2 * ly);
-      f32x4 hq[OPW][S];  // MODE 0, top layer: the streams for the output dots
+      f32x4 hq[OPW][S];  // top layer: the streams for the output dots
 #pragma unroll
       for (int oo = 0; oo < OPW; ++oo) {
         const int to = o0 + oo;
@@ -473,358 +359,226 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
 #pragma unroll
         for (int s = 0; s < S; ++s) z[s] = acc[oo][s];
         z[0] += *reinterpret_cast<const f32x4*>(bi + 16 * to + 4 * g);
-        fz_tanh_jet_f<S, NSO>(sp, z, h);
-        if (ly < LM) {
-          __bf16* im = slot(ly);
-          bf16x4 hi, lo;
-          split4(h[0], hi, lo);
-          fz_put<RS>(im, L, q, to, hi);
-          if constexpr (MODE >= 1) fz_put<RS>(im + S * SIMG, L, q, to, lo);
+        tanh_jet_f<S, NSO>(sp, z, h);
+        // h_l into slot l; h_LM waits in h_0's slot (hi / lo value) for the loss
+        __bf16* im = slot(ly < LM ? ly : ZS);
+        bf16x4 hi, lo;
+        split4(h[0], hi, lo);
+        fz_put<RS>(im, L, q, to, hi);
+        fz_put<RS>(im + S * SIMG, L, q, to, lo);
 #pragma unroll
-          for (int s = 1; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(h[s]));
-        } else if constexpr (MODE != 1) {
+        for (int s = 1; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(h[s]));
+        if (ly == LM) {
 #pragma unroll
           for (int s = 0; s < S; ++s) hq[oo][s] = h[s];
-          if constexpr (MODE == 2) {  // h_LM waits in h_0's slot (hi / lo value) for the loss
-            __bf16* im = slot(ZS);
-            bf16x4 hi, lo;
-            split4(h[0], hi, lo);
-            fz_put<RS>(im, L, q, to, hi);
-            fz_put<RS>(im + S * SIMG, L, q, to, lo);
-#pragma unroll
-            for (int s = 1; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(h[s]));
-          }
-        } else {
-          // reverse through the output layer right here (dJ is known): hb = Ko ub, dKo, then the
-          // top tanh layer's adjoint zb_LM into slot ZS (h_0's slot: its readers, layer 1's GEMM,
-          // are behind the barrier after layer 1; LM = 1: the spare slot 1).  Output columns in a
-          // runtime loop: d_out is 1 for scalar PDEs
-          f32x4 hb[S], zb[S];
-#pragma unroll
-          for (int s = 0; s < S; ++s) hb[s] = zero4();
-          for (int qo = 0; qo < d.d_out; ++qo) {
-            f32x4 kq, pp = zero4();
-#pragma unroll
-            for (int c = 0; c < 4; ++c) kq[c] = Ko[(16 * to + 4 * g + c) * 4 + qo];
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-              const float ub = ubs[(s * FZ_PT + row) * 4 + qo];
-              hb[s] += kq * ub;
-              pp += h[s] * ub;
-            }
-            const float r = row16_sum4(pp);
-            if ((p & 3) == 0) accKo[(16 * to + 4 * g + (p >> 2)) * 4 + qo] += r;
-          }
-          tanh_jet_b<S, NSO>(sp, h, hb, zb);
-          const float r = row16_sum4(zb[0]);
-          if ((p & 3) == 0) accB[LM * W + 16 * to + 4 * g + (p >> 2)] += r;
-#pragma unroll
-          for (int s = 0; s < S; ++s) fz_put<RS>(slot(ZS) + s * SIMG, L, q, to, cvt_hi4(zb[s]));
         }
       }
-      if (MODE != 1 && ly == LM) {  // output-layer partial dots of this wave's features -> LDS
-        for (int qo = 0; qo < (MODE == 2 ? 1 : d.d_out); ++qo) {
+      if (ly == LM) {  // output-layer partial dots of this wave's features -> LDS
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            float a = 0.f;
+        for (int s = 0; s < S; ++s) {
+          float a = 0.f;
 #pragma unroll
-            for (int oo = 0; oo < OPW; ++oo)
+          for (int oo = 0; oo < OPW; ++oo)
 #pragma unroll
-              for (int c = 0; c < 4; ++c) a = fmaf(hq[oo][s][c], Ko[(16 * (o0 + oo) + 4 * g + c) * 4 + qo], a);
-            const float r = col4_sum(a);
-            if (g == 0) outp[((wo * S + s) * FZ_PT + row) * OQ + qo] = r;
-          }
+            for (int c = 0; c < 4; ++c) a = fmaf(hq[oo][s][c], Ko[(16 * (o0 + oo) + 4 * g + c) * 4], a);
+          const float r = col4_sum(a);
+          if (g == 0) outp[(wo * S + s) * FZ_PT + row] = r;
         }
       }
       __syncthreads();
       FZ_TS(2 + 2 * ly);
     }
 
-    if constexpr (MODE == 0) {
-      // ---- output layer: the per-wave partial dots summed in wave order ----------------------
-      const float* bo = aux + aux_bo(d, W);
-      for (int e = tid; e < S * FZ_PT * 4; e += 64 * FZ_WAVES) {
-        const int s = e / (FZ_PT * 4), r = e - s * FZ_PT * 4, pt = r >> 2, qo = r & 3;
-        const int n = pb + pt;
-        if (n < N && qo < d.d_out) {
-          float a = outp[((0 * S + s) * FZ_PT + pt) * OQ + qo];
+    // ---- J of the tile's points: the wave-ordered sums of the partial dots, in place of wave
+    // 0's (each (stream, point) entry read and written by one thread) --------------------------
+    // (the thread index goes through an opaque copy here and at the loss call: the addresses
+    // derived from it would otherwise be hoisted out of the tile loop and, at 256 VGPRs,
+    // spilled - a scratch reload + full vmcnt wait per address on the loss's critical path)
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+    if (tl < S * FZ_PT) {
+      const int s = tl / FZ_PT, pt = tl - s * FZ_PT;
+      float a = outp[(0 * S + s) * FZ_PT + pt];
 #pragma unroll
-          for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * OQ + qo];
-          if (s == 0) a += bo[qo];
-          J[((size_t)s * N + n) * d.d_out + qo] = a;
-        }
+      for (int ww = 1; ww < 4; ++ww) a += outp[(ww * S + s) * FZ_PT + pt];
+      outp[(0 * S + s) * FZ_PT + pt] = s == 0 ? a + aux[aux_bo(d, W)] : a;
+    }
+    __syncthreads();
+    // ---- the per-point loss (generated code: every loss group of the program - residual, SA
+    // weighting, boundary terms with the two points of a periodic pair side by side - and its
+    // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
+    tl = tid;
+    asm volatile("" : "+v"(tl));
+    if (tl < FZ_PT) LossF::template eval<S, FZ_PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc);
+    __syncthreads();
+    FZ_TS(9);
+    // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
+#pragma unroll
+    for (int oo = 0; oo < OPW; ++oo) {
+      const int to = o0 + oo;
+      __bf16* im = slot(ZS);
+      f32x4 h[S], hb[S], zb[S];
+      h[0] = fz_bf4(fz_get<RS>(im, L, q, to)) + fz_bf4(fz_get<RS>(im + S * SIMG, L, q, to));
+#pragma unroll
+      for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(im + s * SIMG, L, q, to));
+      f32x4 kq, pp = zero4();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kq[c] = Ko[(16 * to + 4 * g + c) * 4];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const float ub = ubs[(s * FZ_PT + row) * 4];
+        hb[s] = kq * ub;
+        pp += h[s] * ub;
       }
-    } else {
-      if constexpr (MODE == 2) {
-        // ---- J of the tile's points: the wave-ordered sums of the partial dots, in place of wave
-        // 0's (each (stream, point) entry read and written by one thread) ----------------------
-        // (the thread index goes through an opaque copy here and at the loss call: the addresses
-        // derived from it would otherwise be hoisted out of the tile loop and, at 256 VGPRs,
-        // spilled - a scratch reload + full vmcnt wait per address on the loss's critical path)
-        int tl = tid;
-        asm volatile("" : "+v"(tl));
-        if (tl < S * FZ_PT) {
-          const int s = tl / FZ_PT, pt = tl - s * FZ_PT;
-          float a = outp[((0 * S + s) * FZ_PT + pt) * OQ];
+      {
+        const float r = row16_sum4(pp);
+        if ((p & 3) == 0) accKo[(16 * to + 4 * g + (p >> 2)) * 4] += r;
+      }
+      tanh_jet_b<S, NSO>(sp, h, hb, zb);
+      const float r = row16_sum4(zb[0]);
+      if ((p & 3) == 0) accB[LM * W + 16 * to + 4 * g + (p >> 2)] += r;
 #pragma unroll
-          for (int ww = 1; ww < 4; ++ww) a += outp[((ww * S + s) * FZ_PT + pt) * OQ];
-          outp[((0 * S + s) * FZ_PT + pt) * OQ] = s == 0 ? a + aux[aux_bo(d, W)] : a;
-        }
-        __syncthreads();
-        // ---- the per-point loss (generated code: every loss group of the program - residual, SA
-        // weighting, boundary terms with the two points of a periodic pair side by side - and its
-        // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
-        tl = tid;
-        asm volatile("" : "+v"(tl));
-        if (tl < FZ_PT) LossF::template eval<S, OQ>(outp, xs, tl, pb + tl, N, *P.lptrs, lpre, ubs, lacc);
-        __syncthreads();
-        FZ_TS(9);
-        // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
+      for (int s = 0; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(zb[s]));
+    }
+    __syncthreads();
+    int ll = l;
+    asm volatile("" : "+v"(ll));  // (its addresses recomputed per tile, not hoisted and spilled)
+    if (w == 0 && ll < 4) {  // dbo (ubs is complete since the tile's first barriers)
+      float a = 0.f;
+      for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + ll];
+      accBo[ll] += a;
+    }
+    // ---- hidden layers LM..1: dK_l, hb_{l-1} = K_l zb_l, adjoint of tanh layer l-1 --------
+#pragma unroll
+    for (int ly = LM; ly >= 1; --ly) {
+      const __bf16* Z = slot(ly == LM ? ZS : ly);
+      __bf16* H = slot(ly - 1);
+      const int tb = 10 + 5 * (LM - ly);
+      f32x4 acc[OPW][S];
+      fz_gemm<WT, S, OPW>(acc, Kimg, ly, o0, Z, q, L, l);
+      FZ_TS(tb);
+      // the tanh-jet adjoint (VALU) and dK_ly (MFMA: every wave reads all of H and Z) in one
+      // scheduling region; zb_{ly-1} goes in place of h_{ly-1} after the barrier
+      bf16x4 zbh[OPW][S];
+      float rb[OPW];
+      if (ly >= 2) {
 #pragma unroll
         for (int oo = 0; oo < OPW; ++oo) {
           const int to = o0 + oo;
-          __bf16* im = slot(ZS);
-          f32x4 h[S], hb[S], zb[S];
-          h[0] = fz_bf4(fz_get<RS>(im, L, q, to)) + fz_bf4(fz_get<RS>(im + S * SIMG, L, q, to));
+          f32x4 h[S], zb[S];
+          h[0] = fz_bf4(fz_get<RS>(H, L, q, to)) + fz_bf4(fz_get<RS>(H + S * SIMG, L, q, to));
 #pragma unroll
-          for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(im + s * SIMG, L, q, to));
-          f32x4 kq, pp = zero4();
+          for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(H + s * SIMG, L, q, to));
+          tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
+          rb[oo] = row16_sum4(zb[0]);
 #pragma unroll
-          for (int c = 0; c < 4; ++c) kq[c] = Ko[(16 * to + 4 * g + c) * 4];
+          for (int s = 0; s < S; ++s) zbh[oo][s] = cvt_hi4(zb[s]);
+        }
+      }
+      fz_dk<WT, S, NR, NC, false>(dk[ly - 1], H, Z, r0, c0, l);
+      FZ_TS(tb + 1);
+      if (ly >= 2) {
+        __syncthreads();  // every wave's dK reads of H are done
+        FZ_TS(tb + 2);
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const float ub = ubs[(s * FZ_PT + row) * 4];
-            hb[s] = kq * ub;
-            pp += h[s] * ub;
-          }
+        for (int oo = 0; oo < OPW; ++oo) {
+          const int to = o0 + oo;
+          if ((p & 3) == 0) accB[(ly - 1) * W + 16 * to + 4 * g + (p >> 2)] += rb[oo];
+#pragma unroll
+          for (int s = 0; s < S; ++s) fz_put<RS>(H + s * SIMG, L, q, to, zbh[oo][s]);
+        }
+      } else {
+        // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
+#pragma unroll
+        for (int oo = 0; oo < OPW; ++oo) {
+          const int to = o0 + oo;
+          f32x4 h[S], zb[S];
+          layer0(oo, h);
+          tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
+          const int fo = 16 * to + 4 * g + (p >> 2);
           {
-            const float r = row16_sum4(pp);
-            if ((p & 3) == 0) accKo[(16 * to + 4 * g + (p >> 2)) * 4] += r;
+            const float r = row16_sum4(zb[0]);
+            if ((p & 3) == 0) accB[fo] += r;
           }
-          tanh_jet_b<S, NSO>(sp, h, hb, zb);
-          const float r = row16_sum4(zb[0]);
-          if ((p & 3) == 0) accB[LM * W + 16 * to + 4 * g + (p >> 2)] += r;
+          for (int j = 0; j < d.d_in; ++j) {
+            const float xj = xs[row * TDQ_MAXD + j];
+            f32x4 vv;
 #pragma unroll
-          for (int s = 0; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(zb[s]));
-        }
-        __syncthreads();
-      }
-      int ll = l;
-      asm volatile("" : "+v"(ll));  // (its addresses recomputed per tile, not hoisted and spilled)
-      if (w == 0 && ll < 4) {  // dbo (ubs is complete since the tile's first barriers)
-        float a = 0.f;
-        for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + ll];
-        accBo[ll] += a;
-      }
-      // ---- hidden layers LM..1: dK_l, hb_{l-1} = K_l zb_l, adjoint of tanh layer l-1 --------
+            for (int c = 0; c < 4; ++c) {
+              float a = xj * zb[0][c];
+              constexpr int SO = S - NSO;
 #pragma unroll
-      for (int ly = LM; ly >= 1; --ly) {
-        const __bf16* Z = slot(ly == LM ? ZS : ly);
-        __bf16* H = slot(ly - 1);
-        const int tb = 10 + 5 * (LM - ly);
-        f32x4 acc[OPW][S];
-        fz_gemm<WT, S, OPW, WLO>(acc, Kimg, ly, o0, Z, q, L, l);
-        FZ_TS(tb);
-        // the tanh-jet adjoint (VALU) and dK_ly (MFMA: every wave reads all of H and Z) in one
-        // scheduling region; zb_{ly-1} goes in place of h_{ly-1} after the barrier
-        bf16x4 zbh[OPW][S];
-        float rb[OPW];
-        if (ly >= 2) {
-#pragma unroll
-          for (int oo = 0; oo < OPW; ++oo) {
-            const int to = o0 + oo;
-            f32x4 h[S], zb[S];
-            h[0] = fz_bf4(fz_get<RS>(H, L, q, to)) + fz_bf4(fz_get<RS>(H + S * SIMG, L, q, to));
-#pragma unroll
-            for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(H + s * SIMG, L, q, to));
-            tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
-            rb[oo] = row16_sum4(zb[0]);
-#pragma unroll
-            for (int s = 0; s < S; ++s) zbh[oo][s] = cvt_hi4(zb[s]);
-          }
-        }
-        fz_dk<WT, S, NR, NC, false>(dk[ly - 1], H, Z, r0, c0, l);
-        FZ_TS(tb + 1);
-        if (ly >= 2) {
-          __syncthreads();  // every wave's dK reads of H are done
-          FZ_TS(tb + 2);
-#pragma unroll
-          for (int oo = 0; oo < OPW; ++oo) {
-            const int to = o0 + oo;
-            if ((p & 3) == 0) accB[(ly - 1) * W + 16 * to + 4 * g + (p >> 2)] += rb[oo];
-#pragma unroll
-            for (int s = 0; s < S; ++s) fz_put<RS>(H + s * SIMG, L, q, to, zbh[oo][s]);
-          }
-        } else {
-          // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
-#pragma unroll
-          for (int oo = 0; oo < OPW; ++oo) {
-            const int to = o0 + oo;
-            f32x4 h[S], zb[S];
-            layer0(oo, h);
-            tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
-            const int fo = 16 * to + 4 * g + (p >> 2);
-            {
-              const float r = row16_sum4(zb[0]);
-              if ((p & 3) == 0) accB[fo] += r;
+              for (int s = 1; s < SO; ++s) a += (sp.var[s] == j) ? zb[s][c] : 0.f;
+              vv[c] = a;
             }
-            for (int j = 0; j < d.d_in; ++j) {
-              const float xj = xs[row * TDQ_MAXD + j];
-              f32x4 vv;
-#pragma unroll
-              for (int c = 0; c < 4; ++c) {
-                float a = xj * zb[0][c];
-#pragma unroll
-                for (int s = 1; s < SO; ++s) a += (sp.var[s] == j) ? zb[s][c] : 0.f;
-                vv[c] = a;
-              }
-              const float r = row16_sum4(vv);
-              if ((p & 3) == 0) accK0[j * W + fo] += r;
-            }
+            const float r = row16_sum4(vv);
+            if ((p & 3) == 0) accK0[j * W + fo] += r;
           }
         }
-        FZ_TS(tb + 3);
-        if (ly == 2) {  // rebuild h_0 into slot 0 (zb_LM there is consumed)
-          if (LM == 2) __syncthreads();  // (LM = 2: it was this step's Z)
-#pragma unroll
-          for (int oo = 0; oo < OPW; ++oo) {
-            f32x4 h[S];
-            layer0(oo, h);
-#pragma unroll
-            for (int s = 0; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
-          }
-        }
-        if (ly >= 2) __syncthreads();
-        FZ_TS(tb + 4);
       }
+      FZ_TS(tb + 3);
+      if (ly == 2) {  // rebuild h_0 into slot 0 (zb_LM there is consumed)
+        if (LM == 2) __syncthreads();  // (LM = 2: it was this step's Z)
+#pragma unroll
+        for (int oo = 0; oo < OPW; ++oo) {
+          f32x4 h[S];
+          layer0(oo, h);
+#pragma unroll
+          for (int s = 0; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
+        }
+      }
+      if (ly >= 2) __syncthreads();
+      FZ_TS(tb + 4);
     }
-    if (DYN && tid == 0) fz_tq[1] = tq;  // read after the next tile's first barrier
-    t = tn;
+    ++t;
   }
   TDQ_TS(62);
-  if constexpr (DYN) {  // the last workgroup out re-arms the queue for the next launch
-    if (tid == 0 && atomicAdd(P.tctr + 1, 1) == (int)gridDim.x - 1) {
-      P.tctr[0] = 0;
-      P.tctr[1] = 0;
-    }
-  }
 
-  if constexpr (MODE >= 1) {
-    // ---- this workgroup's gradient-slab row (bf16; WLO: fp32) --------------------------------
-    using ST = typename SlabType<!WLO>::T;
-    ST* gs = reinterpret_cast<ST*>(P.slab) + (size_t)(P.srow + gi) * Pst;
+  // ---- this workgroup's gradient-slab row (bf16) ---------------------------------------------
+  __bf16* gs = reinterpret_cast<__bf16*>(P.slab) + (size_t)(P.srow + gi) * Pst;
 #pragma unroll
-    for (int ly = 1; ly <= LM; ++ly) {
-      if constexpr (WLO) {
-        float* row = reinterpret_cast<float*>(gs) + off_layer(d, ly) + (16 * r0 + 4 * g) * W + 16 * c0 + p;
+  for (int ly = 1; ly <= LM; ++ly) {
+    const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * 2;
+    const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
-          for (int c = 0; c < NC; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) row[(16 * r + e) * W + 16 * c] = dk[ly - 1][r][c][e];
-      } else {
-        const int voff = ((16 * r0 + 4 * g) * W + 16 * c0 + p) * 2;
-        const Tl Gt = tl_make(gs + off_layer(d, ly), 0);
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-          for (int c = 0; c < NC; ++c)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)dk[ly - 1][r][c][e]),
-                                                    Gt.r, voff, ((16 * r + e) * W + 16 * c) * 2, 0);
-      }
-    }
-    __syncthreads();  // LDS partials complete
-    const float* pA = part;
-    const float* pB = part + pq;
-    for (int f = tid; f < W; f += 64 * FZ_WAVES) {
-      gs[d.d_in * W + f] = (ST)(pA[f] + pB[f]);  // b0
-      for (int ly = 1; ly <= LM; ++ly)
-        gs[off_layer(d, ly) + W * W + f] = (ST)(pA[ly * W + f] + pB[ly * W + f]);
-      for (int j = 0; j < d.d_in; ++j) {
-        const int k = (LM + 1) * W + j * W + f;
-        gs[j * W + f] = (ST)(pA[k] + pB[k]);
-      }
-      for (int qo = 0; qo < d.d_out; ++qo) {
-        const int k = (LM + 1 + d.d_in) * W + f * 4 + qo;
-        gs[off_layer(d, LM + 1) + f * d.d_out + qo] = (ST)(pA[k] + pB[k]);
-      }
-    }
-    if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (ST)accBo[tid];
+        for (int e = 0; e < 4; ++e)
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)dk[ly - 1][r][c][e]),
+                                                Gt.r, voff, ((16 * r + e) * W + 16 * c) * 2, 0);
   }
-  if constexpr (MODE == 2) {  // loss partials: the point-threads (wave 0, lanes < FZ_PT) summed
-    if (w == 0) {
+  __syncthreads();  // LDS partials complete
+  const float* pA = part;
+  const float* pB = part + pq;
+  for (int f = tid; f < W; f += 64 * FZ_WAVES) {
+    gs[d.d_in * W + f] = (__bf16)(pA[f] + pB[f]);  // b0
+    for (int ly = 1; ly <= LM; ++ly)
+      gs[off_layer(d, ly) + W * W + f] = (__bf16)(pA[ly * W + f] + pB[ly * W + f]);
+    for (int j = 0; j < d.d_in; ++j) {
+      const int k = (LM + 1) * W + j * W + f;
+      gs[j * W + f] = (__bf16)(pA[k] + pB[k]);
+    }
+    for (int qo = 0; qo < d.d_out; ++qo) {
+      const int k = (LM + 1 + d.d_in) * W + f * 4 + qo;
+      gs[off_layer(d, LM + 1) + f * d.d_out + qo] = (__bf16)(pA[k] + pB[k]);
+    }
+  }
+  if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (__bf16)accBo[tid];
+  // loss partials: the point-threads (wave 0, lanes < FZ_PT) summed
+  if (w == 0) {
 #pragma unroll
-      for (int k = 0; k < LossF::NACC; ++k) {
-        const float v = col4_sum(row16_sum(lacc[k]));
-        if (l == 0 && k < P.nacc) P.lpart[(size_t)(P.prow + gi) * P.nacc + k] = v;
-      }
+    for (int k = 0; k < LossF::NACC; ++k) {
+      const float v = col4_sum(row16_sum(lacc[k]));
+      if (l == 0 && k < P.nacc) P.lpart[(size_t)(P.prow + gi) * P.nacc + k] = v;
     }
   }
   TDQ_TS(63);
 }
 
-template <int WT, int S, int NSO, int LM, int MODE>
-__global__ void __launch_bounds__(64 * FZ_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
-jet_fused_kernel(FzParams P) {
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  fz_body<WT, S, NSO, LM, MODE, FzNoLoss>(P, lds_raw);
-}
-
-// ------------------------------------------------------------------------------------------
-// host side
-// ------------------------------------------------------------------------------------------
 #ifndef __HIPCC_RTC__
-struct FzArgs {
-  const float* X;
-  const float* aux;
-  const bf16x8* fimg;
-  const bf16x8* bimg;
-  const float* dJ;
-  float* J;
-  float* slab;
-  int N, Pst, G, ntiles;
-  NetDims d;
-  JetSpec sp;
-  hipStream_t st;
-};
-
-template <int WT, int S, int NSO, int LM, int MODE>
-int launch_fused(const FzArgs& a) {
-  const size_t lds = fz_lds_bytes(a.d, WT, S, LM, MODE);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&jet_fused_kernel<WT, S, NSO, LM, MODE>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  FzParams P{};
-  P.X = a.X;
-  P.aux = a.aux;
-  P.fimg = a.fimg;
-  P.bimg = a.bimg;
-  P.dJ = a.dJ;
-  P.J = a.J;
-  P.slab = a.slab;
-  P.N = a.N;
-  P.Pst = a.Pst;
-  P.ntiles = a.ntiles;
-  P.p_lo = 0;
-  P.srow = 0;
-  P.d = a.d;
-  P.sp = a.sp;
-  hipLaunchKernelGGL((jet_fused_kernel<WT, S, NSO, LM, MODE>), dim3(a.G), dim3(64 * FZ_WAVES), lds, a.st, P);
-  TDQ_CHECK_LAUNCH();
-  return 0;
-}
-
 // jet_fused.hip
-bool fz_active(const NetDims& d, int WT, int S, int lo);
-int fz_rows(int N);
-int fz_launch(int mode, const float* X, const float* aux, const bf16x8* fimg, const bf16x8* bimg, const float* dJ,
-              float* J, float* slab, int N, int Pst, const NetDims& d, const JetSpec& sp, int S, int nso,
-              hipStream_t st);
+int fz_cus();
+extern "C" int tdq_jet_fused_lds(int d_in, const int* widths, int d_out, int n_hidden, int S, int lo);
 #endif  // __HIPCC_RTC__

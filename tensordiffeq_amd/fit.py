@@ -613,11 +613,6 @@ def point_ranges(program, fop):
     if cfg["precision"] not in ("bf16x3", "bf16") or cfg.get("engine") == "layered":
         return None
     from .ops import jet_hip
-    try:
-        if jet_hip.fused_active(cfg):  # one persistent launch per pass already fills the GPU
-            return None
-    except Exception:  # noqa: BLE001 - no native library: no ranges either way
-        return None
     if spec == "auto":
         # sweeps on MI355X with the specialized loss kernel: bf16 0.38 (0.2018 ms vs 0.2035 at 0.45,
         # 3 passes, profiles/r3_yz_split_sweep_jit.jsonl), bf16x3 0.30-0.40 equal within noise.
@@ -742,10 +737,9 @@ def run_ranges(program, fop, flat, ranges, streams, pack=True, bufs=None, prered
 class LossGradEngine:
     """``(f, g_theta)`` at a flat parameter vector (lambdas frozen, B15); DP all-reduced."""
 
-    def __init__(self, solver, program, lambdas, weight_lo=False):
+    def __init__(self, solver, program, lambdas):
         self.s = solver
         self.program = program
-        self.weight_lo = bool(weight_lo)   # newton_precision "bf16w" (ops/fused_step.py wlo)
         self.flat = solver.u_model.flat
         self.lambdas = lambdas
         self.dist = solver.dist_ctx
@@ -783,11 +777,8 @@ class LossGradEngine:
                 hi = prog.hi_op
                 gx = hi.grad if hi is not None else None
                 from .ops import fused_step
-                fs = fused_step.for_program(prog, wlo=self.weight_lo)
-                if fs is None and self.weight_lo:
-                    from .models.loss import _warn_once
-                    _warn_once(f"newton_precision='bf16w' needs the fused step ({prog.fused_step_w_reason}); "
-                               "the L-BFGS objective runs in plain bf16")
+                # the one-launch objective (bf16: jet_fused.h, bf16x3: jet_fused3.h)
+                fs = fused_step.for_program(prog)
                 if fs is not None:
                     J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
                                                      rows=fop.fl.n_streams)

@@ -526,7 +526,18 @@ def split_by_streams(fl, gr, n_lo):
             return None
     if not lo or not hi:
         return None
-    return compile_graph(g, lo, *ctx), compile_graph(g, hi, *ctx)
+    P_lo, P_hi = compile_graph(g, lo, *ctx), compile_graph(g, hi, *ctx)
+    # both kernels ASSIGN the per-point SA-weight gradient (dlam[a][i] = g) and run concurrently in
+    # the split layout: a weight read by both programs would get only one program's adjoint (a
+    # race).  The caller falls back to another layout instead.
+    if _lam_ids(P_lo) & _lam_ids(P_hi):
+        return None
+    return P_lo, P_hi
+
+
+def _lam_ids(P):
+    """Per-point SA-weight slots a compiled group program loads."""
+    return {a for (op, _, a, _) in P.code if op == OP["LAM"]}
 
 
 def _extra_syms(g, extra, scal_id, fl):

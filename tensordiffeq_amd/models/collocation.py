@@ -380,22 +380,18 @@ class CollocationSolverND:
         return lambda w: eng(torch.as_tensor(w, dtype=torch.float32, device=self.device))
 
     def _get_lbfgs_engine(self, precision=None):
-        """The L-BFGS objective's engine at ``precision`` (default ``newton_precision``).  "bf16w"
-        is the bf16 program evaluated by the fused step with the weights' lo parts
-        (ops/fused_step.py ``wlo``)."""
+        """The L-BFGS objective's engine at ``precision`` (default ``newton_precision``)."""
         default = self.newton_precision or self.precision
         prec = precision or default
-        wlo = prec == "bf16w"
-        kprec = "bf16" if wlo else prec
         if prec != default:
             key = ("lbfgs_engine", prec)
             eng = self._programs.get(key)
-            prog = self.program(precision=kprec)
+            prog = self.program(precision=prec)
             if eng is None or eng.program is not prog:
-                eng = self._programs[key] = LossGradEngine(self, prog, self.lambdas, weight_lo=wlo)
+                eng = self._programs[key] = LossGradEngine(self, prog, self.lambdas)
             return eng
         if self._lbfgs_engine is None:
-            self._lbfgs_engine = LossGradEngine(self, self.program(precision=kprec), self.lambdas, weight_lo=wlo)
+            self._lbfgs_engine = LossGradEngine(self, self.program(precision=prec), self.lambdas)
         return self._lbfgs_engine
 
     def _get_engine(self, batch=None, n_hint=0):
@@ -610,7 +606,7 @@ class CollocationSolverND:
             self.min_loss["l-bfgs"] = float(opt.min_loss)
             self.best_epoch["l-bfgs"] = int(opt.n_iter)
             info = {"impl": "strong-wolfe" + (" (device)" if opt.use_graph else ""), "n_iter": int(opt.n_iter),
-                    "func_evals": int(opt.func_eval), "reason": opt.reason}
+                    "func_evals": int(opt.func_eval), "reason": opt.reason, "restarts": int(opt.n_restarts)}
         bar.close()
         self._best_flat["l-bfgs"] = flat.detach().clone()
         self.best_model["l-bfgs"] = _FlatModel(self.u_model, self._best_flat["l-bfgs"])

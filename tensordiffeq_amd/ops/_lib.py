@@ -56,10 +56,7 @@ def _declare(lib):
         "tdq_jet_bf3_scratch_floats": (L, [I, I, P, I, I, I]),
         "tdq_jet_bf3_slab_floats": (L, [I, I, P, I, I]),
         # persistent point-tile kernels (csrc/jet_fused.h) behind the split-bf16 entry points
-        "tdq_jet_fused_active": (I, [I, P, I, I, I, I]),
-        "tdq_jet_fused_rows": (I, [I]),
-        "tdq_jet_fused_override": (I, [I]),
-        "tdq_fused_step_launch": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, I, P, P, I, I, I, P, P]),
+        "tdq_fused_step_launch": (I, [P, P, P, P, I, I, P, I, I, I, P, I, I, I, P, P, I, I, I, P]),
         "tdq_fused_params_size": (I, []),
         "tdq_jet_fused_lds": (I, [I, P, I, I, I, I]),
         "tdq_device_cus": (I, []),

@@ -18,6 +18,10 @@ range) on a side stream beside it.
 The reference's step is tensordiffeq/models.py:90-135 (``train_op_inner`` / ``update_loss``): a
 tape over the network, the residual and the boundary MSEs, then the optimizer.
 
+Precision ``bf16x3`` (the L-BFGS objective) runs the same one-launch structure with every GEMM
+operand split into bf16 hi + lo (``csrc/jet_fused3.h``: 16-point tiles, since the lo planes double
+the LDS images); its tail reduces fp32 slab rows.
+
 ``TDQ_FUSED_STEP=0`` keeps the separate launches (``fit.run_ranges``).
 """
 from __future__ import annotations
@@ -33,14 +37,14 @@ from . import _lib, jet_hip, loss_jit
 from .jet_mlp import hip_config
 
 _CACHE = {}   # source sha -> (module, func)
-_HEADERS = ("common.h", "jet_common.h", "jet_bf3.h", "jet_fused.h")
+_HEADERS = ("common.h", "jet_common.h", "jet_bf3.h", "jet_fused.h", "jet_fused3.h")
 # the library's hipcc flags (csrc/build.py _flags), as hipRTC options
 RTC_OPTS = "-O3 -std=c++17 -fno-slp-vectorize -munsafe-fp-atomics"
 
 
 def _opts():
     """hipRTC options; ``TDQ_FUSED_STEP_TIMING=1`` adds the phase stamps (tools/fused_step_timing.py)."""
-    extra = os.environ.get("TDQ_FUSED_STEP_DEFINES", "")   # A/B builds, e.g. "-DFZ_CHEAP_TANH=0"
+    extra = os.environ.get("TDQ_FUSED_STEP_DEFINES", "")   # A/B builds, e.g. "-DTDQ_PK_TANH=0"
     return RTC_OPTS + (" -DTDQ_PHASE_TIMING" if os.environ.get("TDQ_FUSED_STEP_TIMING") == "1" else "") + \
         (" " + extra if extra else "")
 
@@ -64,30 +68,20 @@ def header_source():
     return "\n".join(out)
 
 
-def _pre_loads(P):
-    """The program's per-point input loads (VAL / LAM / SCAL) in code order: ``[(r, name, a)]``."""
-    out = []
-    for op, r, a, b in P.code:
-        name = loss_jit._OPN[op]
-        if name in ("VAL", "LAM", "SCAL"):
-            out.append((r, name, a))
-    return out
-
-
 def gen_loss(groups, n_terms, nacc, S):
     """``struct GenLoss`` of the loss groups laid out in the fused point set.  ``groups``: one
     ``(program, start, n_slots, n)`` per group - its ``n`` instances occupy points ``start + k``
     (one slot) or the pairs ``start + 2k, start + 2k + 1`` (two slots: a periodic pair side by side,
-    ``start`` even, so a pair never straddles a 32-point tile).  The statements are those of
-    :func:`.loss_jit._group_code` per point: J streams / coordinates from the tile (the partner's
-    from the next point-thread), loss / scalar-gradient sums into the thread's accumulators, dJ
-    of the instance's points into the tile's ``ubs``.  Points outside every group get dJ = 0.  The
-    per-point inputs (SA weights, data values, scalars) are loaded by ``prefetch`` one tile ahead."""
-    npre = max([1] + [len(_pre_loads(P)) for (P, _, _, _) in groups])
+    ``start`` even, so a pair never straddles a tile of 16 or 32 points).  The statements are those
+    of :func:`.loss_jit._group_code` per point: J streams / coordinates from the tile (the partner's
+    from the next point-thread), per-point inputs (SA weights, data values, scalars) from global
+    memory, loss / scalar-gradient sums into the thread's accumulators, dJ of the instance's points
+    into the tile's ``ubs``.  Points outside every group get dJ = 0.  ``eval<S, PT>`` serves both
+    tile sizes (``PT`` points per tile)."""
     L = []
     e = L.append
     e("struct GenLoss {")
-    e(f"  static constexpr int NACC = {max(1, nacc)}, NPRE = {npre};")
+    e(f"  static constexpr int NACC = {max(1, nacc)};")
 
     def branches(body):
         kw = "if"
@@ -104,33 +98,14 @@ def gen_loss(groups, n_terms, nacc, S):
             e("      return;")
             e("    }")
 
-    # ---- prefetch: the group's input loads, in code order, into pre[]
-    e("  __device__ static void prefetch(const FzLossPtrs& ptr, int n, int N, float (&pre)[NPRE]) {")
-
-    # TDQ_FS_PREFETCH=1: the inputs loaded one tile ahead (the loss phase 3.1k -> 2.5k cycles per
-    # tile) - but the step measured 0.1702 vs 0.1679 ms on one box (the extra live registers,
-    # profiles/r5prefab_prefetch_ab.txt), so eval loads them itself by default
-    pref = os.environ.get("TDQ_FS_PREFETCH", "0") == "1"
-
-    def pre_body(P, ns):
-        if not pref:
-            return
-        for j, (r, name, a) in enumerate(_pre_loads(P)):
-            src = {"VAL": f"ptr.val[{a}][i]", "LAM": f"ptr.lam[{a}][i]", "SCAL": f"*ptr.scal[{a}]"}[name]
-            e(f"      pre[{j}] = {src};")
-
-    branches(pre_body)
-    e("  }")
-    # ---- eval
-    e("  template <int S, int OQ>")
+    e("  template <int S, int PT>")
     e("  __device__ static void eval(const float* jv, const float* xs, int t, int n, int N, "
-      "const FzLossPtrs& ptr, const float (&pre)[NPRE], float* ubs, float (&acc)[NACC]) {")
-    e("    #define JV(s_, k_) jv[((s_) * FZ_PT + (k_)) * OQ]")
-    e("    #define UB(s_, k_) ubs[((s_) * FZ_PT + (k_)) * 4]")
+      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC]) {")
+    e("    #define JV(s_, k_) jv[(s_) * PT + (k_)]")
+    e("    #define UB(s_, k_) ubs[((s_) * PT + (k_)) * 4]")
 
     def eval_body(P, ns):
         nr = max(1, P.n_regs)
-        slot = {r: j for j, (r, _, _) in enumerate(_pre_loads(P))}
         e("      float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
         e("      float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
         e("      float " + ", ".join(f"dj{sl}_{b} = 0.f" for sl in range(ns) for b in range(S)) + ";")
@@ -142,10 +117,8 @@ def gen_loss(groups, n_terms, nacc, S):
                 return f"      v{r} = JV({b}, t + {a});"
             if name == "COORD":
                 return f"      v{r} = xs[(t + {a}) * TDQ_MAXD + {b}];"
-            if not pref:
-                return {"VAL": f"      v{r} = ptr.val[{a}][i];", "LAM": f"      v{r} = ptr.lam[{a}][i];",
-                        "SCAL": f"      v{r} = *ptr.scal[{a}];"}[name]
-            return f"      v{r} = pre[{slot[r]}];"
+            return {"VAL": f"      v{r} = ptr.val[{a}][i];", "LAM": f"      v{r} = ptr.lam[{a}][i];",
+                    "SCAL": f"      v{r} = *ptr.scal[{a}];"}[name]
 
         loss_jit._forward_code(P, e, load)
         for (f, w, tt, c) in P.outputs:
@@ -176,13 +149,15 @@ def gen_loss(groups, n_terms, nacc, S):
     return "\n".join(L)
 
 
-def kernel_source(S, nso, LM, lds, gen, wlo=False, dyn=False):
+def kernel_source(S, nso, LM, lds, gen, lo=False):
+    """The kernel translation unit: the headers, the generated loss, and ``tdq_fused_step`` over
+    ``fz_body`` (bf16, 32-point tiles) or ``fz3_body`` (``lo``: bf16x3, 16-point tiles)."""
+    body = "fz3_body" if lo else "fz_body"
     return (header_source() + "\n" + gen + "\n"
             'extern "C" __global__ void __launch_bounds__(64 * FZ_WAVES) '
             "__attribute__((amdgpu_waves_per_eu(2, 2))) tdq_fused_step(FzParams P) {\n"
             f"  __shared__ __attribute__((aligned(16))) char lds[{lds}];\n"
-            f"  fz_body<8, {S}, {nso}, {LM}, 2, GenLoss, {'true' if wlo else 'false'}, "
-            f"{'true' if dyn else 'false'}>(P, lds);\n"
+            f"  {body}<8, {S}, {nso}, {LM}, GenLoss>(P, lds);\n"
             "}\n")
 
 
@@ -219,20 +194,23 @@ def ineligible(prog, fop):
         cfg = hip_config(prog.net, prog.plan, prog.precision)
     except ValueError as e:
         return str(e)
-    if cfg["precision"] != "bf16" or not jet_hip.is_split_bf16(cfg):
+    if cfg["precision"] not in ("bf16", "bf16x3") or not jet_hip.is_split_bf16(cfg):
         return f"precision {cfg['precision']}"
-    if jet_hip.fused_active(cfg):
-        return "TDQ_FUSED=1 (persistent forward / backward launches)"
+    lo = cfg["precision"] == "bf16x3"
     if cfg["d_out"] != 1:
         return "d_out != 1"
     lib = _lib.load()
-    if lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], 2) < 0:
+    if lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], int(lo)) < 0:
         return f"network {cfg['widths']} / S={cfg['S']} (width-128 MFMA layers 2-3, S <= 4)"
     fl = fop.fl
     for gr in fl.groups:
         if any(s >= cfg["S"] for (_, s) in gr.program.stream_regs) and not _mixed(prog):
             return "a loss group reads streams outside the jet plan"
     mode = _mixed_mode(prog)
+    if mode is not None and lo:
+        # the bf16x3 objective of a mixed program keeps the point-range launches (its boundary
+        # chain runs on the bf16x3 jet_hi kernels beside them)
+        return "bf16x3: high-order boundary streams keep the separate launches"
     if mode == "0":
         return "high-order boundary streams (TDQ_FUSED_STEP_MIXED=0)"
     if mode == "split":
@@ -273,7 +251,8 @@ def _mixed_mode(prog):
 
 def _split_groups(prog, fop, S):
     """``[(group, fused program, side program or None)]`` of the split layout, or the reason it
-    does not apply (an output reading main-plan and high-order streams together)."""
+    does not apply (an output reading main-plan and high-order streams together, or an SA weight
+    read by both halves)."""
     from .. import fusion
     out = []
     for gr in fop.fl.groups:
@@ -282,7 +261,7 @@ def _split_groups(prog, fop, S):
             continue
         sp = fusion.split_by_streams(fop.fl, gr, S)
         if sp is None:
-            return "a loss output reads main-plan and high-order streams together"
+            return "a loss output reads main-plan and high-order streams together (or both read one SA weight)"
         out.append((gr, sp[0], sp[1]))
     return out
 
@@ -293,25 +272,28 @@ class FusedStepOp:
 
     Single-plan programs: EVERY loss group runs in the one launch - the points re-laid out once
     into a fused point set (each group's instances contiguous, a periodic group's two segments
-    interleaved pair by pair), so a step is the fused launch + the two-launch step tail.  Mixed
-    programs (order-3/4 boundary streams from jet_hi.hip, :func:`_mixed_mode`): split layout -
-    every loss output on main-plan streams in the fused launch, the high-order outputs (their own
-    loss op, :func:`fusion.split_by_streams`) with the jet_hi forward / adjoint on a side stream
-    beside it; residual layout - the residual group fused over its own segment, the whole boundary
-    chain (high-order streams, saved-activation forward, loss blocks, backward) on the side
-    stream."""
+    interleaved pair by pair), so a step is the fused launch + the two-launch step tail.  Precision
+    bf16: 32-point tiles (``jet_fused.h``); bf16x3 (the L-BFGS objective): 16-point tiles with hi +
+    lo operands (``jet_fused3.h``) and fp32 slab rows.  Mixed programs (order-3/4 boundary streams
+    from jet_hi.hip, bf16 only, :func:`_mixed_mode`): split layout - every loss output on main-plan
+    streams in the fused launch, the high-order outputs (their own loss op,
+    :func:`fusion.split_by_streams`) with the jet_hi forward / adjoint on a side stream beside it;
+    residual layout - the residual group fused over its own segment, the whole boundary chain
+    (high-order streams, saved-activation forward, loss blocks, backward) on the side stream."""
 
-    def __init__(self, prog, fop, wlo=False):
+    def __init__(self, prog, fop):
         lib = _lib.load(required=True)
-        self.prog, self.fop, self.wlo = prog, fop, bool(wlo)
+        self.prog, self.fop = prog, fop
         cfg = self.cfg = hip_config(prog.net, prog.plan, prog.precision)
+        self.lo = cfg["precision"] == "bf16x3"
+        self.pt = 16 if self.lo else 32
         fl = fop.fl
         S = cfg["S"]
         self.nacc = fop.n_terms + fop.n_scal
         spec = jet_hip.stream_spec(prog.plan)
         nso = sum(1 for s in range(S) if spec[3 * s] == 2)
         LM = cfg["n_hidden"] - 1
-        lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S, 2)
+        lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S, int(self.lo))
         if lds < 0 or lds > 160 * 1024:
             raise ValueError(f"fused step: {lds} bytes of LDS")
         self.lds = lds
@@ -367,28 +349,18 @@ class FusedStepOp:
             pts_b = jet_hip.slab_geometry(cfg, N)[0]
             self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
             self.srow = -(-self.p_bc // pts_b)
-        # dynamic tile queue (fz_body DYN, ``TDQ_FS_DYNAMIC=1``): workgroups that start late take
-        # fewer tiles.  Measured on the split layout (AC-baseline, profiles/r5split_dyn_*): every CU
-        # taken 0.2106 ms (the side chain then waits for the launch to end), 32 CUs left to the side
-        # chain 0.2098 (it overlaps; the join before the tail costs ~10 us) vs 0.2065 with static
-        # ranges and one round more; AC-SA 0.1751 vs 0.1673 static - off by default
-        self.dyn = os.environ.get("TDQ_FS_DYNAMIC", "0") == "1"
-        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), wlo=self.wlo,
-                                    dyn=self.dyn)
+        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), lo=self.lo)
         self.module, self.func = _compile(self.source)
-        ntiles = -(-(self.N - self.p_lo) // 32)
+        ntiles = -(-(self.N - self.p_lo) // self.pt)
         cus = max(1, lib.tdq_device_cus())
         rounds = -(-ntiles // cus)
-        if self.fop2 is not None and not self.dyn:
-            # split layout, static ranges: one round more leaves ~57 CUs to the jet_hi side chain -
-            # AC-baseline 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*
+        if self.fop2 is not None:
+            # split layout: one round more leaves ~57 CUs to the jet_hi side chain - AC-baseline
+            # 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*
             rounds += int(os.environ.get("TDQ_FS_SPLIT_ROUNDS", "1"))
-        # static ranges: the fewest workgroups with the same tiles per workgroup (AC-SA 50k: 1592
-        # tiles, 228 x 7); dynamic queue: one workgroup per CU but the ones the split layout's side
-        # chain needs (with every CU taken its kernels waited for the fused launch to end)
-        reserve = int(os.environ.get("TDQ_FS_DYN_RESERVE", "32")) if self.fop2 is not None else 0
-        self.G = max(1, min(cus - reserve, ntiles)) if self.dyn else -(-ntiles // rounds)
-        self.tctr = torch.zeros(2, dtype=torch.int32, device=dev)
+        # the fewest workgroups with the same tiles per workgroup (AC-SA 50k, bf16: 1592 tiles,
+        # 228 x 7; bf16x3: 3183 tiles, 245 x 13)
+        self.G = -(-ntiles // rounds)
         if self.layout == "residual":   # the fused rows follow the boundary loss blocks' rows in fop.partials
             self.G = min(self.G, fop.n_blocks - self.b_res)
         self.rows = self.srow + self.G
@@ -438,8 +410,7 @@ class FusedStepOp:
             rc = lib.tdq_fused_step_launch(self.func, _lib.ptr(Xf), _lib.ptr(scratch), _lib.ptr(work), self.N,
                                            cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S,
                                            spec_arr, self.p_lo, self.srow, self.G, _lib.ptr(fop.ptrs),
-                                           _lib.ptr(lpart), self.b_res, self.nacc, self.seg_lo,
-                                           _lib.ptr(self.tctr) if self.dyn else None,
+                                           _lib.ptr(lpart), self.b_res, self.nacc, int(self.lo),
                                            _lib.stream_ptr(flat.device))
             _lib.check(rc, "tdq_fused_step_launch")
 
@@ -477,42 +448,35 @@ class FusedStepOp:
                    "tdq_rtc_set_global_ptr")
 
     def tail_kw(self):
-        """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows (the
-        weight-lo objective: ``dp_tail_a`` only, its slab rows are fp32)."""
+        """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows (bf16x3:
+        ``dp_tail_a`` only, its slab rows are fp32)."""
         kw = {"rows": self.rows, "lpart": self.fop.partials if self.layout == "residual" else self.lpart,
               "n_lblocks": self.n_lblocks}
-        if self.wlo:
+        if self.lo:
             kw["half"] = False
         return kw
 
 
-def for_program(prog, wlo=False):
-    """The program's :class:`FusedStepOp` (built once per ``wlo``), or ``None`` (reason in
-    ``prog.fused_step_reason``).  ``wlo``: the L-BFGS objective "bf16w" - bf16 activations, the
-    weights' bf16 hi + lo parts in every GEMM (two MFMAs), fp32 gradient slabs."""
-    key = "_fused_step_w" if wlo else "_fused_step"
-    if getattr(prog, key + "_built", False):
-        return getattr(prog, key)
+def for_program(prog):
+    """The program's :class:`FusedStepOp` (built once), or ``None`` (reason in
+    ``prog.fused_step_reason``)."""
+    if getattr(prog, "_fused_step_built", False):
+        return prog._fused_step
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         # module loads cannot run inside a capture: the engines build the op before capturing
         # (fit.AdamEngine._capture, the L-BFGS drivers' first eager evaluation) - never cache a
         # "not available" decided here
         warnings.warn("fused training step first requested inside a graph capture; using separate launches")
         return None
-    setattr(prog, key + "_built", True)
-    setattr(prog, key, None)
+    prog._fused_step_built = True
+    prog._fused_step = None
     fop = getattr(prog, "fused_op", None)
     why = ineligible(prog, fop)
-    if why is None and wlo and _mixed(prog):
-        why = "bf16w: mixed programs keep the boundary chain in bf16"
     if why is None:
         try:
-            setattr(prog, key, FusedStepOp(prog, fop, wlo=wlo))
+            prog._fused_step = FusedStepOp(prog, fop)
         except Exception as e:  # noqa: BLE001 - the separate launches serve every program
             why = f"{type(e).__name__}: {e}"
             warnings.warn(f"fused training step unavailable, using separate launches: {why}")
-    if wlo:
-        prog.fused_step_w_reason = why
-    else:
-        prog.fused_step_reason = why
-    return getattr(prog, key)
+    prog.fused_step_reason = why
+    return prog._fused_step

@@ -178,23 +178,6 @@ def backward_range(saved, dJ, work, lo, hi):
     _lib.check(rc, "tdq_jet_bwd_bf3_range")
 
 
-def fused_active(cfg):
-    """The persistent point-tile kernels (csrc/jet_fused.h) serve this split-bf16 configuration:
-    one forward launch and one recompute-backward launch over the whole point set (no point
-    ranges, no saved activations)."""
-    if not is_split_bf16(cfg):
-        return False
-    lib = _lib.load()
-    return bool(lib.tdq_jet_fused_active(cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"],
-                                         *_lo_args(cfg)))
-
-
-def fused_override(v):
-    """Tests: force the persistent kernels off (0) / on (1), or back to ``TDQ_FUSED`` (None).
-    Buffers allocated before the switch no longer fit the kernels after it."""
-    _lib.load().tdq_jet_fused_override(-1 if v is None else int(v))
-
-
 def is_split_bf16(cfg):
     """The fused split-bf16 kernels (csrc/jet_bf3.h) serve this configuration."""
     return cfg["precision"] in ("bf16x3", "bf16") and not is_layered(cfg)

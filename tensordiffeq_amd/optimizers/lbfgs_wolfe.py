@@ -21,8 +21,10 @@ conditions of Hager & Zhang (TFP's default line search; ``delta = 0.1``, ``sigma
 ``epsilon = 1e-6``): near the minimum the loss changes only at its rounding level, where the
 sufficient-decrease test is noise - a trial within ``epsilon |f0|`` of ``f0`` whose slope satisfies
 ``sigma g0.d <= g.d <= (2 delta - 1) g0.d`` is accepted.  It runs on the host on the two scalars of
-each trial.  Stops: ``max_iterations``, ``max|g| <= tolerance``, a line search that finds
-no decrease, or an unchanged loss (TFP's zero x / f tolerances).
+each trial.  A line search that finds no decrease along the L-BFGS direction drops the history and
+retries along steepest descent (as for a non-descent direction); only when that fails too does the
+run stop.  Stops: ``max_iterations``, ``max|g| <= tolerance``, no decrease along steepest descent
+either, or an unchanged loss (TFP's zero x / f tolerances).
 
 On a CPU (or without graphs) the same operations run eagerly; that path is the oracle of the tests
 (tests/test_lbfgs_wolfe.py).
@@ -60,8 +62,9 @@ class WolfeLBFGS:
 
     def __init__(self, evaluate, x, m=10, tolerance=1e-20, max_ls=25, all_reduce=None, capture_all_reduce=False,
                  use_graph=None):
-        if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 1:
-            raise ValueError("x must be a contiguous 1-D float32 tensor")
+        # float64: the diagnostic runs on a float64 objective (tools/wolfe_diag.py)
+        if x.dtype not in (torch.float32, torch.float64) or not x.is_contiguous() or x.dim() != 1:
+            raise ValueError("x must be a contiguous 1-D float32 / float64 tensor")
         self.evaluate, self.x, self.m = evaluate, x, int(m)
         self.tolerance, self.max_ls = float(tolerance), int(max_ls)
         self.all_reduce, self.capture_all_reduce = all_reduce, bool(capture_all_reduce)
@@ -69,18 +72,20 @@ class WolfeLBFGS:
         self.cuda = x.is_cuda
         self.use_graph = self.cuda if use_graph is None else (bool(use_graph) and self.cuda)
         p = x.numel()
-        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        dt = x.dtype
+        z = lambda *s: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         self.x0, self.g0, self.d, self.q = x.detach().clone(), z(p), z(p), z(p)
         self.xl, self.gl, self.gt = z(p), z(p), z(p)
         self.S, self.Y = z(self.m, p), z(self.m, p)
         self.rho, self.ys, self.yy, self.alpha = z(self.m), z(self.m), z(self.m), z(self.m)
         pin = self.cuda
-        self.t_host = torch.zeros(1, dtype=torch.float32, pin_memory=pin)
+        self.t_host = torch.zeros(1, dtype=dt, pin_memory=pin)
         self.t_dev = z(1)
-        self.out_host = torch.zeros(4, dtype=torch.float32, pin_memory=pin)
+        self.out_host = torch.zeros(4, dtype=dt, pin_memory=pin)
         self.out_dev = z(4)
         self.graphs = {}
         self.n_iter = self.func_eval = 0
+        self.n_restarts = 0       # line searches retried along steepest descent
         self.reason = "running"
         self.f_hist = []
 
@@ -291,6 +296,13 @@ class WolfeLBFGS:
             t = min(1.0, 1.0 / g1) if self.n_iter == 0 or restarted else 1.0
             res = self._search(t, f0, gtd0, dmax)
             if res is None:
+                if not restarted:
+                    # drop the history and retry along steepest descent (x0, g0 are untouched by
+                    # a failed search) before giving up - ADVICE r5
+                    self.rho.zero_()
+                    restarted = True
+                    self.n_restarts += 1
+                    continue
                 self.reason = "line search found no decrease"
                 break
             t, f1, gtd1 = res

@@ -46,6 +46,7 @@ class DistContext:
         self.initialized = initialized
         self.forced = forced
         self.peer = None            # parallel.peer.PeerComm when the one-shot all-reduce is on
+        self.retired_peers = []     # communicators settle() switched away from (kept allocated)
         self.allreduce_info = {"impl": "torch.distributed"}
 
     @property
@@ -93,8 +94,8 @@ class DistContext:
     def check_health(self):
         """Raise if the peer all-reduce ever timed out waiting for a rank (read at the
         progress / NaN-check cadence, never inside a step)."""
-        if self.peer is not None:
-            self.peer.check()
+        for comm in ([self.peer] if self.peer is not None else []) + self.retired_peers:
+            comm.check()
 
     def broadcast_(self, buf, src=0):
         if self.is_distributed:
@@ -160,13 +161,29 @@ def launcher_env():
     return any(v in os.environ for v in _LAUNCHER_VARS)
 
 
+def _interactive_shell():
+    """True inside a Jupyter kernel (``ipykernel`` is the kernel process itself) or a running
+    IPython shell.  A library that merely imports IPython does not make a plain script interactive,
+    so for IPython the test is whether an IPython instance exists, not whether the module is loaded."""
+    import sys
+    if "ipykernel" in sys.modules:
+        return True
+    ip = sys.modules.get("IPython")
+    if ip is None:
+        return False
+    try:
+        return ip.get_ipython() is not None
+    except Exception:  # noqa: BLE001 - a broken / partial IPython import: not a shell
+        return False
+
+
 def relaunch_argv():
     """The arguments that re-run this program under ``torch.distributed.run``, or None when it
     is not a plain script / module run (an interactive interpreter, a Jupyter / IPython kernel,
     ``python -c``, an embedding host): those must train at world 1 rather than re-run
     something else N times.  ``python -m pkg.mod args`` -> ``-m pkg.mod args``."""
     import sys
-    if hasattr(sys, "ps1") or "ipykernel" in sys.modules or "IPython" in sys.modules:
+    if hasattr(sys, "ps1") or _interactive_shell():
         return None
     main = sys.modules.get("__main__")
     argv = list(sys.argv)
@@ -322,9 +339,11 @@ def shard(t, rank, world):
 
 def destroy():
     global _CTX
-    if _CTX is not None and _CTX.peer is not None:
-        _CTX.peer.close()
+    if _CTX is not None:
+        for comm in ([_CTX.peer] if _CTX.peer is not None else []) + _CTX.retired_peers:
+            comm.close()
         _CTX.peer = None
+        _CTX.retired_peers = []
     if dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

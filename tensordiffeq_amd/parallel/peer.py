@@ -210,7 +210,11 @@ def settle(ctx, n_floats):
     ctx.allreduce_info["settled"] = {"floats": int(n_floats), "peer_us": round(t_peer, 2),
                                      "torch_us": round(t_ref, 2), "choice": "peer" if all(use) else "torch"}
     if not all(use):
-        comm.close()
+        # route NEW collectives to torch.distributed but keep the communicator (its IPC receive
+        # slots and flags) allocated: HIP graphs captured before this point - a cached
+        # LossGradEngine graph, another AdamEngine's graphs at another bucket size - may still
+        # contain the peer kernel, and replaying them after a close would read freed memory
+        ctx.retired_peers.append(comm)
         ctx.peer = None
         ctx.allreduce_info["impl"] = "torch.distributed"
         ctx.allreduce_info["peer"] = "off: slower in-graph at the step's bucket size"

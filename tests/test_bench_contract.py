@@ -192,6 +192,14 @@ def test_relaunch_argv_forms(monkeypatch):
     monkeypatch.delitem(sys.modules, "ipykernel", raising=False)
     monkeypatch.delitem(sys.modules, "IPython", raising=False)
     assert tdist.relaunch_argv() == [os.path.join(ROOT, "bench.py"), "--gpus", "2"]
+    # a library that imports IPython does not make a plain script interactive
+    fake_ip = types.ModuleType("IPython")
+    fake_ip.get_ipython = lambda: None
+    monkeypatch.setitem(sys.modules, "IPython", fake_ip)
+    assert tdist.relaunch_argv() == [os.path.join(ROOT, "bench.py"), "--gpus", "2"]
+    fake_ip.get_ipython = lambda: object()                               # a running IPython shell
+    assert tdist.relaunch_argv() is None
+    monkeypatch.delitem(sys.modules, "IPython", raising=False)
     main.__spec__ = types.SimpleNamespace(name="examples.ac_dist")       # python -m examples.ac_dist
     assert tdist.relaunch_argv() == ["-m", "examples.ac_dist", "--gpus", "2"]
     main.__spec__ = None

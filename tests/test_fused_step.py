@@ -1,7 +1,8 @@
 """One-launch residual training step (ops/fused_step.py, csrc/jet_fused.h MODE 2).
 
-CPU: the generated kernel (headers + the residual group's loss as ``GenLoss``) compiles with hipRTC
-for gfx950 for several traced programs, and eligibility is decided from the program's layout.
+CPU: the generated kernels (headers + the program's loss as ``GenLoss``; the bf16 step and the
+bf16x3 objective) compile with hipRTC for gfx950 for several traced programs, and eligibility is
+decided from the program's layout.
 GPU: the fused step's loss, SA-weight gradients and parameter gradient match the separate-launch
 step (saved-activation kernels + specialized loss kernel) at the bf16 level, and a short training
 run follows the same trajectory.
@@ -60,7 +61,7 @@ def test_fused_step_source_compiles(problem, layers):
     assert fl.groups[-1].segs == [last]
     cfg = hip_config(prog.net, prog.plan, "bf16")
     lib = _lib.load()
-    lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], 2)
+    lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], 0)
     if lds < 0:   # a 1-MFMA-layer net ([2, 128, 128, 1]): MODE 2 needs two
         assert cfg["n_hidden"] - 1 < 2
         return
@@ -77,8 +78,9 @@ def test_fused_step_source_compiles(problem, layers):
     if problem == "ac":   # the periodic pair group reads its partner point
         assert "t + 1" in gen
     _compile_ok(fused_step.kernel_source(cfg["S"], nso, cfg["n_hidden"] - 1, lds, gen))
-    if problem == "ac":   # the dynamic tile queue variant (split layout of mixed programs)
-        _compile_ok(fused_step.kernel_source(cfg["S"], nso, cfg["n_hidden"] - 1, lds, gen, dyn=True))
+    lds3 = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], cfg["S"], 1)
+    assert 0 < lds3 <= 160 * 1024, lds3
+    _compile_ok(fused_step.kernel_source(cfg["S"], nso, cfg["n_hidden"] - 1, lds3, gen, lo=True))
 
 
 def test_fused_step_not_on_cpu():
@@ -89,33 +91,33 @@ def test_fused_step_not_on_cpu():
 
 
 # --------------------------------------------------------------------------- GPU ---------
-def _acsa(n_f, seed=0, problem="ac-sa"):
+def _acsa(n_f, seed=0, problem="ac-sa", precision="bf16"):
     import bench
     torch.manual_seed(seed)
-    return bench.PROBLEMS[problem]["build"](n_f, 1, "hip", torch.device("cuda", 0), False, "bf16",
+    return bench.PROBLEMS[problem]["build"](n_f, 1, "hip", torch.device("cuda", 0), False, precision,
                                             layers=(2, 128, 128, 128, 128, 1))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("problem,n_f,mixed,dyn", [("ac-sa", 50000, "split", "0"), ("ac-sa", 3001, "split", "0"),
-                                                   ("ac-sa", 50000, "split", "1"),
-                                                   ("ac-baseline", 20000, "split", "1"),
-                                                   ("ac-baseline", 20000, "split", "0"),
-                                                   ("ac-baseline", 20000, "1", "0")])
-def test_fused_step_matches_separate_launches(problem, n_f, mixed, dyn, monkeypatch):
+@pytest.mark.parametrize("problem,n_f,mixed,precision", [("ac-sa", 50000, "split", "bf16"),
+                                                         ("ac-sa", 3001, "split", "bf16"),
+                                                         ("ac-baseline", 20000, "split", "bf16"),
+                                                         ("ac-baseline", 20000, "1", "bf16"),
+                                                         ("ac-sa", 50000, "split", "bf16x3"),
+                                                         ("ac-sa", 3001, "split", "bf16x3")])
+def test_fused_step_matches_separate_launches(problem, n_f, mixed, precision, monkeypatch):
     """One evaluation: every loss term, the theta gradient and the SA-weight gradients of the fused
     step vs the separate launches (saved-activation kernels + specialized loss kernel).  AC-SA runs
     every group in the fused launch (IC with SA weights, the periodic pairs, the residual);
     AC-baseline (order-4 periodic streams): split layout - every main-plan output fused, the
     u_xxx / u_xxxx outputs on the jet_hi side chain; layout "1" - the residual only."""
     monkeypatch.setenv("TDQ_FUSED_STEP_MIXED", mixed)
-    monkeypatch.setenv("TDQ_FS_DYNAMIC", dyn)   # the dynamic tile queue (opt-in)
     from tensordiffeq_amd.fit import LossGradEngine
     from tensordiffeq_amd.ops import fused_step
     out = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("TDQ_FUSED_STEP", flag)
-        m = _acsa(n_f, problem=problem)
+        m = _acsa(n_f, problem=problem, precision=precision)
         prog = m.program()
         fop = prog.fused_op
         fs = fused_step.for_program(prog)
@@ -124,7 +126,7 @@ def test_fused_step_matches_separate_launches(problem, n_f, mixed, dyn, monkeypa
             assert fs.mixed == (problem == "ac-baseline")
             if fs.mixed:
                 assert fs.layout == ("split" if mixed == "split" else "residual")
-            assert fs.dyn == (dyn == "1")
+            assert fs.lo == (precision == "bf16x3")
         else:
             assert fs is None
         eng = LossGradEngine(m, prog, m.lambdas)
@@ -134,12 +136,15 @@ def test_fused_step_matches_separate_launches(problem, n_f, mixed, dyn, monkeypa
     g1, g0 = out["1"][0][:-1], out["0"][0][:-1]
     rel = ((g1 - g0).norm() / g0.norm()).item()
     terms = [(a.item(), b.item()) for a, b in zip(out["1"][2], out["0"][2])]
-    print(f"FUSED_STEP {problem} n_f={n_f} terms {[(f'{a:.5e}', f'{b:.5e}') for a, b in terms]} grad rel {rel:.3e}")
+    print(f"FUSED_STEP {problem} n_f={n_f} {precision} terms {[(f'{a:.5e}', f'{b:.5e}') for a, b in terms]} grad rel {rel:.3e}")
+    # bf16: the two kernel designs round different operands (layer 0's tanh form, slab precision);
+    # bf16x3: both at the split-bf16 level
+    tl, tg = (2e-2, 3e-2) if precision == "bf16" else (5e-5, 1e-4)
     for a, b in terms:
-        assert abs(a - b) <= 2e-2 * abs(b) + 1e-6, terms
-    assert rel < 3e-2, rel
+        assert abs(a - b) <= tl * abs(b) + 1e-6, terms
+    assert rel < tg, rel
     for a, b in zip(out["1"][1], out["0"][1]):
-        assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < 3e-2
+        assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < tg
 
 
 @pytest.mark.gpu
@@ -168,29 +173,3 @@ def test_fused_step_deterministic(monkeypatch):
     a = eng.evaluate_fg().clone()
     b = eng.evaluate_fg().clone()
     assert torch.equal(a, b)
-
-
-@pytest.mark.gpu
-def test_fused_step_weight_lo_gradient_vs_fp64():
-    """newton_precision "bf16w" (the weights' hi + lo parts in every GEMM, fp32 slab rows): the
-    L-BFGS objective's gradient is closer to the fp64 jet than the bf16 step's."""
-    import bench
-    from tensordiffeq_amd.fit import LossGradEngine
-    from tensordiffeq_amd.ops import fused_step
-    dev = torch.device("cuda", 0)
-    m = bench.build_problem(20000, 1, "hip", dev, False, "bf16")
-    prog = m.program()
-    ref = bench.build_problem(20000, 1, "jet", dev, False, "bf16")
-    p64 = m.u_model.flat.detach().double().requires_grad_(True)
-    lams = [lam.detach().double() for lam in m.lambdas]
-    tot, _ = ref.program().evaluate(p64, lams)
-    g64, = torch.autograd.grad(tot, [p64])
-    errs = {}
-    for wlo in (False, True):
-        assert fused_step.for_program(prog, wlo=wlo) is not None
-        fg = LossGradEngine(m, prog, m.lambdas, weight_lo=wlo).evaluate_fg().double()
-        torch.cuda.synchronize()
-        errs[wlo] = (((fg[:-1] - g64).norm() / g64.norm()).item(), abs(fg[-1].item() - tot.item()) / tot.item())
-    print(f"FUSED_STEP_WLO grad/loss rel err vs fp64: bf16 {errs[False]}, bf16w {errs[True]}")
-    assert errs[True][0] < 3e-2 and errs[True][1] < 2e-2
-    assert errs[True][0] <= errs[False][0] * 1.05

@@ -1,8 +1,8 @@
-"""Step-time regression bounds on MI355X (~1.15x the measured values, box-to-box spread is ~5 %):
-the flagship AC-SA bf16 Adam step on the fused step (ops/fused_step.py: 0.165-0.170 ms,
-profiles/r5unr_unroll_sweep.jsonl, r5acc_accuracy_ab.jsonl) and the AC-baseline step with its
-order-4 periodic BC on the fused step's split layout (main-plan outputs fused, the u_xxx / u_xxxx
-outputs on the jet_hi.hip side chain: 0.207 ms, profiles/r5split_ac_baseline_layouts.txt)."""
+"""Step-time regression bounds on MI355X (~1.12x the driver's measured values; box-to-box spread is
+~5 %): the flagship AC-SA bf16 Adam step on the fused step (ops/fused_step.py: BENCH_r05 0.1657 ms)
+and the AC-baseline step with its order-4 periodic BC on the fused step's split layout (main-plan
+outputs fused, the u_xxx / u_xxxx outputs on the jet_hi.hip side chain: 0.207-0.215 ms,
+profiles/r5split_ac_baseline_layouts.txt)."""
 import os
 import sys
 
@@ -32,7 +32,7 @@ def test_ac_sa_step_time():
     ms, m = _step_ms("ac-sa")
     print(f"PERF ac-sa {ms:.4f} ms/step")
     assert m.active_backend == "hip"
-    assert ms < 0.195, ms
+    assert ms < 0.185, ms
 
 
 @pytest.mark.timeout(240)
@@ -44,15 +44,15 @@ def test_ac_baseline_step_time_on_fused_path():
     from tensordiffeq_amd.ops import fused_step
     fs = fused_step.for_program(prog)
     assert fs is not None and fs.layout == "split", prog.fused_step_reason
-    assert ms < 0.24, ms   # measured 0.207 ms (profiles/r5split_ac_baseline_layouts.txt)
+    assert ms < 0.235, ms   # measured 0.207-0.215 ms (profiles/r5split_ac_baseline_layouts.txt)
 
 
 @pytest.mark.timeout(300)
 def test_ac_baseline_step_within_ac_sa_ratio():
     """The order-4 periodic program keeps a fused path: same box, same process, its step within
-    1.35x the AC-SA step (measured 1.23x: 0.207 / 0.168 ms - the jet_hi side chain's kernels only
+    1.30x the AC-SA step (measured 1.23-1.28x: 0.207 / 0.168 ms - the jet_hi side chain's kernels only
     get the CUs the persistent fused workgroups leave, profiles/r5split2_timeline_*)."""
     sa, _ = _step_ms("ac-sa")
     acb, _ = _step_ms("ac-baseline")
     print(f"PERF ratio ac-baseline / ac-sa {acb / sa:.3f} ({acb:.4f} / {sa:.4f} ms)")
-    assert acb / sa < 1.35, (acb, sa)
+    assert acb / sa < 1.30, (acb, sa)

@@ -14,19 +14,6 @@ from tensordiffeq_amd.boundaries import IC, DomainND, periodicBC
 from tensordiffeq_amd.ops.loss_fused import LF_BLOCK, FusedLossOp
 
 
-@pytest.fixture(autouse=True)
-def _saved_activation_kernels():
-    """Point ranges serve the saved-activation kernels (bf16x3, TDQ_FUSED=0, plans outside the
-    persistent kernels' envelope); the bf16 AC plan below would otherwise take the persistent
-    kernels, which run one launch over every point (test_no_ranges_with_persistent_kernels)."""
-    from tensordiffeq_amd.ops import _lib, jet_hip
-    if _lib.available():
-        jet_hip.fused_override(0)
-    yield
-    if _lib.available():
-        jet_hip.fused_override(None)
-
-
 def _program(n_f=20000):
     tdq.set_seed(0)
     D = DomainND(["x", "t"], time_var="t")
@@ -131,16 +118,3 @@ def test_cut_on_slab_chunk_boundary_enables_prereduce(monkeypatch):
     monkeypatch.delenv("TDQ_PREREDUCE")
     off = [(0, r[0][1] + 128) + r[0][2:], (r[0][1] + 128,) + r[1][1:]]
     assert fit.prereduce_chunk(prog, off) == 0
-
-
-def test_no_ranges_with_persistent_kernels(monkeypatch):
-    from tensordiffeq_amd.ops import _lib, jet_hip
-    if not _lib.available():
-        pytest.skip("native library not built")
-    prog, fop = _program()
-    prog.precision = "bf16"
-    monkeypatch.setenv("TDQ_SPLIT", "auto")
-    jet_hip.fused_override(1)
-    assert fit.point_ranges(prog, fop) is None
-    prog.precision = "bf16x3"                              # L-BFGS objective: saved activations
-    assert fit.point_ranges(prog, fop) is not None
