@@ -210,6 +210,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   };
   int t = t0;
   if (t < t1) fetch(t);
+  TDQ_TS(0);
   while (t < t1) {
     const int pb = P.p_lo + t * PT;
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
@@ -217,6 +218,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     if (tid < PT * TDQ_MAXD) xs[tid] = xpre;
     if (t + 1 < t1) fetch(t + 1);
     __syncthreads();
+    FZ_TS(1);
 
     // ---- layer 0 -> slot 0 ----------------------------------------------------------------
     {
@@ -225,6 +227,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       fz3_put_h<WT, S>(slot(0), L, o, h, fz3_vimg(slot(0), WT, S) + voff);
     }
     __syncthreads();
+    FZ_TS(2);
 
     // ---- hidden layers 1..LM on MFMA ------------------------------------------------------
 #pragma unroll
@@ -232,6 +235,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
       f32x4 z[S], h[S];
       fz3_gemm<WT, S>(z, Wimg, ly, o, slot(ly - 1), L, l);
+      FZ_TS(1 + 2 * ly);
       z[0] += *reinterpret_cast<const f32x4*>(bi + 16 * o + 4 * g);
       tanh_jet_f<S, NSO>(sp, z, h);
       // h_l into slot l; h_LM waits in h_0's slot for the loss and the top adjoint
@@ -248,6 +252,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
         }
       }
       __syncthreads();
+      FZ_TS(2 + 2 * ly);
     }
 
     // ---- J of the tile's points: the wave-ordered sums of the partial dots -------------------
@@ -266,6 +271,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     asm volatile("" : "+v"(tl));
     if (tl < PT) LossF::template eval<S, PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc);
     __syncthreads();
+    FZ_TS(9);
     // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
     {
       __bf16* im = slot(0);
@@ -308,8 +314,10 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     for (int ly = LM; ly >= 1; --ly) {
       const __bf16* Z = slot(ly == LM ? 0 : ly);
       __bf16* H = slot(ly - 1);
+      const int tb = 10 + 5 * (LM - ly);
       f32x4 acc[S];
       fz3_gemm<WT, S>(acc, Kimg, ly, o, Z, L, l);
+      FZ_TS(tb);
       bf16x4 zbh[S], zbl[S];
       float rb = 0.f;
       if (ly >= 2) {
@@ -321,8 +329,10 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
         for (int s = 0; s < S; ++s) split4(zb[s], zbh[s], zbl[s]);
       }
       fz3_dk<WT, S, NR, NC>(dk[ly - 1], H, Z, r0, c0, l);
+      FZ_TS(tb + 1);
       if (ly >= 2) {
         __syncthreads();  // every wave's dK reads of H are done
+        FZ_TS(tb + 2);
         if ((p & 3) == 0) accB[(ly - 1) * W + 16 * o + 4 * g + (p >> 2)] += rb;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -354,6 +364,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
           if ((p & 3) == 0) accK0[j * W + fo] += r;
         }
       }
+      FZ_TS(tb + 3);
       if (ly == 2) {  // rebuild h_0 into slot 0 (zb_LM there is consumed)
         if (LM == 2) __syncthreads();  // (LM = 2: it was this step's Z)
         f32x4 h[S];
@@ -361,9 +372,11 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
         fz3_put_h<WT, S>(slot(0), L, o, h, fz3_vimg(slot(0), WT, S) + voff);
       }
       if (ly >= 2) __syncthreads();
+      FZ_TS(tb + 4);
     }
     ++t;
   }
+  TDQ_TS(62);
 
   // ---- this workgroup's gradient-slab row (fp32) ---------------------------------------------
   float* gs = P.slab + (size_t)(P.srow + gi) * Pst;
@@ -393,4 +406,5 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       if (l == 0 && k < P.nacc) P.lpart[(size_t)(P.prow + gi) * P.nacc + k] = v;
     }
   }
+  TDQ_TS(63);
 }

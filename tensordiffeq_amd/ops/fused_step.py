@@ -149,20 +149,26 @@ def gen_loss(groups, n_terms, nacc, S):
     return "\n".join(L)
 
 
+def kernel_name(lo=False):
+    """``tdq_fused_step`` (bf16 step) / ``tdq_fused_step3`` (bf16x3 objective): distinct names in
+    the kernel traces."""
+    return "tdq_fused_step3" if lo else "tdq_fused_step"
+
+
 def kernel_source(S, nso, LM, lds, gen, lo=False):
     """The kernel translation unit: the headers, the generated loss, and ``tdq_fused_step`` over
     ``fz_body`` (bf16, 32-point tiles) or ``fz3_body`` (``lo``: bf16x3, 16-point tiles)."""
     body = "fz3_body" if lo else "fz_body"
     return (header_source() + "\n" + gen + "\n"
             'extern "C" __global__ void __launch_bounds__(64 * FZ_WAVES) '
-            "__attribute__((amdgpu_waves_per_eu(2, 2))) tdq_fused_step(FzParams P) {\n"
+            f"__attribute__((amdgpu_waves_per_eu(2, 2))) {kernel_name(lo)}(FzParams P) {{\n"
             f"  __shared__ __attribute__((aligned(16))) char lds[{lds}];\n"
             f"  {body}<8, {S}, {nso}, {LM}, GenLoss>(P, lds);\n"
             "}\n")
 
 
-def _compile(src):
-    """``(module, function)`` of the fused-step kernel in ``src`` (compiled once per process)."""
+def _compile(src, name="tdq_fused_step"):
+    """``(module, function)`` of the fused-step kernel ``name`` in ``src`` (compiled once per process)."""
     lib = _lib.load(required=True)
     arch = loss_jit.device_arch()
     opts = _opts()
@@ -176,7 +182,7 @@ def _compile(src):
             raise RuntimeError(f"hipRTC compile failed ({rc}): {log.value.decode(errors='replace')[:2000]}")
         try:
             mod, fn = ctypes.c_void_p(0), ctypes.c_void_p(0)
-            _lib.check(lib.tdq_rtc_load(code, b"tdq_fused_step", ctypes.byref(mod), ctypes.byref(fn)),
+            _lib.check(lib.tdq_rtc_load(code, name.encode(), ctypes.byref(mod), ctypes.byref(fn)),
                        "hipModuleLoadData")
         finally:
             lib.tdq_rtc_free(code)
@@ -350,7 +356,7 @@ class FusedStepOp:
             self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
             self.srow = -(-self.p_bc // pts_b)
         self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), lo=self.lo)
-        self.module, self.func = _compile(self.source)
+        self.module, self.func = _compile(self.source, kernel_name(self.lo))
         ntiles = -(-(self.N - self.p_lo) // self.pt)
         cus = max(1, lib.tdq_device_cus())
         rounds = -(-ntiles // cus)
