@@ -514,6 +514,66 @@ template <> struct SlabType<true> { using T = __bf16; };
 __device__ __forceinline__ void slab_put(float* p, float v) { slab_store(p, v); }
 __device__ __forceinline__ void slab_put(__bf16* p, float v) { *p = (__bf16)v; }
 
+// Weight images written element by element (the inverse of the pack kernels of jet_bf3.hip): the
+// Adam tail (tail_adam_kernel) and the L-BFGS direction kernel (lbfgs.hip) scatter every updated
+// parameter straight into the next evaluation's images, so no pack launch is needed.
+struct TailImg {
+  __bf16* fimg;  // forward A image (nullptr: no image update)
+  __bf16* bimg;  // backward A image
+  float* aux;
+  NetDims d;
+  int WT;
+};
+
+// element (row, kf) of hidden layer `layer`'s A image -> bf16 hi / lo (inverse of pack_frag)
+__device__ __forceinline__ void img_put(__bf16* __restrict__ img, int layer, int row, int kf, int WT, __bf16 hi,
+                                        __bf16 lo) {
+  const int KB = WT / 2;
+  const int o = row >> 4, p = row & 15, kb = kf >> 5, rr = kf & 31;
+  const int g = (rr & 15) >> 2, j = (rr & 3) + (rr >= 16 ? 4 : 0);
+  const int lane = p + 16 * g;
+  const size_t frag = ((size_t)(layer - 1) * WT + o) * KB + kb;
+  img[((frag * 2) * 64 + lane) * 8 + j] = hi;
+  img[((frag * 2 + 1) * 64 + lane) * 8 + j] = lo;
+}
+
+// flat (Keras-order) parameter e with new value v -> its slot in the images (inverse of pack_all)
+__device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti) {
+  const NetDims& d = ti.d;
+  const int W = 16 * ti.WT, w = hw(d, 0);
+  const int n0 = d.d_in * w;
+  if (e < n0) {
+    const int j = e / w;
+    ti.aux[j * W + (e - j * w)] = v;
+    return;
+  }
+  if (e < n0 + w) {
+    ti.aux[aux_b0(d, W) + (e - n0)] = v;
+    return;
+  }
+  if (e < off_layer(d, d.n_hidden)) {  // hidden layer i >= 1: kernel [w_{i-1}][w_i], bias [w_i]
+    int i = 1;
+    while (i + 1 < d.n_hidden && e >= off_layer(d, i + 1)) ++i;
+    const int q = e - off_layer(d, i), wi = hw(d, i - 1), wo = hw(d, i);
+    if (q < wi * wo) {
+      const int in = q / wo, out = q - in * wo;
+      const __bf16 hi = (__bf16)v, lo = (__bf16)(v - (float)hi);
+      img_put(ti.fimg, i, out, in, ti.WT, hi, lo);  // forward: A[row = out][k = in]
+      img_put(ti.bimg, i, in, out, ti.WT, hi, lo);  // backward: A[row = in][k = out]
+    } else {
+      ti.aux[aux_bh(d, W) + (i - 1) * W + (q - wi * wo)] = v;
+    }
+    return;
+  }
+  const int r2 = e - off_layer(d, d.n_hidden), wl = hw(d, d.n_hidden - 1);
+  if (r2 < wl * d.d_out) {
+    const int f = r2 / d.d_out;
+    ti.aux[aux_ko(d, W) + f * 4 + (r2 - f * d.d_out)] = v;
+  } else {
+    ti.aux[aux_bo(d, W) + (r2 - wl * d.d_out)] = v;
+  }
+}
+
 // layer 0 (input -> width, VALU; derivative streams are rows of K0): the post-activation streams of
 // feature tile t (forward).
 template <int WT, int S, int NSO>

@@ -156,63 +156,6 @@ __global__ void __launch_bounds__(256) slab_reduce2_bf3(const float* __restrict_
     if (4 * q + e < P) grad[4 * q + e] = gx != nullptr ? a[e] + gx[4 * q + e] : a[e];
 }
 
-struct TailImg {
-  __bf16* fimg;  // forward A image (nullptr: no image update)
-  __bf16* bimg;  // backward A image
-  float* aux;
-  NetDims d;
-  int WT;
-};
-
-// element (row, kf) of hidden layer `layer`'s A image -> bf16 hi / lo (inverse of pack_frag)
-__device__ __forceinline__ void img_put(__bf16* __restrict__ img, int layer, int row, int kf, int WT, __bf16 hi,
-                                        __bf16 lo) {
-  const int KB = WT / 2;
-  const int o = row >> 4, p = row & 15, kb = kf >> 5, rr = kf & 31;
-  const int g = (rr & 15) >> 2, j = (rr & 3) + (rr >= 16 ? 4 : 0);
-  const int lane = p + 16 * g;
-  const size_t frag = ((size_t)(layer - 1) * WT + o) * KB + kb;
-  img[((frag * 2) * 64 + lane) * 8 + j] = hi;
-  img[((frag * 2 + 1) * 64 + lane) * 8 + j] = lo;
-}
-
-// flat (Keras-order) parameter e with new value v -> its slot in the images (inverse of pack_all)
-__device__ __forceinline__ void scatter_param(float v, int e, const TailImg& ti) {
-  const NetDims& d = ti.d;
-  const int W = 16 * ti.WT, w = hw(d, 0);
-  const int n0 = d.d_in * w;
-  if (e < n0) {
-    const int j = e / w;
-    ti.aux[j * W + (e - j * w)] = v;
-    return;
-  }
-  if (e < n0 + w) {
-    ti.aux[aux_b0(d, W) + (e - n0)] = v;
-    return;
-  }
-  if (e < off_layer(d, d.n_hidden)) {  // hidden layer i >= 1: kernel [w_{i-1}][w_i], bias [w_i]
-    int i = 1;
-    while (i + 1 < d.n_hidden && e >= off_layer(d, i + 1)) ++i;
-    const int q = e - off_layer(d, i), wi = hw(d, i - 1), wo = hw(d, i);
-    if (q < wi * wo) {
-      const int in = q / wo, out = q - in * wo;
-      const __bf16 hi = (__bf16)v, lo = (__bf16)(v - (float)hi);
-      img_put(ti.fimg, i, out, in, ti.WT, hi, lo);  // forward: A[row = out][k = in]
-      img_put(ti.bimg, i, in, out, ti.WT, hi, lo);  // backward: A[row = in][k = out]
-    } else {
-      ti.aux[aux_bh(d, W) + (i - 1) * W + (q - wi * wo)] = v;
-    }
-    return;
-  }
-  const int r2 = e - off_layer(d, d.n_hidden), wl = hw(d, d.n_hidden - 1);
-  if (r2 < wl * d.d_out) {
-    const int f = r2 / d.d_out;
-    ti.aux[aux_ko(d, W) + f * 4 + (r2 - f * d.d_out)] = v;
-  } else {
-    ti.aux[aux_bo(d, W) + (r2 - wl * d.d_out)] = v;
-  }
-}
-
 // Adam over every group, one ELEMENT per thread (args.start in elements; float4 slots per thread
 // measured ~2 us slower per step, profiles/r2_v10_ab_tail_elem.jsonl); group 0 = theta, whose
 // gradient is the second slab pass of its column (the f32x4 pass's summation order, so the
@@ -694,5 +637,20 @@ int tdq_fused_step_launch(void* func, const float* X, float* scratch, float* wor
 }
 
 int tdq_fused_params_size() { return (int)sizeof(FzParams); }
+
+// The weight-image target of a forward scratch (TailImg: forward / backward A images + aux image)
+// for kernels that scatter updated parameters into it (lbfgs.hip lbfgs_dir_step_kernel); returns
+// the struct's size, or -1 (unsupported network / buffer too small).
+int tdq_img_target(float* scratch, int d_in, const int* widths, int d_out, int n_hidden, void* out, int out_bytes) {
+  NetDims d;
+  if (scratch == nullptr || out == nullptr || !make_dims(d, d_in, widths, 0, d_out, n_hidden)) return -1;
+  const int WT = width_tiles(d.width);
+  if (WT < 2 || out_bytes < (int)sizeof(TailImg)) return -1;
+  float *img, *bimg, *aux;
+  scratch_images(scratch, n_hidden, WT, &img, &bimg, &aux);
+  TailImg ti{reinterpret_cast<__bf16*>(img), reinterpret_cast<__bf16*>(bimg), aux, d, WT};
+  *reinterpret_cast<TailImg*>(out) = ti;
+  return (int)sizeof(TailImg);
+}
 
 }  // extern "C"

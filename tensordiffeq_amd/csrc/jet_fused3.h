@@ -44,17 +44,27 @@ __host__ __device__ inline int fz3_lds_bytes(const NetDims& d, int WT, int S, in
   return fz_nslot(LM) * fz3_slot_bytes(WT, S) + fz3_fl_floats(d, WT, S, LM) * 4;
 }
 
-// acc[s] = sum_kb A(o, kb) B(kb, s), both split: A from the weight image (hi + lo fragments, all
-// k-blocks issued up front: one L2 latency per GEMM instead of one per k-block), B from the slot's
-// hi / lo images; three MFMAs per product (lo terms first, as mfma3)
-template <int WT, int S>
-__device__ __forceinline__ void fz3_gemm(f32x4 (&acc)[S], const bf16x8* __restrict__ wimg, int layer, int o,
-                                         const __bf16* im, const FzLane& L, int l) {
-  constexpr int KB = WT / 2, RS = bf3_img_rs(WT), SIMG = FZ3_PT * RS, SP = fz3_sp(S), NSTEP = WT * KB;
+// A fragments (hi + lo, every k-block) of one GEMM's weight-image rows, all issued at the GEMM's
+// start (one L2 latency per GEMM).  Issuing them one phase ahead (right after the previous GEMM's
+// MFMAs, so the latency hides behind the epilogue / loss) measured SLOWER: 430 vs 324 us per
+// objective evaluation - the 32 extra live VGPRs spilled (28 vs 12, gpurun_out r6e)
+template <int WT>
+struct Fz3W {
+  bf16x8 h[WT / 2], l[WT / 2];
+};
+template <int WT>
+__device__ __forceinline__ void fz3_load_w(Fz3W<WT>& w, const bf16x8* __restrict__ wimg, int layer, int o, int l) {
+  constexpr int KB = WT / 2, NSTEP = WT * KB;
   const Tl Wi = tl_make(wimg + (size_t)(layer - 1) * NSTEP * 128, l);
-  bf16x8 ah[KB], al[KB];
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) img_frag<true>(Wi, o * KB + kb, ah[kb], al[kb]);
+  for (int kb = 0; kb < KB; ++kb) img_frag<true>(Wi, o * KB + kb, w.h[kb], w.l[kb]);
+}
+
+// acc[s] = sum_kb A(o, kb) B(kb, s), both split: A from the preloaded weight fragments, B from the
+// slot's hi / lo images; three MFMAs per product (lo terms first, as mfma3)
+template <int WT, int S>
+__device__ __forceinline__ void fz3_gemm(f32x4 (&acc)[S], const Fz3W<WT>& w, const __bf16* im, const FzLane& L) {
+  constexpr int KB = WT / 2, RS = bf3_img_rs(WT), SIMG = FZ3_PT * RS, SP = fz3_sp(S);
 #pragma unroll
   for (int s = 0; s < S; ++s) acc[s] = zero4();
 #pragma unroll
@@ -66,7 +76,7 @@ __device__ __forceinline__ void fz3_gemm(f32x4 (&acc)[S], const bf16x8* __restri
       bl[s] = fz_bfrag<RS>(im + (SP + s) * SIMG, L, 0, kb);
     }
 #pragma unroll
-    for (int s = 0; s < S; ++s) acc[s] = mfma3(ah[kb], al[kb], bh[s], bl[s], acc[s]);
+    for (int s = 0; s < S; ++s) acc[s] = mfma3(w.h[kb], w.l[kb], bh[s], bl[s], acc[s]);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -210,6 +220,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   };
   int t = t0;
   if (t < t1) fetch(t);
+  Fz3W<WT> wf;  // a GEMM's weight fragments
   TDQ_TS(0);
   while (t < t1) {
     const int pb = P.p_lo + t * PT;
@@ -234,7 +245,8 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     for (int ly = 1; ly <= LM; ++ly) {
       const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
       f32x4 z[S], h[S];
-      fz3_gemm<WT, S>(z, Wimg, ly, o, slot(ly - 1), L, l);
+      fz3_load_w<WT>(wf, Wimg, ly, o, l);
+      fz3_gemm<WT, S>(z, wf, slot(ly - 1), L);
       FZ_TS(1 + 2 * ly);
       z[0] += *reinterpret_cast<const f32x4*>(bi + 16 * o + 4 * g);
       tanh_jet_f<S, NSO>(sp, z, h);
@@ -316,7 +328,8 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       __bf16* H = slot(ly - 1);
       const int tb = 10 + 5 * (LM - ly);
       f32x4 acc[S];
-      fz3_gemm<WT, S>(acc, Kimg, ly, o, Z, L, l);
+      fz3_load_w<WT>(wf, Kimg, ly, o, l);
+      fz3_gemm<WT, S>(acc, wf, Z, L);
       FZ_TS(tb);
       bf16x4 zbh[S], zbl[S];
       float rb = 0.f;

@@ -27,6 +27,7 @@
 // tensordiffeq_amd/optimizers/lbfgs_device.py).  Once a stopping test fires every kernel is a
 // no-op, so graph replays past convergence change nothing.
 #include "common.h"
+#include "jet_bf3.h"
 
 #define LB_MAXM 64
 #define LB_NF 5
@@ -592,7 +593,10 @@ __global__ void __launch_bounds__(256) lbfgs_axpy_kernel(float* __restrict__ x, 
 //                     fixed lr), so every element does x += t d right after computing d (old x
 //                     kept in x_prev); the last-ticket block reduces g.d / |d|_1 and runs the
 //                     descent test - in the rare stop case it restores x from x_prev, so the
-//                     trajectory is bit-identical to the five-launch path.
+//                     trajectory is bit-identical to the five-launch path.  With a weight-image
+//                     target (the split-bf16 objective's scratch) every new x element is also
+//                     scattered into the next evaluation's bf16 hi / lo A images and fp32 aux
+//                     image, so the objective runs without its pack launch.
 // The order of every reduction is the five-launch path's: same values, bit for bit.
 __global__ void __launch_bounds__(256) lbfgs_dots_logic_kernel(const float* __restrict__ fg,
                                                                const float* __restrict__ g_old,
@@ -628,7 +632,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
                                                              float* __restrict__ best_x, float* __restrict__ x_prev,
                                                              double* __restrict__ st, const double* __restrict__ coef,
                                                              double* __restrict__ part2, int* __restrict__ ticket,
-                                                             LbCfg c) {
+                                                             LbCfg c, TailImg ti) {
   __shared__ double red[8];
   __shared__ double qs[4][64];
   __shared__ int last, stop;
@@ -670,7 +674,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
         // write-through (sc1): a plain store would leave a dirty line in this XCD's L2 whose
         // write-back at kernel end could land after the last block's restore of the same element.
         __hip_atomic_store(&x_prev[j], xj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&x[j], fmaf(tn, df, xj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float xn = fmaf(tn, df, xj);
+        __hip_atomic_store(&x[j], xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ti.fimg != nullptr) scatter_param(xn, j, ti);  // the next evaluation's weight images
         acc[0] += (double)g * df;
         acc[1] += fabs((double)df);
       }
@@ -713,9 +719,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
   if (stop) {  // undo the speculative step: x stays where the reference leaves it
     // every block stored x_prev / x write-through and drained them before its ticket (vmcnt(0)
     // above): sc1 loads see them, sc1 stores overwrite the speculative x in memory
-    for (int j = threadIdx.x; j < c.p; j += 256)
-      __hip_atomic_store(&x[j], __hip_atomic_load(&x_prev[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = threadIdx.x; j < c.p; j += 256) {
+      const float xo = __hip_atomic_load(&x_prev[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&x[j], xo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ti.fimg != nullptr) scatter_param(xo, j, ti);  // (the images' lines: one block, kernel end)
+    }
   }
 }
 
@@ -756,12 +764,18 @@ int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, fl
 
 // The same update in two launches (lbfgs_dots_logic + lbfgs_dir_step, see above); it also takes
 // the step (no tdq_lbfgs_axpy).  ticket: 2 ints, zero on the first call (re-armed by the kernels);
-// x_prev: p floats.
+// x_prev: p floats; img (nullable): a TailImg (tdq_img_target) whose images the step also writes.
 int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
                            float* x_prev, double* st, double* SY, double* YY, double* coef, double* part, double* part2,
                            float* fhist, int* ticket, int p, int m, int max_iter, int nchunks, int nblk, int fhist_len,
-                           double max_eval, double lr, double tol_fun, double tol_x, int legacy_stop, void* stream) {
+                           double max_eval, double lr, double tol_fun, double tol_x, int legacy_stop, const void* img,
+                           void* stream) {
   if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
+  TailImg ti{};
+  if (img != nullptr) {
+    ti = *reinterpret_cast<const TailImg*>(img);
+    if (param_count(ti.d) != p) return (int)hipErrorInvalidValue;  // images of another network
+  }
   LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t lds = lbfgs_logic_lds(m);
@@ -776,7 +790,7 @@ int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, fl
                      YY, coef, fhist, ticket, c);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(lbfgs_dir_step_kernel, dim3(nblk), dim3(256), 0, s, x, fg, g_old, d, S, Y, best_x, x_prev, st,
-                     coef, part2, ticket + 1, c);
+                     coef, part2, ticket + 1, c, ti);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -764,7 +764,29 @@ class LossGradEngine:
             self._tail = ok
         return ok
 
-    def _body(self):
+    def _fused_bufs(self):
+        """Persistent forward / backward buffers of the one-launch objective."""
+        if getattr(self, "_fbufs", None) is None:
+            from .ops import jet_hip
+            prog = self.program
+            J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
+                                             rows=prog.fused_op.fl.n_streams)
+            self._fbufs = (J, saved, jet_hip.alloc_backward(saved))
+        return self._fbufs
+
+    def image_target(self):
+        """``(img_target, evaluate_fg without the pack launch)`` when the objective is the
+        one-launch fused step (its weight images can be written by the optimizer's own update
+        kernel, csrc/lbfgs.hip), else ``None``."""
+        fop = getattr(self.program, "fused_op", None)
+        if fop is None or not self._fused_tail() or getattr(self.program, "hi_op", None) is not None:
+            return None
+        from .ops import fused_step, jet_hip
+        if fused_step.for_program(self.program) is None:
+            return None
+        return jet_hip.img_target(self._fused_bufs()[1]), (lambda: self._body(pack=False))
+
+    def _body(self, pack=True):
         fop = getattr(self.program, "fused_op", None)
         if fop is not None:
             from .ops import jet_hip
@@ -777,13 +799,12 @@ class LossGradEngine:
                 hi = prog.hi_op
                 gx = hi.grad if hi is not None else None
                 from .ops import fused_step
-                # the one-launch objective (bf16: jet_fused.h, bf16x3: jet_fused3.h)
+                # the one-launch objective (bf16: jet_fused.h, bf16x3: jet_fused3.h) on persistent
+                # buffers (the image target of the device L-BFGS points into their scratch)
                 fs = fused_step.for_program(prog)
                 if fs is not None:
-                    J, saved = jet_hip.alloc_forward(prog.X_all, self.flat, prog.net, prog.plan, prog.precision,
-                                                     rows=fop.fl.n_streams)
-                    work = jet_hip.alloc_backward(saved)
-                    fs.run(saved, J, work, self.flat, pack=True)
+                    J, saved, work = self._fused_bufs()
+                    fs.run(saved, J, work, self.flat, pack=pack)
                     jet_hip.dp_tail_a(saved, work, fg[:-1], fop, total=fg[-1:], gextra=gx, **fs.tail_kw())
                     return fg
                 if self._ranges:

@@ -15,6 +15,7 @@ reports the true global loss (B4); repeated ``fit`` calls resume (B6); L-BFGS ru
 from __future__ import annotations
 
 import math
+import os
 import time
 
 import numpy as np
@@ -559,8 +560,12 @@ class CollocationSolverND:
 
             def on_poll(opt):
                 ctx.check_health()   # a peer all-reduce timeout inside the L-BFGS graph
-                it = opt.n_iter
-                f = float(opt.st[lbfgs_device.F])
+                polled = getattr(opt, "polled", None)   # the pipelined poll's host snapshot
+                if polled is not None:
+                    it, f = polled["n_iter"], polled["f"]
+                else:
+                    it = opt.n_iter
+                    f = float(opt.st[lbfgs_device.F])
                 if self.metrics is not None:
                     self.metrics.log("lbfgs", it, f)
                 bar.n = min(it, newton_iter)
@@ -572,7 +577,8 @@ class CollocationSolverND:
                                         capture_all_reduce=ctx.capturable(flat.numel() + 1),
                                         use_graph=_use_graphs(self.device),
                                         poll_every=max(1, min(int(self.log_every), 64)), on_poll=on_poll,
-                                        stop=stop)
+                                        stop=stop, images=eng.image_target()
+                                        if os.environ.get("TDQ_LBFGS_IMAGES", "1") != "0" else None)
             ctx.check_health()
             with torch.no_grad():
                 flat.copy_(opt.best_x)
@@ -598,14 +604,18 @@ class CollocationSolverND:
             # L-BFGS with 10 pairs and tolerance 1e-20, state on the device (optimizers/lbfgs_wolfe.py)
             from ..fit import _use_graphs
             from ..optimizers import lbfgs_wolfe
+            prec = getattr(getattr(eng, "program", None), "precision", None)
+            prec = prec if getattr(getattr(eng, "program", None), "backend", None) == "hip" else "fp32"
             opt = lbfgs_wolfe.minimize(eng.evaluate_fg, flat.data, newton_iter,
                                        all_reduce=ctx.all_reduce_ if ctx.is_distributed else None,
                                        capture_all_reduce=ctx.capturable(flat.numel() + 1),
-                                       use_graph=_use_graphs(self.device), on_iter=on_eval)
+                                       use_graph=_use_graphs(self.device), on_iter=on_eval,
+                                       hz_eps=lbfgs_wolfe.hz_eps_for(prec))
             ctx.check_health()
             self.min_loss["l-bfgs"] = float(opt.min_loss)
             self.best_epoch["l-bfgs"] = int(opt.n_iter)
             info = {"impl": "strong-wolfe" + (" (device)" if opt.use_graph else ""), "n_iter": int(opt.n_iter),
+                    "hz_eps": opt.hz_eps,
                     "func_evals": int(opt.func_eval), "reason": opt.reason, "restarts": int(opt.n_restarts)}
         bar.close()
         self._best_flat["l-bfgs"] = flat.detach().clone()

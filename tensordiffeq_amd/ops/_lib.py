@@ -79,7 +79,8 @@ def _declare(lib):
         "tdq_lbfgs_nst": (I, []),
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
-        "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P]),
+        "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P, P]),
+        "tdq_img_target": (I, [P, I, P, I, I, P, I]),
         "tdq_layered_epi": (I, [I, P, P, P, L, I, I, P, P, P, P, P, P]),
         # high-order (<= 4) jets of small point sets (csrc/jet_hi.hip, ops/jet_hi.py)
         "tdq_jet_hi_scratch_floats": (L, [I, I]),

@@ -454,13 +454,10 @@ class FusedStepOp:
                    "tdq_rtc_set_global_ptr")
 
     def tail_kw(self):
-        """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows (bf16x3:
-        ``dp_tail_a`` only, its slab rows are fp32)."""
-        kw = {"rows": self.rows, "lpart": self.fop.partials if self.layout == "residual" else self.lpart,
-              "n_lblocks": self.n_lblocks}
-        if self.lo:
-            kw["half"] = False
-        return kw
+        """Keyword arguments of ``jet_hip.step_tail`` / ``dp_tail_a`` for this step's rows (the slab
+        precision follows the program's: bf16 rows for bf16, fp32 rows for bf16x3)."""
+        return {"rows": self.rows, "lpart": self.fop.partials if self.layout == "residual" else self.lpart,
+                "n_lblocks": self.n_lblocks}
 
 
 def for_program(prog):

@@ -197,6 +197,19 @@ def pack_images(saved):
     _lib.check(rc, "tdq_jet_bf3_pack")
 
 
+def img_target(saved):
+    """The weight-image target of a forward scratch (``csrc`` ``TailImg``: forward / backward A
+    images + aux image) as a ctypes buffer: kernels that update the parameters scatter the new
+    values into it (the L-BFGS direction kernel), so the next evaluation needs no pack launch."""
+    lib = _lib.load()
+    X, P, scratch, cfg, spec, S = saved
+    buf = ctypes.create_string_buffer(256)
+    rc = lib.tdq_img_target(_lib.ptr(scratch), cfg["d_in"], _warg(cfg), cfg["d_out"], cfg["n_hidden"], buf, 256)
+    if rc <= 0:
+        raise RuntimeError("tdq_img_target: unsupported network")
+    return buf
+
+
 def slab_geometry(cfg, N):
     """``(points per backward workgroup, slab rows, first-pass chunks, rows per chunk)`` of the
     split-bf16 backward over N points (``tdq_bf3_slab_geometry``)."""

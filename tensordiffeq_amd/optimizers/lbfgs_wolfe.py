@@ -39,6 +39,23 @@ from ..graphs import capture_graph
 
 C1, C2 = 1e-4, 0.9
 HZ_DELTA, HZ_SIGMA, HZ_EPS = 0.1, 0.9, 1e-6   # approximate Wolfe (Hager & Zhang 2005, TFP's defaults)
+# approximate-Wolfe loss tolerance per objective precision.  HZ's epsilon must cover the noise of
+# f: with the split-bf16 objective (hi + lo operands, gradient 3.4e-6 vs fp64) TFP's 1e-6 makes
+# the line search fail on AC-SA after ~1.2k of 10k iterations (L2 0.106), 1e-5 / 1e-4 after
+# 1.3k / 3.8k, while 1e-3 runs all 10k (L2 4.9e-2, loss 0.061 -> 0.0044); the same start on the
+# fp32 / fp64 objectives (N_f 5k) runs the full schedule at 1e-6 (tools/wolfe_diag.py,
+# profiles/r6g_wolfe_diag.jsonl, r6h_wolfe_eps_sweep.jsonl)
+HZ_EPS_BY_PRECISION = {"fp32": HZ_EPS, "bf16x3": 1e-3, "bf16": 1e-2}
+
+
+def hz_eps_for(precision):
+    """The approximate-Wolfe tolerance for an objective evaluated in ``precision``
+    (``TDQ_WOLFE_EPS`` overrides)."""
+    import os
+    env = os.environ.get("TDQ_WOLFE_EPS")
+    if env:
+        return float(env)
+    return HZ_EPS_BY_PRECISION.get(precision, HZ_EPS)
 
 
 def _cubic(x1, f1, g1, x2, f2, g2, lo, hi):
@@ -61,12 +78,13 @@ class WolfeLBFGS:
     ``[grad | loss]`` at the current ``x`` (it reads ``x`` itself, like the device L-BFGS)."""
 
     def __init__(self, evaluate, x, m=10, tolerance=1e-20, max_ls=25, all_reduce=None, capture_all_reduce=False,
-                 use_graph=None):
+                 use_graph=None, hz_eps=HZ_EPS):
         # float64: the diagnostic runs on a float64 objective (tools/wolfe_diag.py)
         if x.dtype not in (torch.float32, torch.float64) or not x.is_contiguous() or x.dim() != 1:
             raise ValueError("x must be a contiguous 1-D float32 / float64 tensor")
         self.evaluate, self.x, self.m = evaluate, x, int(m)
         self.tolerance, self.max_ls = float(tolerance), int(max_ls)
+        self.hz_eps = float(hz_eps)   # approximate-Wolfe loss tolerance (relative to |f0|)
         self.all_reduce, self.capture_all_reduce = all_reduce, bool(capture_all_reduce)
         dev = x.device
         self.cuda = x.is_cuda
@@ -211,7 +229,7 @@ class WolfeLBFGS:
         n = 0
 
         def approx_wolfe(f, gtd):
-            return f <= f0 + HZ_EPS * abs(f0) and HZ_SIGMA * gtd0 <= gtd <= (2.0 * HZ_DELTA - 1.0) * gtd0
+            return f <= f0 + self.hz_eps * abs(f0) and HZ_SIGMA * gtd0 <= gtd <= (2.0 * HZ_DELTA - 1.0) * gtd0
 
         while n < self.max_ls:
             f, gtd = self._trial(t)
@@ -329,9 +347,9 @@ class WolfeLBFGS:
 
 
 def minimize(evaluate, x, max_iter, m=10, tolerance=1e-20, all_reduce=None, capture_all_reduce=False,
-             use_graph=None, on_iter=None):
+             use_graph=None, on_iter=None, hz_eps=HZ_EPS):
     """Line-search L-BFGS on ``x`` (in place; left at the final iterate).  Returns the
     :class:`WolfeLBFGS` (``n_iter``, ``func_eval``, ``reason``, ``min_loss``, ``f_hist``)."""
     opt = WolfeLBFGS(evaluate, x, m=m, tolerance=tolerance, all_reduce=all_reduce,
-                     capture_all_reduce=capture_all_reduce, use_graph=use_graph)
+                     capture_all_reduce=capture_all_reduce, use_graph=use_graph, hz_eps=hz_eps)
     return opt.minimize(max_iter, on_iter=on_iter)

@@ -300,3 +300,22 @@ def test_fused_update_descent_stop_restores_x(monkeypatch):
         outs.append((x.clone(), opt.reason, opt.n_iter))
     assert outs[0][1] == outs[1][1] == LD.REASONS[5]
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][0], torch.ones(5000, device="cuda"))
+
+
+@pytest.mark.gpu
+def test_device_lbfgs_images_from_update_match_pack(monkeypatch):
+    """The fused update scatters the next x into the one-launch objective's weight images
+    (TDQ_LBFGS_IMAGES, default on) instead of a pack launch per evaluation: the same trajectory,
+    bit for bit (AC-SA, bf16x3 objective)."""
+    import bench
+    from tensordiffeq_amd.ops import fused_step
+    hist = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TDQ_LBFGS_IMAGES", flag)
+        m = bench.build_problem(4096, 1, "hip", torch.device("cuda", 0), False, "bf16", newton_precision="bf16x3")
+        m.fit(tf_iter=200)
+        m.fit(newton_iter=60)
+        assert fused_step.for_program(m.program(precision="bf16x3")) is not None
+        hist[flag] = (m.lbfgs_state.history(), m.u_model.flat.detach().clone())
+    assert hist["1"][0] == hist["0"][0]
+    assert torch.equal(hist["1"][1], hist["0"][1])

@@ -104,19 +104,44 @@ def test_solver_graph_mode_lbfgs_cpu():
 
 @pytest.mark.gpu
 def test_graph_lbfgs_on_gpu():
+    """newton_eager=False on the HIP objective (bf16x3, one-launch fused step): the line search
+    does not give up early (it used to stop after 27 of 100 iterations with TFP's 1e-6
+    approximate-Wolfe tolerance), and the loss it reaches is within the same range as the same
+    algorithm on the float64 torch-jet objective from the same start (trajectories of a line
+    search from a raw start are not reproducible across objectives: measured 301 -> 37.9 on the
+    split-bf16 objective with the precision-aware tolerance 1e-3 vs -> 20.2 in fp64 with 1e-6)."""
     import time
 
     import bench
+    from tensordiffeq_amd.optimizers import lbfgs_wolfe
     torch.manual_seed(0)
-    m = bench.build_problem(20000, 1, "hip", torch.device("cuda", 0), False, "bf16")
+    dev = torch.device("cuda", 0)
+    m = bench.build_problem(20000, 1, "hip", dev, False, "bf16", newton_precision="bf16x3")
     m.fit(tf_iter=50)
     before = m.min_loss["adam"]
+    x0 = m.u_model.flat.detach().clone()
     t0 = time.perf_counter()
     m.fit(newton_iter=100, newton_eager=False)
     dt = time.perf_counter() - t0
     info = m.fit_info["lbfgs"]
-    print(f"WOLFE_GPU iters {info['n_iter']} evals {info['func_evals']} reason {info['reason']} "
-          f"loss {before:.4e} -> {m.min_loss['l-bfgs']:.4e} wall {dt:.2f}s")
+    # the same 100 iterations on the float64 objective (torch jet, no graphs)
+    ref = bench.build_problem(20000, 1, "jet", dev, False, "bf16")
+    prog = ref.program()
+    lam64 = [lam.detach().double() for lam in m.lambdas]
+    x = x0.double().clone()
+
+    def evaluate():
+        p = x.detach().requires_grad_(True)
+        tot, _ = prog.evaluate(p, lam64)
+        g, = torch.autograd.grad(tot, [p])
+        return torch.cat([g.reshape(-1), tot.detach().reshape(1)])
+    opt64 = lbfgs_wolfe.minimize(evaluate, x, 100, use_graph=False)
+    print(f"WOLFE_GPU iters {info['n_iter']} evals {info['func_evals']} restarts {info['restarts']} reason "
+          f"{info['reason']} eps {info['hz_eps']} loss {before:.4e} -> {m.min_loss['l-bfgs']:.4e} wall {dt:.2f}s; "
+          f"fp64 objective: iters {opt64.n_iter} reason {opt64.reason} loss {opt64.min_loss:.4e}")
     assert info["impl"] == "strong-wolfe (device)"
-    assert m.min_loss["l-bfgs"] < before
+    assert info["n_iter"] == 100, info          # no early stop on a failed line search
+    assert opt64.n_iter == 100
+    assert m.min_loss["l-bfgs"] < 0.25 * before
     assert info["func_evals"] <= 3 * info["n_iter"] + 5
+    assert m.min_loss["l-bfgs"] < 2.5 * opt64.min_loss and opt64.min_loss < 2.5 * m.min_loss["l-bfgs"]

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--objectives", nargs="*", default=["fp64", "bf16x3", "fp32"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--hz-eps", type=float, nargs="*", default=[1e-6],
+                    help="approximate-Wolfe loss tolerances to run (HIP objectives)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     m = bench.build_problem(a.npts, 1, "hip", dev, False, "bf16", seed=a.seed)
@@ -47,7 +49,8 @@ def main():
             "l2": float(bench.l2_on_ac_grid(m))}
     print(json.dumps(rec0), flush=True)
     out = [rec0]
-    for obj in a.objectives:
+    runs = [(obj, e) for obj in a.objectives for e in (a.hz_eps if obj != "fp64" else [1e-6])]
+    for obj, eps in runs:
         with torch.no_grad():
             m.u_model.flat.copy_(x_adam)
             for lam, v in zip(m.lambdas, lams):
@@ -70,13 +73,13 @@ def main():
             evaluate = eng.evaluate_fg
             use_graph = True
         t0 = time.perf_counter()
-        opt = lbfgs_wolfe.minimize(evaluate, x, a.iters, use_graph=use_graph)
+        opt = lbfgs_wolfe.minimize(evaluate, x, a.iters, use_graph=use_graph, hz_eps=eps)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         with torch.no_grad():
             m.u_model.flat.copy_(x.float())
         f = opt.f_hist
-        rec = {"what": "wolfe", "objective": obj, "npts": a.npts, "seed": a.seed, "n_iter": opt.n_iter,
+        rec = {"what": "wolfe", "objective": obj, "hz_eps": eps, "npts": a.npts, "seed": a.seed, "n_iter": opt.n_iter,
                "func_evals": opt.func_eval, "restarts": opt.n_restarts, "reason": opt.reason,
                "f_start": f[0], "f_end": f[-1], "f_at": {str(k): f[k] for k in (10, 100, 1000, 3000, 5000) if k < len(f)},
                "s": round(wall, 2), "ms_per_eval": round(1e3 * wall / max(1, opt.func_eval), 3),
