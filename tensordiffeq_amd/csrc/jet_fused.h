@@ -77,13 +77,18 @@ __host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int
 // 2.57e-2 with tanh_s1 (profiles/r5acc2_l2_six_seeds.jsonl).  In the hidden layers the cheap form
 // cost accuracy (L2 median 2.99e-2, profiles/r5acc_accuracy_ab.jsonl): they use tanh_jet_f.
 // !CHEAP (the bf16x3 objective, jet_fused3.h): tanh_s1, the saved-activation kernels' tanh.
-template <int WT, int S, int NSO, bool CHEAP = true>
+template <int WT, int S, int NSO, bool CHEAP = true, int DIN = 0>
 __device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const NetDims& d, const float* xrow, int t,
                                       int g, f32x4 (&h)[S]) {
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
   const int f0 = 16 * t + 4 * g;
   f32x4 z = *reinterpret_cast<const f32x4*>(aux + aux_b0(d, W) + f0);
-  for (int j = 0; j < d.d_in; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+  if constexpr (DIN > 0) {  // compile-time input width (the generated fused-step kernels)
+#pragma unroll
+    for (int j = 0; j < DIN; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+  } else {
+    for (int j = 0; j < d.d_in; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+  }
   f32x4 ka[S];
   ka[0] = zero4();
 #pragma unroll
@@ -257,7 +262,10 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   const float* __restrict__ aux_g = P.aux;
   const int N = P.N, Pst = P.Pst, ntiles = P.ntiles;
   const NetDims& d = P.d;
-  const JetSpec& sp = P.sp;
+  // the stream spec and input width as compile-time constants of the generated loss struct
+  // (ops/fused_step.py spec_source): the one-hot stream selects and first-layer loops fold away
+  constexpr JetSpec sp = LossF::SPEC;
+  constexpr int DIN = LossF::DIN;
   constexpr int W = 16 * WT, OPW = WT / 4, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
   constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
   constexpr int ZS = 0;                    // slot of h_LM / zb_LM (h_0's slot once layer 1 has read it)
@@ -307,7 +315,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   const float* Ko = aux + aux_ko(d, W);
 
   // layer 0 (input -> width, VALU) of feature tile o0 + oo at this lane's point
-  auto layer0 = [&](int oo, f32x4(&h)[S]) { fz_h0<WT, S, NSO>(sp, aux, d, xs + row * TDQ_MAXD, o0 + oo, g, h); };
+  auto layer0 = [&](int oo, f32x4(&h)[S]) { fz_h0<WT, S, NSO, true, DIN>(sp, aux, d, xs + row * TDQ_MAXD, o0 + oo, g, h); };
 
   // this thread's element of a tile's x (one: FZ_PT * TDQ_MAXD <= 512), fetched one tile ahead so
   // the global latency hides behind the current tile
@@ -500,7 +508,8 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
             const float r = row16_sum4(zb[0]);
             if ((p & 3) == 0) accB[fo] += r;
           }
-          for (int j = 0; j < d.d_in; ++j) {
+#pragma unroll
+          for (int j = 0; j < DIN; ++j) {
             const float xj = xs[row * TDQ_MAXD + j];
             f32x4 vv;
 #pragma unroll

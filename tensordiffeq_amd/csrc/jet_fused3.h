@@ -152,7 +152,10 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   const float* __restrict__ aux_g = P.aux;
   const int N = P.N, Pst = P.Pst, ntiles = P.ntiles;
   const NetDims& d = P.d;
-  const JetSpec& sp = P.sp;
+  // the stream spec and input width as compile-time constants of the generated loss struct
+  // (ops/fused_step.py spec_source): the one-hot stream selects and first-layer loops fold away
+  constexpr JetSpec sp = LossF::SPEC;
+  constexpr int DIN = LossF::DIN;
   constexpr int W = 16 * WT, RS = bf3_img_rs(WT), SIMG = FZ3_PT * RS, SP = fz3_sp(S), VRS = fz3_vrs();
   constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
   constexpr int SLOT = fz3_slot_bytes(WT, S), PT = FZ3_PT;
@@ -206,7 +209,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   const float* Ko = aux + aux_ko(d, W);
 
   // layer 0 (input -> width, VALU; the accurate tanh) of this wave's feature tile at this lane's point
-  auto layer0 = [&](f32x4(&h)[S]) { fz_h0<WT, S, NSO, false>(sp, aux, d, xs + p * TDQ_MAXD, o, g, h); };
+  auto layer0 = [&](f32x4(&h)[S]) { fz_h0<WT, S, NSO, false, DIN>(sp, aux, d, xs + p * TDQ_MAXD, o, g, h); };
 
   static_assert(PT * TDQ_MAXD <= 64 * FZ_WAVES, "one element per thread");
   float xpre = 0.f;
@@ -362,7 +365,8 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
           const float r = row16_sum4(zb[0]);
           if ((p & 3) == 0) accB[fo] += r;
         }
-        for (int j = 0; j < d.d_in; ++j) {
+#pragma unroll
+        for (int j = 0; j < DIN; ++j) {
           const float xj = xs[p * TDQ_MAXD + j];
           f32x4 vv;
 #pragma unroll

@@ -68,7 +68,33 @@ def header_source():
     return "\n".join(out)
 
 
-def gen_loss(groups, n_terms, nacc, S):
+def spec_source(spec, S, d_in):
+    """``SPEC`` / ``DIN`` members of the generated struct: the plan's stream spec (csrc
+    jet_common.h ``make_spec``) and the input width as compile-time constants, so the kernel's
+    one-hot stream selects and first-layer loops fold away (the kernels require them)."""
+    if spec is None or d_in is None:
+        raise ValueError("gen_loss: the stream spec and d_in are compile-time constants of the kernel")
+    M = 8   # TDQ_MAXS
+    st, var, ia, ib = [0] * M, [0] * M, [0] * M, [0] * M
+    selA = [[0.0] * M for _ in range(M)]
+    selB = [[0.0] * M for _ in range(M)]
+    for s in range(S):
+        ty, a, b = spec[3 * s:3 * s + 3]
+        st[s] = ty
+        if ty == 1:
+            var[s] = a
+        if ty == 2:
+            ia[s], ib[s] = a, b
+            selA[s][a] = 1.0
+            selB[s][b] = 1.0
+    arr = lambda v: "{" + ", ".join(str(x) for x in v) + "}"  # noqa: E731
+    mat = lambda m: "{" + ", ".join("{" + ", ".join(f"{x:.1f}f" for x in r) + "}" for r in m) + "}"  # noqa: E731
+    return [f"  static constexpr JetSpec SPEC = {{{arr(st)}, {arr(var)}, {mat(selA)}, {mat(selB)}, {arr(ia)}, "
+            f"{arr(ib)}}};",
+            f"  static constexpr int DIN = {int(d_in)};"]
+
+
+def gen_loss(groups, n_terms, nacc, S, spec=None, d_in=None):
     """``struct GenLoss`` of the loss groups laid out in the fused point set.  ``groups``: one
     ``(program, start, n_slots, n)`` per group - its ``n`` instances occupy points ``start + k``
     (one slot) or the pairs ``start + 2k, start + 2k + 1`` (two slots: a periodic pair side by side,
@@ -82,6 +108,8 @@ def gen_loss(groups, n_terms, nacc, S):
     e = L.append
     e("struct GenLoss {")
     e(f"  static constexpr int NACC = {max(1, nacc)};")
+    for ln in spec_source(spec, S, d_in):
+        e(ln)
 
     def branches(body):
         kw = "if"
@@ -167,27 +195,100 @@ def kernel_source(S, nso, LM, lds, gen, lo=False):
             "}\n")
 
 
-def _compile(src, name="tdq_fused_step"):
-    """``(module, function)`` of the fused-step kernel ``name`` in ``src`` (compiled once per process)."""
+_PENDING = {}   # source key -> (thread, [code bytes | exception])
+
+
+def _key(src):
+    return hashlib.sha256((loss_jit.device_arch() + _opts() + src).encode()).hexdigest()
+
+
+def _rtc_compile(src):
+    """hipRTC compile of ``src`` to code-object bytes (host only: no GPU call)."""
     lib = _lib.load(required=True)
-    arch = loss_jit.device_arch()
-    opts = _opts()
-    key = hashlib.sha256((arch + opts + src).encode()).hexdigest()
-    if key not in _CACHE:
-        code, size = ctypes.c_void_p(0), ctypes.c_longlong(0)
-        log = ctypes.create_string_buffer(16384)
-        rc = lib.tdq_rtc_compile_ex(src.encode(), b"tdq_fused_step.hip", arch.encode(), opts.encode(),
-                                    ctypes.byref(code), ctypes.byref(size), log, len(log))
-        if rc != 0:
-            raise RuntimeError(f"hipRTC compile failed ({rc}): {log.value.decode(errors='replace')[:2000]}")
+    code, size = ctypes.c_void_p(0), ctypes.c_longlong(0)
+    log = ctypes.create_string_buffer(16384)
+    rc = lib.tdq_rtc_compile_ex(src.encode(), b"tdq_fused_step.hip", loss_jit.device_arch().encode(),
+                                _opts().encode(), ctypes.byref(code), ctypes.byref(size), log, len(log))
+    if rc != 0:
+        raise RuntimeError(f"hipRTC compile failed ({rc}): {log.value.decode(errors='replace')[:2000]}")
+    try:
+        return ctypes.string_at(code, size.value)
+    finally:
+        lib.tdq_rtc_free(code)
+
+
+def compile_async(src):
+    """Start the hipRTC compile of ``src`` on a host thread (ctypes releases the GIL), so a later
+    :func:`_compile` of the same source only loads the module.  No-op when it is cached or pending."""
+    import threading
+    k = _key(src)
+    if k in _CACHE or k in _PENDING:
+        return
+    out = []
+
+    def work():
         try:
-            mod, fn = ctypes.c_void_p(0), ctypes.c_void_p(0)
-            _lib.check(lib.tdq_rtc_load(code, name.encode(), ctypes.byref(mod), ctypes.byref(fn)),
-                       "hipModuleLoadData")
-        finally:
-            lib.tdq_rtc_free(code)
-        _CACHE[key] = (mod, fn)
-    return _CACHE[key]
+            out.append(_rtc_compile(src))
+        except Exception as e:  # noqa: BLE001 - re-raised by _compile
+            out.append(e)
+    th = threading.Thread(target=work, name="tdq-rtc", daemon=True)
+    _PENDING[k] = (th, out)
+    th.start()
+
+
+def _compile(src, name="tdq_fused_step"):
+    """``(module, function)`` of the fused-step kernel ``name`` in ``src`` (compiled once per
+    process; a compile started by :func:`compile_async` is joined)."""
+    lib = _lib.load(required=True)
+    k = _key(src)
+    if k not in _CACHE:
+        pend = _PENDING.pop(k, None)
+        if pend is not None:
+            pend[0].join()
+            code = pend[1][0]
+            if isinstance(code, Exception):
+                raise code
+        else:
+            code = _rtc_compile(src)
+        buf = ctypes.create_string_buffer(code, len(code))
+        mod, fn = ctypes.c_void_p(0), ctypes.c_void_p(0)
+        _lib.check(lib.tdq_rtc_load(buf, name.encode(), ctypes.byref(mod), ctypes.byref(fn)), "hipModuleLoadData")
+        _CACHE[k] = (mod, fn)
+    return _CACHE[k]
+
+
+def prebuild(prog):
+    """Start compiling the fused step of a single-plan program in the background (the L-BFGS
+    objective while the Adam phase runs: its hipRTC compile, ~0.35 s, then overlaps the Adam
+    steps).  Returns whether a compile was started (or was already cached)."""
+    if not torch.cuda.is_available():
+        return False
+    fop = getattr(prog, "fused_op", None)
+    if ineligible(prog, fop) is not None or _mixed(prog):
+        return False
+    lib = _lib.load()
+    cfg = hip_config(prog.net, prog.plan, prog.precision)
+    S = cfg["S"]
+    spec = jet_hip.stream_spec(prog.plan)
+    nso = sum(1 for s in range(S) if spec[3 * s] == 2)
+    lo = cfg["precision"] == "bf16x3"
+    lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S, int(lo))
+    gen = gen_loss(_plain_layout(fop.fl), fop.n_terms, fop.n_terms + fop.n_scal, S, spec=spec, d_in=cfg["d_in"])
+    compile_async(kernel_source(S, nso, cfg["n_hidden"] - 1, lds, gen, lo=lo))
+    return True
+
+
+def _plain_layout(fl):
+    """``[(program, start, n_slots, n)]`` of the fused point set of a single-plan program: groups
+    in program order, pair groups on even offsets."""
+    layout, pos = [], 0
+    for gr in fl.groups:
+        ns = len(gr.segs)
+        if ns == 2 and pos % 2:
+            pos += 1
+        layout.append((gr.program, pos, ns, gr.n))
+        pos += ns * gr.n
+    return layout
 
 
 def ineligible(prog, fop):
@@ -355,7 +456,8 @@ class FusedStepOp:
             pts_b = jet_hip.slab_geometry(cfg, N)[0]
             self.p_bc = min(N, -(-self.seg_lo // 128) * 128) if self.seg_lo > 0 else 0
             self.srow = -(-self.p_bc // pts_b)
-        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S), lo=self.lo)
+        self.source = kernel_source(S, nso, LM, lds, gen_loss(layout, fop.n_terms, self.nacc, S, spec=spec,
+                                                              d_in=cfg["d_in"]), lo=self.lo)
         self.module, self.func = _compile(self.source, kernel_name(self.lo))
         ntiles = -(-(self.N - self.p_lo) // self.pt)
         cus = max(1, lib.tdq_device_cus())

@@ -73,7 +73,7 @@ def test_fused_step_source_compiles(problem, layers):
         pos += pos % 2 if ns == 2 else 0
         layout.append((gr.program, pos, ns, gr.n))
         pos += ns * gr.n
-    gen = fused_step.gen_loss(layout, op.n_terms, op.n_terms + op.n_scal, cfg["S"])
+    gen = fused_step.gen_loss(layout, op.n_terms, op.n_terms + op.n_scal, cfg["S"], spec=spec, d_in=cfg["d_in"])
     assert "JV(" in gen and "UB(" in gen
     if problem == "ac":   # the periodic pair group reads its partner point
         assert "t + 1" in gen

@@ -34,7 +34,7 @@ def sources():
         pos += pos % 2 if ns == 2 else 0
         layout.append((gr.program, pos, ns, gr.n))
         pos += ns * gr.n
-    gen = fused_step.gen_loss(layout, op.n_terms, op.n_terms + op.n_scal, S)
+    gen = fused_step.gen_loss(layout, op.n_terms, op.n_terms + op.n_scal, S, spec=spec, d_in=cfg["d_in"])
     out = {}
     for lo in (0, 1):
         lds = lib.tdq_jet_fused_lds(cfg["d_in"], jet_hip._warg(cfg), cfg["d_out"], cfg["n_hidden"], S, lo)
