@@ -82,7 +82,7 @@ __device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const
                                       int g, f32x4 (&h)[S]) {
   constexpr int S1 = S - 1 - NSO, SO = 1 + S1, W = 16 * WT;
   const int f0 = 16 * t + 4 * g;
-  f32x4 z = *reinterpret_cast<const f32x4*>(aux + aux_b0(d, W) + f0);
+  f32x4 z = *reinterpret_cast<const f32x4*>(aux + (DIN > 0 ? DIN * W : aux_b0(d, W)) + f0);
   if constexpr (DIN > 0) {  // compile-time input width (the generated fused-step kernels)
 #pragma unroll
     for (int j = 0; j < DIN; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
@@ -266,6 +266,11 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   // (ops/fused_step.py spec_source): the one-hot stream selects and first-layer loops fold away
   constexpr JetSpec sp = LossF::SPEC;
   constexpr int DIN = LossF::DIN;
+  // compile-time aux-image / LDS offsets (d_in = DIN, n_hidden = LM + 1): LDS accesses then take
+  // immediate offsets instead of runtime address arithmetic
+  constexpr int W_ = 16 * WT;
+  constexpr int A_B0 = DIN * W_, A_BH = (DIN + 1) * W_, A_KO = (DIN + LM + 1) * W_, A_BO = (DIN + LM + 5) * W_;
+  constexpr int NAUX = (A_BO + 4 + 3) / 4 * 4;           // fz_aux_floats
   constexpr int W = 16 * WT, OPW = WT / 4, RS = bf3_img_rs(WT), SIMG = FZ_PT * RS;
   constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
   constexpr int ZS = 0;                    // slot of h_LM / zb_LM (h_0's slot once layer 1 has read it)
@@ -274,12 +279,12 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   __bf16* img = reinterpret_cast<__bf16*>(lds_raw);
   auto slot = [&](int k) { return img + k * (S + 1) * SIMG; };
   float* fl = reinterpret_cast<float*>(img + fz_img_elems(WT, S, LM));
-  const int naux = fz_aux_floats(d, W);
+  constexpr int naux = NAUX;
   float* aux = fl;                            // the aux image (biases, K0, Ko, bo), copied once
   float* xs = aux + naux;                     // [FZ_PT][TDQ_MAXD]
   float* ubs = xs + FZ_PT * TDQ_MAXD;         // [S][FZ_PT][4] dJ of the tile
   float* part = ubs + S * FZ_PT * 4;          // [2 column tiles][...] partials
-  const int pq = (LM + 1) * W + d.d_in * W + 4 * W;  // partial floats per column tile
+  constexpr int pq = (LM + 1) * W + DIN * W + 4 * W;  // partial floats per column tile
   float* outp = part + 2 * pq + 4;            // [4][S][FZ_PT] output-layer dots
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
@@ -294,7 +299,6 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   float* accB = part + q * pq;                      // [LM + 1][W]  bias partials (layer 0..LM)
   float* accK0 = accB + (LM + 1) * W;               // [d_in][W]
   float* accKo = accK0 + d.d_in * W;                // [W][4]
-  float* accBo = part + 2 * pq;                     // [4]
   // Loop-invariant weight loads must not be hoisted out of the tile loop (they would pin ~100
   // VGPRs for the whole launch): the image pointers go through an opaque copy at every tile.
   const bf16x8* Wimg = P.fimg;
@@ -303,6 +307,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   for (int e = tid; e < naux; e += 64 * FZ_WAVES) aux[e] = e < aux_floats(d, W) ? aux_g[e] : 0.f;
   f32x4 dk[LM][NR][NC];
   float lacc[LossF::NACC];  // this point-thread's loss / scalar-gradient sums (all tiles)
+  float bo_acc = 0.f;       // this point-thread's output-bias gradient (its points' value-stream dJ)
 #pragma unroll
   for (int k = 0; k < LossF::NACC; ++k) lacc[k] = 0.f;
 #pragma unroll
@@ -312,7 +317,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) dk[i][r][c] = zero4();
   for (int e = tid; e < 2 * pq + 4; e += 64 * FZ_WAVES) part[e] = 0.f;
-  const float* Ko = aux + aux_ko(d, W);
+  const float* Ko = aux + A_KO;
 
   // layer 0 (input -> width, VALU) of feature tile o0 + oo at this lane's point
   auto layer0 = [&](int oo, f32x4(&h)[S]) { fz_h0<WT, S, NSO, true, DIN>(sp, aux, d, xs + row * TDQ_MAXD, o0 + oo, g, h); };
@@ -355,7 +360,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     // ---- hidden layers 1..LM on MFMA ------------------------------------------------------
 #pragma unroll
     for (int ly = 1; ly <= LM; ++ly) {
-      const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
+      const float* bi = aux + A_BH + (ly - 1) * W;
       f32x4 acc[OPW][S];
       fz_gemm<WT, S, OPW>(acc, Wimg, ly, o0, slot(ly - 1), q, L, l);
       FZ_TS(1 + 2 * ly);
@@ -409,7 +414,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       float a = outp[(0 * S + s) * FZ_PT + pt];
 #pragma unroll
       for (int ww = 1; ww < 4; ++ww) a += outp[(ww * S + s) * FZ_PT + pt];
-      outp[(0 * S + s) * FZ_PT + pt] = s == 0 ? a + aux[aux_bo(d, W)] : a;
+      outp[(0 * S + s) * FZ_PT + pt] = s == 0 ? a + aux[A_BO] : a;
     }
     __syncthreads();
     // ---- the per-point loss (generated code: every loss group of the program - residual, SA
@@ -420,6 +425,11 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     if (tl < FZ_PT) LossF::template eval<S, FZ_PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc);
     __syncthreads();
     FZ_TS(9);
+    // dbo: each point-thread adds its point's value-stream dJ (one LDS read; a 32-step loop on
+    // four lanes of wave 0 used to hold that wave - and the next barrier - for ~1-2k cycles)
+    tl = tid;
+    asm volatile("" : "+v"(tl));
+    if (tl < FZ_PT) bo_acc += ubs[tl * 4];
     // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
 #pragma unroll
     for (int oo = 0; oo < OPW; ++oo) {
@@ -449,13 +459,6 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       for (int s = 0; s < S; ++s) fz_put<RS>(im + s * SIMG, L, q, to, cvt_hi4(zb[s]));
     }
     __syncthreads();
-    int ll = l;
-    asm volatile("" : "+v"(ll));  // (its addresses recomputed per tile, not hoisted and spilled)
-    if (w == 0 && ll < 4) {  // dbo (ubs is complete since the tile's first barriers)
-      float a = 0.f;
-      for (int pt = 0; pt < FZ_PT; ++pt) a += ubs[pt * 4 + ll];
-      accBo[ll] += a;
-    }
     // ---- hidden layers LM..1: dK_l, hb_{l-1} = K_l zb_l, adjoint of tanh layer l-1 --------
 #pragma unroll
     for (int ly = LM; ly >= 1; --ly) {
@@ -574,9 +577,10 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       gs[off_layer(d, LM + 1) + f * d.d_out + qo] = (__bf16)(pA[k] + pB[k]);
     }
   }
-  if (tid < d.d_out) gs[off_layer(d, LM + 1) + W * d.d_out + tid] = (__bf16)accBo[tid];
-  // loss partials: the point-threads (wave 0, lanes < FZ_PT) summed
+  // the output bias (d_out = 1) and the loss partials: the point-threads (wave 0, lanes < FZ_PT) summed
   if (w == 0) {
+    const float bo = col4_sum(row16_sum(bo_acc));
+    if (l == 0) gs[off_layer(d, LM + 1) + W] = (__bf16)bo;
 #pragma unroll
     for (int k = 0; k < LossF::NACC; ++k) {
       const float v = col4_sum(row16_sum(lacc[k]));

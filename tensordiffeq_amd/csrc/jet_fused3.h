@@ -156,6 +156,11 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   // (ops/fused_step.py spec_source): the one-hot stream selects and first-layer loops fold away
   constexpr JetSpec sp = LossF::SPEC;
   constexpr int DIN = LossF::DIN;
+  // compile-time aux-image / LDS offsets (d_in = DIN, n_hidden = LM + 1): LDS accesses then take
+  // immediate offsets instead of runtime address arithmetic
+  constexpr int W_ = 16 * WT;
+  constexpr int A_B0 = DIN * W_, A_BH = (DIN + 1) * W_, A_KO = (DIN + LM + 1) * W_, A_BO = (DIN + LM + 5) * W_;
+  constexpr int NAUX = (A_BO + 4 + 3) / 4 * 4;           // fz_aux_floats
   constexpr int W = 16 * WT, RS = bf3_img_rs(WT), SIMG = FZ3_PT * RS, SP = fz3_sp(S), VRS = fz3_vrs();
   constexpr int NR = WT / 4, NC = WT / 2;  // dK tiles per wave: row block (w >> 1), column block (w & 1)
   constexpr int SLOT = fz3_slot_bytes(WT, S), PT = FZ3_PT;
@@ -164,12 +169,12 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   static_assert(SLOT % 16 == 0, "slot alignment");
   auto slot = [&](int k) { return reinterpret_cast<__bf16*>(lds_raw + k * SLOT); };
   float* fl = reinterpret_cast<float*>(lds_raw + fz_nslot(LM) * SLOT);
-  const int naux = fz_aux_floats(d, W);
+  constexpr int naux = NAUX;
   float* aux = fl;                            // the aux image (biases, K0, Ko, bo), copied once
   float* xs = aux + naux;                     // [PT][TDQ_MAXD]
   float* ubs = xs + PT * TDQ_MAXD;            // [S][PT][4] dJ of the tile
   float* part = ubs + S * PT * 4;             // partials
-  const int pq = (LM + 1) * W + d.d_in * W + 4 * W;
+  constexpr int pq = (LM + 1) * W + DIN * W + 4 * W;
   float* outp = part + pq + 4;                // [8 waves][S][PT] output-layer dots
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
@@ -183,7 +188,6 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   float* accB = part;                               // [LM + 1][W]  bias partials (layer 0..LM)
   float* accK0 = accB + (LM + 1) * W;               // [d_in][W]
   float* accKo = accK0 + d.d_in * W;                // [W][4]
-  float* accBo = part + pq;                         // [4]
   const bf16x8* Wimg = P.fimg;
   const bf16x8* Kimg = P.bimg;
 
@@ -198,6 +202,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   }
   f32x4 dk[LM][NR][NC];
   float lacc[LossF::NACC];
+  float bo_acc = 0.f;  // this point-thread's output-bias gradient (its points' value-stream dJ)
 #pragma unroll
   for (int k = 0; k < LossF::NACC; ++k) lacc[k] = 0.f;
 #pragma unroll
@@ -206,7 +211,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int c = 0; c < NC; ++c) dk[i][r][c] = zero4();
-  const float* Ko = aux + aux_ko(d, W);
+  const float* Ko = aux + A_KO;
 
   // layer 0 (input -> width, VALU; the accurate tanh) of this wave's feature tile at this lane's point
   auto layer0 = [&](f32x4(&h)[S]) { fz_h0<WT, S, NSO, false, DIN>(sp, aux, d, xs + p * TDQ_MAXD, o, g, h); };
@@ -246,7 +251,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     // ---- hidden layers 1..LM on MFMA ------------------------------------------------------
 #pragma unroll
     for (int ly = 1; ly <= LM; ++ly) {
-      const float* bi = aux + aux_bh(d, W) + (ly - 1) * W;
+      const float* bi = aux + A_BH + (ly - 1) * W;
       f32x4 z[S], h[S];
       fz3_load_w<WT>(wf, Wimg, ly, o, l);
       fz3_gemm<WT, S>(z, wf, slot(ly - 1), L);
@@ -278,7 +283,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       float a = outp[s * PT + pt];
 #pragma unroll
       for (int ww = 1; ww < FZ_WAVES; ++ww) a += outp[(ww * S + s) * PT + pt];
-      outp[s * PT + pt] = s == 0 ? a + aux[aux_bo(d, W)] : a;
+      outp[s * PT + pt] = s == 0 ? a + aux[A_BO] : a;
     }
     __syncthreads();
     // ---- the per-point loss (generated) and its reverse sweep -> dJ into ubs ---------------
@@ -287,6 +292,9 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     if (tl < PT) LossF::template eval<S, PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc);
     __syncthreads();
     FZ_TS(9);
+    tl = tid;
+    asm volatile("" : "+v"(tl));
+    if (tl < PT) bo_acc += ubs[tl * 4];  // dbo: this point's value-stream dJ
     // ---- reverse through the output layer: hb = Ko ub, dKo, the top tanh layer's adjoint ----
     {
       __bf16* im = slot(0);
@@ -317,13 +325,6 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       }
     }
     __syncthreads();
-    int ll = l;
-    asm volatile("" : "+v"(ll));
-    if (w == 0 && ll == 0) {  // dbo
-      float a = 0.f;
-      for (int pt = 0; pt < PT; ++pt) a += ubs[pt * 4];
-      accBo[0] += a;
-    }
     // ---- hidden layers LM..1: dK_l, hb_{l-1} = K_l zb_l, adjoint of tanh layer l-1 --------
 #pragma unroll
     for (int ly = LM; ly >= 1; --ly) {
@@ -414,9 +415,10 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     for (int j = 0; j < d.d_in; ++j) gs[j * W + f] = part[(LM + 1) * W + j * W + f];
     gs[off_layer(d, LM + 1) + f] = part[(LM + 1 + d.d_in) * W + f * 4];
   }
-  if (tid == 0) gs[off_layer(d, LM + 1) + W] = accBo[0];
-  // loss partials: the point-threads (wave 0, lanes < PT) summed
+  // the output bias and the loss partials: the point-threads (wave 0, lanes < PT) summed
   if (w == 0) {
+    const float bo = col4_sum(row16_sum(bo_acc));
+    if (l == 0) gs[off_layer(d, LM + 1) + W] = bo;
 #pragma unroll
     for (int k = 0; k < LossF::NACC; ++k) {
       const float v = col4_sum(row16_sum(lacc[k]));
