@@ -185,6 +185,7 @@ __device__ __forceinline__ void fz_gemm(f32x4 (&acc)[OPW][S], const bf16x8* __re
     for (int oo = 0; oo < OPW; ++oo)
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[oo][s] = mfma_bf(a[kb & 1][oo], b[s], acc[oo][s]);
+    // (a scheduling barrier per k-block: without it the step took 0.152 vs 0.146 ms, gpurun_out r6n)
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -331,7 +332,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     if (tid < FZ_PT * TDQ_MAXD) {
       const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
       const int n = min(pb + pt, N - 1);
-      xpre = j < d.d_in ? X[(size_t)n * d.d_in + j] : 0.f;
+      xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
     }
   };
   int t = t0;
