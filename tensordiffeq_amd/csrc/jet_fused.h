@@ -84,8 +84,21 @@ __device__ __forceinline__ void fz_h0(const JetSpec& sp, const float* aux, const
   const int f0 = 16 * t + 4 * g;
   f32x4 z = *reinterpret_cast<const f32x4*>(aux + (DIN > 0 ? DIN * W : aux_b0(d, W)) + f0);
   if constexpr (DIN > 0) {  // compile-time input width (the generated fused-step kernels)
+    // scalar FMAs, not f32x4 arithmetic: the vector form compiles to v_pk_fma_f32 whose result
+    // the next-but-one VALU reads; in the layer-0 adjoint (right after the dK_1 MFMA burst) that
+    // read returned stale lanes 48-63 of component 0 on some runs - b0 / K0 gradients of every
+    // 12th-of-16 feature differed run to run (profiles/r6s_bf16_nondeterminism.md).  Scalar form:
+    // bitwise reproducible, same step time.
+    float x[DIN];
 #pragma unroll
-    for (int j = 0; j < DIN; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
+    for (int j = 0; j < DIN; ++j) x[j] = xrow[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float a = z[c];
+#pragma unroll
+      for (int j = 0; j < DIN; ++j) a = fmaf(x[j], aux[j * W + f0 + c], a);
+      z[c] = a;
+    }
   } else {
     for (int j = 0; j < d.d_in; ++j) z += xrow[j] * *reinterpret_cast<const f32x4*>(aux + j * W + f0);
   }

@@ -674,11 +674,18 @@ class CollocationSolverND:
             params = self._best_flat["overall"]
         X = torch.as_tensor(np.asarray(X_star) if not torch.is_tensor(X_star) else X_star,
                             dtype=torch.float32).to(self.device)
-        with torch.no_grad():
-            u = torch.cat([self.u_model(X[i:i + chunk], params=params)
-                           for i in range(0, X.shape[0], chunk)], dim=0)
-        prog = self.program()
-        f = prog.residual_on(self.f_model, X, params=params, chunk=chunk)
+        # u is the value stream of the same jet launch that computes the residual's derivatives
+        # (HIP kernels on the hip backend), in bf16x3 when the solver trains in bf16 (the
+        # L-BFGS phase's program, usually built already): prediction error ~1e-5, not bf16's ~1e-3
+        prog = self.program(precision="bf16x3" if self.precision == "bf16" else None)
+        vals = []
+        f = prog.residual_on(self.f_model, X, params=params, chunk=chunk, values=vals)
+        if vals and all(v is not None for v in vals):
+            u = torch.cat(vals, dim=0)
+        else:
+            with torch.no_grad():
+                u = torch.cat([self.u_model(X[i:i + chunk], params=params)
+                               for i in range(0, X.shape[0], chunk)], dim=0)
         f_np = [x.cpu().numpy() for x in f]
         return u.cpu().numpy(), (f_np[0] if len(f_np) == 1 else tuple(f_np))
 

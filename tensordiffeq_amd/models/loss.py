@@ -456,8 +456,12 @@ class LossProgram:
         return jet_hi.eligible(self.net, self.plan_hi)
 
     # ---------------------------------------------------------------- prediction -----
-    def residual_on(self, fn, X, params=None, extra=(), chunk=65536):
-        """Evaluate residual(s) of ``fn`` on arbitrary points (no parameter gradients)."""
+    def residual_on(self, fn, X, params=None, extra=(), chunk=65536, values=None):
+        """Evaluate residual(s) of ``fn`` on arbitrary points (no parameter gradients).
+
+        ``values``: a list that receives the network output of every chunk - the jet's value
+        stream (``streams[0] == ()``) of the same kernel launch that computed the derivatives, or
+        None per chunk on the autograd backend."""
         outs = []
         for lo in range(0, X.shape[0], chunk):
             Xc = X[lo:lo + chunk]
@@ -465,10 +469,14 @@ class LossProgram:
                 cols = [Xc[:, j:j + 1].detach().clone().requires_grad_(True) for j in range(self.d_in)]
                 with torch.enable_grad():
                     o = fn(_ParamView(self.net, params), *extra, *cols)
+                if values is not None:
+                    values.append(None)
             else:
                 with torch.no_grad():
                     plan = self.plan_for(fn)
                     J = self.jet(params if params is not None else self.net.flat, X=Xc, plan=plan)
+                    if values is not None:
+                        values.append(J[0].reshape(Xc.shape[0], -1).detach())
                     cols = [Xc[:, j:j + 1] for j in range(self.d_in)]
                     ctx = autodiff.JetContext(cols, jet_dict(J, plan))
                     with autodiff.use(ctx):

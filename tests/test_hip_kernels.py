@@ -351,8 +351,18 @@ def test_mixed_plan_high_order_periodic():
     a.fit(tf_iter=10)
     b.fit(tf_iter=10)
     assert abs(a.losses[-1]["Total Loss"] - b.losses[-1]["Total Loss"]) / b.losses[-1]["Total Loss"] < 1e-3
-    u, f = a.predict(np.random.rand(100, 2))
+    Xp = np.random.rand(100, 2)
+    u, f = a.predict(Xp)
     assert np.isfinite(u).all() and np.isfinite(f).all()
+    # u: the HIP jet's value stream (bf16x3 for a bf16 solver) vs the network in float64
+    ws = [(k.detach().double(), b.detach().double()) for k, b in a.u_model.weights()]
+    h = torch.as_tensor(Xp, dtype=torch.float64, device=ws[0][0].device)
+    for i, (k, b) in enumerate(ws):
+        h = torch.addmm(b, h, k)
+        h = torch.tanh(h) if i < len(ws) - 1 else h
+    err = float(np.abs(u - h.cpu().numpy()).max() / max(1e-6, np.abs(h.cpu().numpy()).max()))
+    print(f"PREDICT_U_FP64 {err:.3e}")
+    assert err < 1e-4, err
 
 
 def test_step_book_and_adam_snapshot_match_torch():

@@ -150,6 +150,13 @@ def test_predict_and_best_model():
         ma.u_model.flat.copy_(m.u_model.flat)
     _, fa = ma.predict(X)
     np.testing.assert_allclose(f, fa, rtol=1e-4, atol=1e-5)
+    # u is the jet's value stream: equal to the network evaluated in float64
+    ws = [(k.detach().double(), b.detach().double()) for k, b in m.u_model.weights()]
+    h = torch.as_tensor(X, dtype=torch.float64)
+    for i, (k, b) in enumerate(ws):
+        h = torch.addmm(b, h, k)
+        h = torch.tanh(h) if i < len(ws) - 1 else h
+    np.testing.assert_allclose(u, h.numpy(), rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("fmt", ["npz", "pt", "dir"])
