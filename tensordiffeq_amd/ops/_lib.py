@@ -66,6 +66,10 @@ def _declare(lib):
         "tdq_lay_tn": (I, [I, P, P, L, P, P, L, P, I, I, I, I, P]),
         "tdq_lay_xtz": (I, [P, I, P, I, I, P, I, P]),
         "tdq_lay_xtz2": (I, [P, I, P, P, P, I, I, P, I, P]),
+        "tdq_colsum_work": (L, [I, L]),
+        "tdq_colsum": (I, [P, L, I, L, P, L, L, L, P, L, I, P, P]),
+        "tdq_lay_bplanes": (I, [P, I, I, I, P, P, P]),
+        "tdq_lay_l0grad": (I, [P, I, I, P, I, P, P, P]),
         "tdq_lay_nnj": (I, [I, I, I, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, I, P, P, I, P]),
         "tdq_lay_in_fwd": (I, [I, I, P, P, I, P, P, I, I, P, P, P]),
         "tdq_lay_out_bwd": (I, [I, I, I, P, P, I, P, P, P, I, I, P, P, P, P, I, P]),

@@ -124,6 +124,41 @@ def _planes(o):
     return o.h, getattr(o, "l", None)
 
 
+def _colsum(src, R, M, out, lds=None, W=None, sj=None, sf=1, bias=None, nbias=0):
+    """``out`` element m = sum over the R rows of ``src`` (row stride ``lds``, default M) of column
+    m, at ``out``'s storage offset (m // W) * sj + (m % W) * sf (defaults: contiguous) - the
+    fixed-order HIP column sum (csrc/lay_reduce.hip ``tdq_colsum``) in place of ``torch.sum``;
+    ``bias`` [bdim] is added to the first ``nbias`` elements."""
+    lib = _lib.load(required=True)
+    W = M if W is None else W
+    sj = W if sj is None else sj
+    nw = int(lib.tdq_colsum_work(int(R), int(M)))
+    work = torch.empty(max(nw, 1), dtype=torch.float32, device=src.device) if nw > 0 else None
+    _lib.check(lib.tdq_colsum(_lib.ptr(src), int(M if lds is None else lds), int(R), int(M), _lib.ptr(out), int(W),
+                              int(sj), int(sf), _lib.ptr(bias), int(nbias),
+                              int(bias.numel()) if bias is not None else 1, _lib.ptr(work),
+                              _lib.stream_ptr(src.device)), "tdq_colsum")
+    return out
+
+
+def _bplanes(bt, prec):
+    """The :class:`_Op` of an NN GEMM's B^T operand [Nout, K] from fp32 weights (a view of a
+    contiguous tensor or its transpose): bf16 hi (/ lo) planes in one launch
+    (csrc/lay_reduce.hip ``tdq_lay_bplanes``), not a transpose copy + casts."""
+    if bt.is_contiguous():
+        src, tr = bt, 0
+    elif bt.t().is_contiguous():
+        src, tr = bt.t(), 1
+    else:
+        return _Op(bt.contiguous(), prec)
+    h = torch.empty(bt.shape, dtype=torch.bfloat16, device=bt.device)
+    l = torch.empty_like(h) if prec == "bf16x3" else None
+    lib = _lib.load(required=True)
+    _lib.check(lib.tdq_lay_bplanes(_lib.ptr(src), src.shape[0], src.shape[1], tr, _lib.ptr(h), _lib.ptr(l),
+                                   _lib.stream_ptr(bt.device)), "tdq_lay_bplanes")
+    return _Op.parts(prec, h, l)
+
+
 def _mm_w(a, w, prec, out=None):
     """a @ w for an activation operand ``a`` [M, K] (:class:`_Op`) and fp32 weights ``w`` [K, N]
     (the weights' transposed operand ``[N, K]`` is formed here - W x W, small)."""
@@ -188,8 +223,7 @@ def _mm_tn(a, b, out):
         rc = lib.tdq_lay_tn(_PREC[a.prec], _lib.ptr(ah.contiguous()), _lib.ptr(al), Ma, _lib.ptr(bh.contiguous()),
                             _lib.ptr(bl), Nb, _lib.ptr(part), L, Ma, Nb, rows, _lib.stream_ptr(x.device))
         _lib.check(rc, "tdq_lay_tn")
-        torch.sum(part, dim=0, out=out)
-        return out
+        return _colsum(part, nch, Ma * Nb, out, W=Nb, sj=out.stride(0), sf=out.stride(1))
     L = x.shape[0]
     C = 64 if L >= 64 * 1024 else max(1, L // 1024)
     L0 = L - L % C
@@ -246,7 +280,7 @@ def _nnj(mode, prec, spec, S, N, a, bt, bias=None, H=None, part=None, X=None, ko
     layer may also take the output layer (``ko`` [Nout, d_out], ``jpart`` [ceil(Nout / 64), S, N,
     d_out]): J's partial dots per 64-column group come out of the same epilogue."""
     ah, al = _planes(a)
-    bo = _Op(bt.contiguous(), prec) if prec != "fp32" else None
+    bo = _bplanes(bt, prec) if prec != "fp32" else None
     bh, bl = _planes(bo) if bo is not None else (bt.contiguous(), None)
     Nout, K = bt.shape
     dev = ah.device
@@ -283,7 +317,8 @@ def _xtz(Xm, out, Z=None, H=None, rows=32):
         part = torch.empty((-(-R // rows), xj.shape[1], W), dtype=torch.float32, device=Xm.device)
         _lib.check(lib.tdq_lay_xtz2(_lib.ptr(xj), xj.shape[1], _lib.ptr(Z), _lib.ptr(zh), _lib.ptr(zl), R, W,
                                     _lib.ptr(part), rows, _lib.stream_ptr(Xm.device)), "tdq_lay_xtz2")
-        out[:, j0:j0 + xj.shape[1]].copy_(part.sum(dim=0).t())
+        # part [rows, nj, W] summed over rows: element (j, f) -> out[f][j0 + j]
+        _colsum(part, part.shape[0], xj.shape[1] * W, out[:, j0:], W=W, sj=out.stride(1), sf=out.stride(0))
     return out
 
 
@@ -356,11 +391,12 @@ def forward_raw(X, P, net, plan, precision="fp32"):
             h, o = saved(*_nnj(EPI_FWD, precision, spec, S, N, Ho[-1], K.t(), bias=b, **kw))
             Hs.append(h)
             Ho.append(o)
-        if jpart is not None:
-            J = jpart.sum(dim=0)
+        if jpart is not None:   # J = the 64-column partials summed, + bo on the value stream
+            J = torch.empty((S, N, d_out), dtype=torch.float32, device=X.device)
+            _colsum(jpart, jpart.shape[0], S * N * d_out, J, bias=bo, nbias=N * d_out)
         else:
             J = _mm_w(Ho[-1], Ko, precision).view(S, N, d_out)
-        J[0] += bo
+            J[0] += bo
         return J, ("layered", X, P, net, spec, Hs, Ho, precision, fused)
     Z = torch.zeros((S, N, W0), dtype=P.dtype, device=X.device)
     if X.is_cuda:   # layer 0: the input is exact fp32, d_in <= 8 columns - FMAs, not a GEMM
@@ -396,7 +432,7 @@ def backward_raw(saved, dJ, grad=None):
     S, N = dJ.shape[0], dJ.shape[1]
     dJ = dJ.contiguous()
     Ko, _ = ws[-1]
-    dJo = _Op(dJ.view(S * N, dJ.shape[2]), prec)
+    dJo = None
     last = len(ws) - 2
     if fused and dJ.shape[2] <= 64:   # dKo = H^T dJ, a few columns: FMA partials on exact dJ, H = hi + lo
         if prec == "fp32":
@@ -404,13 +440,18 @@ def backward_raw(saved, dJ, grad=None):
         else:
             _xtz(dJ.view(S * N, dJ.shape[2]), gw[-1][0], H=Hs[last], rows=64)
     else:
+        dJo = _Op(dJ.view(S * N, dJ.shape[2]), prec)
         _mm_tn(Ho[-1], dJo, gw[-1][0])
-    torch.sum(dJ[0], dim=0, out=gw[-1][1])
+    if dJ.is_cuda and _hip_gemm():
+        _colsum(dJ, N, dJ.shape[2], gw[-1][1])   # dJ[0] [N, d_out] summed over the points
+    else:
+        torch.sum(dJ[0], dim=0, out=gw[-1][1])
     HB = None
     if not fused or dJ.shape[2] > 4:   # (the fused path forms HB = dJ Ko^T inside lay_out_bwd_kernel)
         if dJ.shape[2] == 1:  # an outer product: a K = 1 GEMM ran 10x slower than this broadcast
             HB = (dJ.view(S * N, 1) * Ko.view(1, -1)).view(S, N, Ko.shape[0])
         else:
+            dJo = dJo if dJo is not None else _Op(dJ.view(S * N, dJ.shape[2]), prec)
             HB = _mm_bt(dJo, Ko, prec).view(S, N, Ko.shape[0])
     part0 = ZB0 = None
     if fused:
@@ -448,7 +489,8 @@ def backward_raw(saved, dJ, grad=None):
         for i in range(last, 0, -1):
             K, _ = ws[i]
             _mm_tn(Ho[i - 1], ZBo, gw[i][0])
-            torch.sum(db.reshape(-1, db.shape[-1]), dim=0, out=gw[i][1])
+            dbr = db.reshape(-1, db.shape[-1])
+            _colsum(dbr, dbr.shape[0], dbr.shape[1], gw[i][1], lds=dbr.stride(0))
             # HB_{i-1} = ZB_i K_i^T with layer i-1's adjoint jet in the GEMM epilogue (K is the B^T
             # operand); the input layer's comes out as gradient partials only
             W = K.shape[0]
@@ -461,12 +503,12 @@ def backward_raw(saved, dJ, grad=None):
                 _nnj(EPI_BWD0, prec, spec, S, N, ZBo, K, H=Hs[0], part=part0, X=X)
     dK0, gb0 = gw[0]
     if part0 is not None:
-        tot = part0.sum(dim=0)                       # [S + d_in, W0]: stream sums, then X^T zb
-        dK0.copy_(tot[S:])
-        for s in range(1, S):
-            if spec[3 * s] == 1:
-                dK0[spec[3 * s + 1]] += tot[s]
-        gb0.copy_(tot[0])
+        # [S + d_in, W0]: stream sums, then X^T zb -> dK0 (+ first-order streams), b0
+        tot = torch.empty(part0.shape[1:], dtype=torch.float32, device=part0.device)
+        _colsum(part0, part0.shape[0], tot.numel(), tot)
+        lib = _lib.load(required=True)
+        _lib.check(lib.tdq_lay_l0grad(_lib.ptr(tot), S, X.shape[1], _spec_c(spec), tot.shape[1], _lib.ptr(dK0),
+                                      _lib.ptr(gb0), _lib.stream_ptr(tot.device)), "tdq_lay_l0grad")
         return grad
     if ZB0 is None:
         for i in range(last, 0, -1):
