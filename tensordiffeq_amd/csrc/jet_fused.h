@@ -66,9 +66,10 @@ __host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int
   return fz_img_elems(WT, S, LM) * 2 + fz_fl_floats(d, WT, S, LM) * 4;
 }
 
-// Layer 0 (input -> width, VALU) of feature tile t at one point x (LDS row) - computed three times
-// per tile (forward, the h_0 image rebuild for dK_1, the layer-0 adjoint), always by this function,
-// so every pass sees the same h_0.  Its derivative streams are rows of K0: h_a = s1 K0[a],
+// Layer 0 (input -> width, VALU) of feature tile t at one point x (LDS row) - computed twice per
+// tile in the bf16 step (forward, the h_0 image rebuild for dK_1 that the layer-0 adjoint then reads;
+// three times in the bf16x3 objective, whose adjoint recomputes it), always by this function, so
+// every pass sees the same h_0.  Its derivative streams are rows of K0: h_a = s1 K0[a],
 // h_ab = s2 K0[a] K0[b] (z_ab = 0).
 // CHEAP (the bf16 step): tanh z = 1 - 2 r, s1 = 4 e r^2 with e = exp(2 min(z, 15)), r = 1 / (1 + e)
 // (exp, rcp and ~6 FMA-class ops; s1 from e, not 1 - h^2, which cancels for saturated units).  On
@@ -513,12 +514,15 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
           for (int s = 0; s < S; ++s) fz_put<RS>(H + s * SIMG, L, q, to, zbh[oo][s]);
         }
       } else {
-        // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
+        // layer 0: zb_0 from h_0 (the slot-0 image the ly = 2 step rebuilt) -> first-layer
+        // partials (K0, b0)
 #pragma unroll
         for (int oo = 0; oo < OPW; ++oo) {
           const int to = o0 + oo;
           f32x4 h[S], zb[S];
-          layer0(oo, h);
+          h[0] = fz_bf4(fz_get<RS>(H, L, q, to)) + fz_bf4(fz_get<RS>(H + S * SIMG, L, q, to));
+#pragma unroll
+          for (int s = 1; s < S; ++s) h[s] = fz_bf4(fz_get<RS>(H + s * SIMG, L, q, to));
           tanh_jet_b<S, NSO>(sp, h, acc[oo], zb);
           const int fo = 16 * to + 4 * g + (p >> 2);
           {
@@ -549,8 +553,16 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
         for (int oo = 0; oo < OPW; ++oo) {
           f32x4 h[S];
           layer0(oo, h);
+          // with the value stream's lo plane, as the hidden layers' images: the layer-0 adjoint
+          // (ly = 1) reads h_0 back from here instead of recomputing layer 0 a third time (step
+          // 0.1425 vs 0.1452 ms, L2 median 2.23e-2 vs 2.16e-2 - seed noise; fp64 gradient 2.8e-3
+          // either way: profiles/r6w_l0_image_ab.txt)
+          bf16x4 hi, lo;
+          split4(h[0], hi, lo);
+          fz_put<RS>(slot(0), L, q, o0 + oo, hi);
+          fz_put<RS>(slot(0) + S * SIMG, L, q, o0 + oo, lo);
 #pragma unroll
-          for (int s = 0; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
+          for (int s = 1; s < S; ++s) fz_put<RS>(slot(0) + s * SIMG, L, q, o0 + oo, cvt_hi4(h[s]));
         }
       }
       if (ly >= 2) __syncthreads();
