@@ -192,7 +192,19 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   const bf16x8* Wimg = P.fimg;
   const bf16x8* Kimg = P.bimg;
 
+  // this XCD's L2 warmed with the weight images (hi and lo) before the first tile (as fz_body)
+  bf16x8 wpf[2];
+  {
+    constexpr int NI16 = LM * WT * (WT / 2) * 128 * 4 * 4 / 16;  // 16-byte granules per image
+    const int xw = gi >> 3, nx = (G + 7) >> 3;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = (xw + k * nx) * 64 * FZ_WAVES + tid;
+      wpf[k] = e < 2 * NI16 ? (e < NI16 ? P.fimg[e] : P.bimg[e - NI16]) : bf16x8{};
+    }
+  }
   for (int e = tid; e < naux; e += 64 * FZ_WAVES) aux[e] = e < aux_floats(d, W) ? aux_g[e] : 0.f;
+  asm volatile("" ::"v"(wpf[0]), "v"(wpf[1]));
   for (int e = tid; e < pq + 4; e += 64 * FZ_WAVES) part[e] = 0.f;
   if constexpr (SP != S) {  // the padding stream's images (hi, lo) of every slot stay zero
     for (int k = 0; k < fz_nslot(LM); ++k)
