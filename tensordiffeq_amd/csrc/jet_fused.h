@@ -319,6 +319,19 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   const bf16x8* Wimg = P.fimg;
   const bf16x8* Kimg = P.bimg;
 
+  // this thread's element of a tile's x (one: FZ_PT * TDQ_MAXD <= 512), fetched one tile ahead so
+  // the global latency hides behind the current tile
+  static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES, "one element per thread");
+  float xpre = 0.f;
+  auto fetch = [&](int tt) {
+    const int pb = P.p_lo + tt * FZ_PT;
+    if (tid < FZ_PT * TDQ_MAXD) {
+      const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
+      const int n = min(pb + pt, N - 1);
+      xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
+    }
+  };
+  if (t0 < t1) fetch(t0);  // first, so its latency overlaps the set-up below
   // warm this XCD's L2 with the weight images before the first tile's GEMMs: the workgroups of an
   // XCD (blocks gi, gi + 8, ... when the dispatcher deals them round-robin) each touch a slice (the
   // first tile's GEMMs ran 500-800 cycles slower each without: step 0.1429 -> 0.1400 ms,
@@ -352,20 +365,8 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   // layer 0 (input -> width, VALU) of feature tile o0 + oo at this lane's point
   auto layer0 = [&](int oo, f32x4(&h)[S]) { fz_h0<WT, S, NSO, true, DIN>(sp, aux, d, xs + row * TDQ_MAXD, o0 + oo, g, h); };
 
-  // this thread's element of a tile's x (one: FZ_PT * TDQ_MAXD <= 512), fetched one tile ahead so
-  // the global latency hides behind the current tile
-  static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES, "one element per thread");
-  float xpre = 0.f;
-  auto fetch = [&](int tt) {
-    const int pb = P.p_lo + tt * FZ_PT;
-    if (tid < FZ_PT * TDQ_MAXD) {
-      const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
-      const int n = min(pb + pt, N - 1);
-      xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
-    }
-  };
+
   int t = t0;
-  if (t < t1) fetch(t);
   TDQ_TS(0);
   while (t < t1) {
     const int pb = P.p_lo + t * FZ_PT;

@@ -192,6 +192,16 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   const bf16x8* Wimg = P.fimg;
   const bf16x8* Kimg = P.bimg;
 
+  float xpre = 0.f;
+  auto fetch = [&](int tt) {
+    const int pb = P.p_lo + tt * PT;
+    if (tid < PT * TDQ_MAXD) {
+      const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
+      const int n = min(pb + pt, N - 1);
+      xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
+    }
+  };
+  if (t0 < t1) fetch(t0);  // first, so its latency overlaps the set-up below
   // this XCD's L2 warmed with the weight images (hi and lo) before the first tile (as fz_body)
   bf16x8 wpf[2];
   {
@@ -230,17 +240,8 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   auto layer0 = [&](f32x4(&h)[S]) { fz_h0<WT, S, NSO, false, DIN>(sp, aux, d, xs + p * TDQ_MAXD, o, g, h); };
 
   static_assert(PT * TDQ_MAXD <= 64 * FZ_WAVES, "one element per thread");
-  float xpre = 0.f;
-  auto fetch = [&](int tt) {
-    const int pb = P.p_lo + tt * PT;
-    if (tid < PT * TDQ_MAXD) {
-      const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
-      const int n = min(pb + pt, N - 1);
-      xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
-    }
-  };
+
   int t = t0;
-  if (t < t1) fetch(t);
   Fz3W<WT> wf;  // a GEMM's weight fragments
   TDQ_TS(0);
   while (t < t1) {
