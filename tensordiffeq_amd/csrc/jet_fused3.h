@@ -371,9 +371,10 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
           fz_put<RS>(H + (SP + s) * SIMG, L, 0, o, zbl[s]);
         }
       } else {
-        // layer 0: zb_0 from h_0 recomputed in fp32 -> first-layer partials (K0, b0)
+        // layer 0: zb_0 from h_0 as the ly = 2 step rebuilt it into slot 0 (value stream fp32,
+        // the others hi + lo) -> first-layer partials (K0, b0); not a third layer-0 evaluation
         f32x4 h[S], zb[S];
-        layer0(h);
+        fz3_get_h<WT, S>(H, L, o, h, fz3_vimg(H, WT, S) + voff);
         tanh_jet_b<S, NSO>(sp, h, acc, zb);
         const int fo = 16 * o + 4 * g + (p >> 2);
         {
