@@ -60,7 +60,7 @@ __host__ __device__ inline int fz_fl_floats(const NetDims& d, int WT, int S, int
   const int common = fz_aux_floats(d, W) + FZ_PT * TDQ_MAXD + S * FZ_PT * 4;
   const int part = 2 * ((LM + 1) * W + d.d_in * W + 4 * W) + 4;
   const int outp = 4 * S * FZ_PT;
-  return common + part + outp;
+  return common + part + outp + FZ_PT;  // + the loss's prefetched per-point input
 }
 __host__ __device__ inline int fz_lds_bytes(const NetDims& d, int WT, int S, int LM) {
   return fz_img_elems(WT, S, LM) * 2 + fz_fl_floats(d, WT, S, LM) * 4;
@@ -264,10 +264,13 @@ struct FzParams {
 
 // The generated loss (ops/fused_step.py gen_loss) has this interface:
 //   NACC: loss / scalar-gradient sums per point-thread;
-//   eval<S>(jv, xs, t, n, N, ptrs, ubs, acc) on the tile's point-thread t (point n of the fused
+//   eval<S>(jv, xs, t, n, N, ptrs, ubs, acc, pv) on the tile's point-thread t (point n of the fused
 //   point set): J of the tile's point k, stream s at jv[s * PT + k], coordinates at
 //   xs[k * TDQ_MAXD + j]; writes dJ of the points it owns to ubs[(s * PT + k) * 4] (zero for points
-//   outside every loss group) and adds loss / scalar-gradient sums to acc.
+//   outside every loss group) and adds loss / scalar-gradient sums to acc;
+//   pre(n, N, ptrs): the first per-point global input of point n's group (an SA weight or a data
+//   value), which the kernel loads one tile ahead (with the coordinates) and passes in as pv - the
+//   loss phase then waits for no global load on the common groups.
 // Eight waves (two per SIMD, so one wave's tanh-jet VALU work runs beside the other's MFMAs):
 // wave w computes column tile q = w >> 2 (16 points) of feature tiles 2 (w & 3).. (OPW of them) in
 // every GEMM / epilogue, and owns an NR x NC block of each hidden layer's dK tiles.
@@ -301,6 +304,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
   float* part = ubs + S * FZ_PT * 4;          // [2 column tiles][...] partials
   constexpr int pq = (LM + 1) * W + DIN * W + 4 * W;  // partial floats per column tile
   float* outp = part + 2 * pq + 4;            // [4][S][FZ_PT] output-layer dots
+  float* lpre = outp + 4 * S * FZ_PT;         // [FZ_PT] the loss's prefetched first input
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -321,7 +325,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
 
   // this thread's element of a tile's x (one: FZ_PT * TDQ_MAXD <= 512), fetched one tile ahead so
   // the global latency hides behind the current tile
-  static_assert(FZ_PT * TDQ_MAXD <= 64 * FZ_WAVES, "one element per thread");
+  static_assert(FZ_PT * TDQ_MAXD + FZ_PT <= 64 * FZ_WAVES, "one element per thread");
   float xpre = 0.f;
   auto fetch = [&](int tt) {
     const int pb = P.p_lo + tt * FZ_PT;
@@ -329,6 +333,8 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
       const int n = min(pb + pt, N - 1);
       xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
+    } else if (tid < FZ_PT * TDQ_MAXD + FZ_PT) {  // the loss's first per-point input (GenLoss::pre)
+      xpre = LossF::pre(pb + tid - FZ_PT * TDQ_MAXD, N, *P.lptrs);
     }
   };
   if (t0 < t1) fetch(t0);  // first, so its latency overlaps the set-up below
@@ -373,6 +379,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
     __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
     if (tid < FZ_PT * TDQ_MAXD) xs[tid] = xpre;
+    else if (tid < FZ_PT * TDQ_MAXD + FZ_PT) lpre[tid - FZ_PT * TDQ_MAXD] = xpre;
     if (t + 1 < t1) fetch(t + 1);
     __syncthreads();
     FZ_TS(1);
@@ -453,7 +460,7 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
     // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
     tl = tid;
     asm volatile("" : "+v"(tl));
-    if (tl < FZ_PT) LossF::template eval<S, FZ_PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc);
+    if (tl < FZ_PT) LossF::template eval<S, FZ_PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc, lpre[tl]);
     __syncthreads();
     FZ_TS(9);
     // dbo: each point-thread adds its point's value-stream dJ (one LDS read; a 32-step loop on

@@ -38,7 +38,7 @@ __host__ __device__ constexpr int fz3_slot_bytes(int WT, int S) {
 __host__ __device__ inline int fz3_fl_floats(const NetDims& d, int WT, int S, int LM) {
   const int W = 16 * WT;
   return fz_aux_floats(d, W) + FZ3_PT * TDQ_MAXD + S * FZ3_PT * 4 + ((LM + 1) * W + d.d_in * W + 4 * W) + 4 +
-         FZ_WAVES * S * FZ3_PT;
+         FZ_WAVES * S * FZ3_PT + FZ3_PT;  // + the loss's prefetched per-point input
 }
 __host__ __device__ inline int fz3_lds_bytes(const NetDims& d, int WT, int S, int LM) {
   return fz_nslot(LM) * fz3_slot_bytes(WT, S) + fz3_fl_floats(d, WT, S, LM) * 4;
@@ -177,6 +177,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
   float* part = ubs + S * PT * 4;             // partials
   constexpr int pq = (LM + 1) * W + DIN * W + 4 * W;
   float* outp = part + pq + 4;                // [8 waves][S][PT] output-layer dots
+  float* lpre = outp + FZ_WAVES * S * PT;     // [PT] the loss's prefetched first input
 
   const int tid = threadIdx.x, l = tid & 63, p = l & 15, g = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -199,6 +200,8 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       const int pt = tid / TDQ_MAXD, j = tid - pt * TDQ_MAXD;
       const int n = min(pb + pt, N - 1);
       xpre = j < DIN ? X[(size_t)n * DIN + j] : 0.f;
+    } else if (tid < PT * TDQ_MAXD + PT) {  // the loss's first per-point input (GenLoss::pre)
+      xpre = LossF::pre(pb + tid - PT * TDQ_MAXD, N, *P.lptrs);
     }
   };
   if (t0 < t1) fetch(t0);  // first, so its latency overlaps the set-up below
@@ -249,6 +252,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     asm volatile("" : "+s"(Wimg), "+s"(Kimg));
     __syncthreads();  // the previous tile's readers of xs / ubs / images are done (and aux / part set)
     if (tid < PT * TDQ_MAXD) xs[tid] = xpre;
+    else if (tid < PT * TDQ_MAXD + PT) lpre[tid - PT * TDQ_MAXD] = xpre;
     if (t + 1 < t1) fetch(t + 1);
     __syncthreads();
     FZ_TS(1);
@@ -303,7 +307,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     // ---- the per-point loss (generated) and its reverse sweep -> dJ into ubs ---------------
     tl = tid;
     asm volatile("" : "+v"(tl));
-    if (tl < PT) LossF::template eval<S, PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc);
+    if (tl < PT) LossF::template eval<S, PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc, lpre[tl]);
     __syncthreads();
     FZ_TS(9);
     tl = tid;

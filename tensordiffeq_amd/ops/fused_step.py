@@ -126,13 +126,44 @@ def gen_loss(groups, n_terms, nacc, S, spec=None, d_in=None):
             e("      return;")
             e("    }")
 
+    # the first per-point global input (SA weight / data value) of each group: the kernel loads it
+    # for the NEXT tile during this one (pre, into an LDS word per point) - the loss phase then
+    # waits for no global load on the common groups (bf16 step 0.1397 -> 0.1382 ms, objective
+    # 278.2 -> 277.0 us: profiles/r6ae_loss_input_prefetch_ab.txt)
+    first = {}
+    for gi, (P, start, ns, n) in enumerate(groups):
+        seen = []
+
+        def probe(name, r, a, b, seen=seen):
+            if name in ("VAL", "LAM") and not seen:
+                seen.append((name, a))
+            return ""
+        loss_jit._forward_code(P, lambda _ln: None, probe)
+        first[gi] = seen[0] if seen else None
+    e("  __device__ static float pre(int n, int N, const FzLossPtrs& ptr) {")
+    kw = "if"
+    for gi, (P, start, ns, n) in enumerate(groups):
+        if first[gi] is None:
+            continue
+        nm, a = first[gi]
+        arr = {"VAL": "val", "LAM": "lam"}[nm]
+        end = start + ns * n
+        idx = f"(n - {start}) >> 1" if ns == 2 else f"n - {start}"
+        e(f"    {kw} (n >= {start} && n < {end} && n < N) return ptr.{arr}[{a}][{idx}];")
+        kw = "else if"
+    e("    return 0.f;")
+    e("  }")
     e("  template <int S, int PT>")
     e("  __device__ static void eval(const float* jv, const float* xs, int t, int n, int N, "
-      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC]) {")
+      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC], float pv) {")
     e("    #define JV(s_, k_) jv[(s_) * PT + (k_)]")
     e("    #define UB(s_, k_) ubs[((s_) * PT + (k_)) * 4]")
 
+    cur = {}
+
     def eval_body(P, ns):
+        fp = first[[g[0] for g in groups].index(P)]
+        cur["first"], cur["used"] = fp, False
         nr = max(1, P.n_regs)
         e("      float " + ", ".join(f"v{r}" for r in range(nr)) + ";")
         e("      float " + ", ".join(f"a{r} = 0.f" for r in range(nr)) + ";")
@@ -145,6 +176,9 @@ def gen_loss(groups, n_terms, nacc, S, spec=None, d_in=None):
                 return f"      v{r} = JV({b}, t + {a});"
             if name == "COORD":
                 return f"      v{r} = xs[(t + {a}) * TDQ_MAXD + {b}];"
+            if (name, a) == cur["first"] and not cur["used"]:
+                cur["used"] = True
+                return f"      v{r} = pv;   // prefetched (pre)"
             return {"VAL": f"      v{r} = ptr.val[{a}][i];", "LAM": f"      v{r} = ptr.lam[{a}][i];",
                     "SCAL": f"      v{r} = *ptr.scal[{a}];"}[name]
 
