@@ -262,10 +262,20 @@ struct FzParams {
   int prow, nacc;
 };
 
+// J of stream s at tile point k from the NW waves' partial output dots jv[(w * S + s) * PT + k]
+// (summed in wave order, + the output bias on the value stream) - read by the generated loss
+template <int S, int PT, int NW>
+__device__ __forceinline__ float fz_jsum(const float* jv, int s, int k, float bo) {
+  float a = jv[s * PT + k];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) a += jv[(w * S + s) * PT + k];
+  return s == 0 ? a + bo : a;
+}
+
 // The generated loss (ops/fused_step.py gen_loss) has this interface:
 //   NACC: loss / scalar-gradient sums per point-thread;
-//   eval<S>(jv, xs, t, n, N, ptrs, ubs, acc, pv) on the tile's point-thread t (point n of the fused
-//   point set): J of the tile's point k, stream s at jv[s * PT + k], coordinates at
+//   eval<S, PT, NW>(jv, xs, t, n, N, ptrs, ubs, acc, pv, bo) on the tile's point-thread t (point n
+//   of the fused point set): J of the tile's point k, stream s = fz_jsum(jv, s, k, bo), coordinates at
 //   xs[k * TDQ_MAXD + j]; writes dJ of the points it owns to ubs[(s * PT + k) * 4] (zero for points
 //   outside every loss group) and adds loss / scalar-gradient sums to acc;
 //   pre(n, N, ptrs): the first per-point global input of point n's group (an SA weight or a data
@@ -440,27 +450,14 @@ __device__ __forceinline__ void fz_body(const FzParams& P, char* lds_raw) {
       FZ_TS(2 + 2 * ly);
     }
 
-    // ---- J of the tile's points: the wave-ordered sums of the partial dots, in place of wave
-    // 0's (each (stream, point) entry read and written by one thread) --------------------------
-    // (the thread index goes through an opaque copy here and at the loss call: the addresses
-    // derived from it would otherwise be hoisted out of the tile loop and, at 256 VGPRs,
-    // spilled - a scratch reload + full vmcnt wait per address on the loss's critical path)
-    int tl = tid;
-    asm volatile("" : "+v"(tl));
-    if (tl < S * FZ_PT) {
-      const int s = tl / FZ_PT, pt = tl - s * FZ_PT;
-      float a = outp[(0 * S + s) * FZ_PT + pt];
-#pragma unroll
-      for (int ww = 1; ww < 4; ++ww) a += outp[(ww * S + s) * FZ_PT + pt];
-      outp[(0 * S + s) * FZ_PT + pt] = s == 0 ? a + aux[A_BO] : a;
-    }
-    __syncthreads();
     // ---- the per-point loss (generated code: every loss group of the program - residual, SA
     // weighting, boundary terms with the two points of a periodic pair side by side - and its
     // reverse sweep) -> dJ of the tile's points into ubs -----------------------------------
-    tl = tid;
+    // (J = the four wo-waves' partial dots, summed inside the loss: one phase and one barrier
+    // fewer, 0.1383 -> 0.1376 ms, profiles/r6ag_jsum_ab.txt)
+    int tl = tid;
     asm volatile("" : "+v"(tl));
-    if (tl < FZ_PT) LossF::template eval<S, FZ_PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc, lpre[tl]);
+    if (tl < FZ_PT) LossF::template eval<S, FZ_PT, 4>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc, lpre[tl], aux[A_BO]);
     __syncthreads();
     FZ_TS(9);
     // dbo: each point-thread adds its point's value-stream dJ (one LDS read; a 32-step loop on

@@ -293,7 +293,9 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
       FZ_TS(2 + 2 * ly);
     }
 
-    // ---- J of the tile's points: the wave-ordered sums of the partial dots -------------------
+    // ---- J of the tile's points: the wave-ordered sums of the partial dots (here, over 64
+    // threads: eight partials per J read inside the 16-thread loss measured 1 % slower,
+    // profiles/r6ag_jsum_ab.txt) -------------------------------------------------------------
     int tl = tid;
     asm volatile("" : "+v"(tl));
     if (tl < S * PT) {
@@ -307,7 +309,7 @@ __device__ __forceinline__ void fz3_body(const FzParams& P, char* lds_raw) {
     // ---- the per-point loss (generated) and its reverse sweep -> dJ into ubs ---------------
     tl = tid;
     asm volatile("" : "+v"(tl));
-    if (tl < PT) LossF::template eval<S, PT>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc, lpre[tl]);
+    if (tl < PT) LossF::template eval<S, PT, 1>(outp, xs, tl, pb + tl, N, *P.lptrs, ubs, lacc, lpre[tl], 0.f);
     __syncthreads();
     FZ_TS(9);
     tl = tid;

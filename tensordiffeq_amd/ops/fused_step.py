@@ -153,10 +153,12 @@ def gen_loss(groups, n_terms, nacc, S, spec=None, d_in=None):
         kw = "else if"
     e("    return 0.f;")
     e("  }")
-    e("  template <int S, int PT>")
+    e("  template <int S, int PT, int NW>")
     e("  __device__ static void eval(const float* jv, const float* xs, int t, int n, int N, "
-      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC], float pv) {")
-    e("    #define JV(s_, k_) jv[(s_) * PT + (k_)]")
+      "const FzLossPtrs& ptr, float* ubs, float (&acc)[NACC], float pv, float bo) {")
+    # J of (stream, point): the NW waves' partial output dots summed here (wave order, + bo on the
+    # value stream) instead of in a separate phase behind one more barrier
+    e("    #define JV(s_, k_) fz_jsum<S, PT, NW>(jv, (s_), (k_), bo)")
     e("    #define UB(s_, k_) ubs[((s_) * PT + (k_)) * 4]")
 
     cur = {}
