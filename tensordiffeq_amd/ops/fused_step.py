@@ -561,11 +561,12 @@ class FusedStepOp:
         if side is None:
             fused()
             return
-        if self.fop2 is not None and os.environ.get("TDQ_FS_SPLIT_ORDER", "side_first") == "side_first":
-            # split layout: the jet_hi forward goes first - launched beside a running fused kernel it
-            # only gets the CUs the persistent workgroups leave free (143 us instead of 18,
-            # profiles/r5split_*); ahead of it, its ~100 workgroups finish while the fused
-            # kernel's fill the rest of the GPU
+        if self.fop2 is not None and os.environ.get("TDQ_FS_SPLIT_ORDER", "fused_first") == "side_first":
+            # split layout, side chain first (round-5 default: the jet_hi forward then gets the GPU
+            # before the persistent workgroups fill it).  Round 6 (faster fused kernel, one extra
+            # tile round leaving 56 CUs): fused first 0.1638 vs side first 0.1736 ms/step,
+            # profiles/r6aj_ac_baseline_split_order.txt - the fused launch no longer starts ~11 us
+            # into the step behind the fork
             ev = torch.cuda.Event()
             ev.record(cur)
             side.wait_event(ev)

@@ -2,7 +2,7 @@
 the flagship AC-SA bf16 Adam step on the fused step (ops/fused_step.py: round 6 final 0.140-0.142 ms,
 profiles/r6m_bench_driver.json, r6n_sched_barrier_ab.txt) and the AC-baseline step with its
 order-4 periodic BC on the fused step's split layout (main-plan outputs fused, the u_xxx / u_xxxx
-outputs on the jet_hi.hip side chain: 0.180 ms, ratio 1.22, profiles/r6o_perf_guards.txt)."""
+outputs on the jet_hi.hip side chain: 0.163-0.168 ms, ratio 1.18, profiles/r6ak_ac_baseline_order_check.txt)."""
 import os
 import sys
 
@@ -44,15 +44,16 @@ def test_ac_baseline_step_time_on_fused_path():
     from tensordiffeq_amd.ops import fused_step
     fs = fused_step.for_program(prog)
     assert fs is not None and fs.layout == "split", prog.fused_step_reason
-    assert ms < 0.205, ms   # measured 0.180 ms (profiles/r6o_perf_guards.txt)
+    assert ms < 0.185, ms   # measured 0.163-0.168 ms, fused-first split order (profiles/r6aj_*, r6ak_*)
 
 
 @pytest.mark.timeout(300)
 def test_ac_baseline_step_within_ac_sa_ratio():
     """The order-4 periodic program keeps a fused path: same box, same process, its step within
-    1.30x the AC-SA step (round 6: 1.22x, 0.180 / 0.147 ms; round 5 1.23-1.28x: 0.207 / 0.168 ms - the jet_hi side chain's kernels only
+    1.25x the AC-SA step (round 6 final: 1.18x, 0.1634 / 0.1387 ms, fused-first split order;
+    mid-round 1.22x, 0.180 / 0.147 ms; round 5 1.23-1.28x: 0.207 / 0.168 ms - the jet_hi side chain's kernels only
     get the CUs the persistent fused workgroups leave, profiles/r5split2_timeline_*)."""
     sa, _ = _step_ms("ac-sa")
     acb, _ = _step_ms("ac-baseline")
     print(f"PERF ratio ac-baseline / ac-sa {acb / sa:.3f} ({acb:.4f} / {sa:.4f} ms)")
-    assert acb / sa < 1.30, (acb, sa)
+    assert acb / sa < 1.25, (acb, sa)
