@@ -505,6 +505,7 @@ class FusedStepOp:
         # the fewest workgroups with the same tiles per workgroup (AC-SA 50k, bf16: 1592 tiles,
         # 228 x 7; bf16x3: 3183 tiles, 245 x 13)
         self.G = -(-ntiles // rounds)
+        self.free_cus = cus - self.G   # CUs the persistent workgroups leave to a side chain
         if self.layout == "residual":   # the fused rows follow the boundary loss blocks' rows in fop.partials
             self.G = min(self.G, fop.n_blocks - self.b_res)
         self.rows = self.srow + self.G
@@ -561,12 +562,13 @@ class FusedStepOp:
         if side is None:
             fused()
             return
-        if self.fop2 is not None and os.environ.get("TDQ_FS_SPLIT_ORDER", "fused_first") == "side_first":
-            # split layout, side chain first (round-5 default: the jet_hi forward then gets the GPU
-            # before the persistent workgroups fill it).  Round 6 (faster fused kernel, one extra
-            # tile round leaving 56 CUs): fused first 0.1638 vs side first 0.1736 ms/step,
-            # profiles/r6aj_ac_baseline_split_order.txt - the fused launch no longer starts ~11 us
-            # into the step behind the fork
+        # split layout: which branch is captured first.  With >= 32 CUs left to the side chain
+        # (AC-baseline 50k: 56) the fused launch goes first and no longer starts ~11 us into the step
+        # behind the fork: 0.1638 vs 0.1736 ms/step (profiles/r6aj_ac_baseline_split_order.txt).
+        # With few free CUs (AC-dist 500k: 7) the jet_hi forward launched second waited for the whole
+        # fused launch (964 us) and the chain ran after it (profiles/r6am_*): side chain first
+        order = os.environ.get("TDQ_FS_SPLIT_ORDER", "fused_first" if self.free_cus >= 32 else "side_first")
+        if self.fop2 is not None and order == "side_first":
             ev = torch.cuda.Event()
             ev.record(cur)
             side.wait_event(ev)
