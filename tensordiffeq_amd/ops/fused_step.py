@@ -499,9 +499,11 @@ class FusedStepOp:
         cus = max(1, lib.tdq_device_cus())
         rounds = -(-ntiles // cus)
         if self.fop2 is not None:
-            # split layout: one round more leaves ~57 CUs to the jet_hi side chain - AC-baseline
-            # 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*
-            rounds += int(os.environ.get("TDQ_FS_SPLIT_ROUNDS", "1"))
+            # split layout: one round more leaves ~57 CUs to the jet_hi side chain - AC-baseline 50k
+            # (7 rounds) 0.2070 vs 0.2105 ms/step (+2 rounds: 0.2277), profiles/r5split3_*; with many
+            # rounds the extra one costs more than the side chain gains - AC-dist 500k (62 rounds)
+            # 1.043-1.048 ms/step without it, 1.058-1.060 with it (profiles/r6ao_ac_dist_rounds.txt)
+            rounds += int(os.environ.get("TDQ_FS_SPLIT_ROUNDS", "1" if rounds <= 16 else "0"))
         # the fewest workgroups with the same tiles per workgroup (AC-SA 50k, bf16: 1592 tiles,
         # 228 x 7; bf16x3: 3183 tiles, 245 x 13)
         self.G = -(-ntiles // rounds)
