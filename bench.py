@@ -474,7 +474,8 @@ def main(argv=None):
         divs = [k for k in range(16, 3, -1) if args.steps % k == 0]
         os.environ["TDQ_STEP_UNROLL"] = str(8 if args.steps % 8 == 0 else (divs[0] if divs else 8))
     layers = tuple(int(v) for v in (args.layers or spec["layers"]).split(","))
-    model = spec["build"](n_glob, world, args.backend, device, dist, args.precision, layers=layers)
+    model = spec["build"](n_glob, world, args.backend, device, dist, args.precision, layers=layers,
+                          newton_precision=args.newton_precision)
     eng = get_engine(model, args.warmup + args.steps + 2)
     backend = backend_of(model)
     elapsed, n_warm, warm_s = time_steps(eng, ctx, device, args.steps, args.warmup, args.min_warmup_s)
