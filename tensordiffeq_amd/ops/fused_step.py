@@ -42,10 +42,17 @@ _HEADERS = ("common.h", "jet_common.h", "jet_bf3.h", "jet_fused.h", "jet_fused3.
 RTC_OPTS = "-O3 -std=c++17 -fno-slp-vectorize -munsafe-fp-atomics"
 
 
-def _opts():
+# the bf16x3 objective's kernel under LLVM's max-ILP machine scheduler: 273.3-274.8 vs 277.3-278.2 us
+# per evaluation, L-BFGS 0.3190 vs 0.3220 ms per iteration; the bf16 step is faster on the default
+# scheduler (0.1378 vs 0.1421 ms) - profiles/r6ba_sched_strategy_ab.txt
+RTC_OPTS_LO = " -mllvm -amdgpu-sched-strategy=max-ilp"
+
+
+def _opts(src=""):
     """hipRTC options; ``TDQ_FUSED_STEP_TIMING=1`` adds the phase stamps (tools/fused_step_timing.py)."""
     extra = os.environ.get("TDQ_FUSED_STEP_DEFINES", "")   # A/B builds, e.g. "-DTDQ_PK_TANH=0"
-    return RTC_OPTS + (" -DTDQ_PHASE_TIMING" if os.environ.get("TDQ_FUSED_STEP_TIMING") == "1" else "") + \
+    return RTC_OPTS + (RTC_OPTS_LO if "fz3_body<" in src else "") + \
+        (" -DTDQ_PHASE_TIMING" if os.environ.get("TDQ_FUSED_STEP_TIMING") == "1" else "") + \
         (" " + extra if extra else "")
 
 
@@ -235,7 +242,7 @@ _PENDING = {}   # source key -> (thread, [code bytes | exception])
 
 
 def _key(src):
-    return hashlib.sha256((loss_jit.device_arch() + _opts() + src).encode()).hexdigest()
+    return hashlib.sha256((loss_jit.device_arch() + _opts(src) + src).encode()).hexdigest()
 
 
 def _rtc_compile(src):
@@ -244,7 +251,7 @@ def _rtc_compile(src):
     code, size = ctypes.c_void_p(0), ctypes.c_longlong(0)
     log = ctypes.create_string_buffer(16384)
     rc = lib.tdq_rtc_compile_ex(src.encode(), b"tdq_fused_step.hip", loss_jit.device_arch().encode(),
-                                _opts().encode(), ctypes.byref(code), ctypes.byref(size), log, len(log))
+                                _opts(src).encode(), ctypes.byref(code), ctypes.byref(size), log, len(log))
     if rc != 0:
         raise RuntimeError(f"hipRTC compile failed ({rc}): {log.value.decode(errors='replace')[:2000]}")
     try:
