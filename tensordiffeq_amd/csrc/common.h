@@ -52,9 +52,19 @@ __device__ __forceinline__ float row16_sum4(f32x4 v) {
 
 // sum over the 4 lanes l, l^16, l^32, l^48 (same point, different feature groups)
 __device__ __forceinline__ float col4_sum(float v) {
+#ifdef TDQ_COL4_BPERMUTE
   v += __shfl_xor(v, 16, 64);
   v += __shfl_xor(v, 32, 64);
   return v;
+#else
+  // the same two butterfly steps on the CDNA4 row-swap instructions (VALU, not the LDS crossbar of
+  // ds_bpermute): v_permlane16_swap pairs 16-lane rows 0-1 and 2-3, v_permlane32_swap the halves
+  const int lane = __lane_id();
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v += __uint_as_float((lane & 16) ? a[0] : a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return v + __uint_as_float((lane & 32) ? b[0] : b[1]);
+#endif
 }
 
 #define TDQ_CHECK_LAUNCH() \

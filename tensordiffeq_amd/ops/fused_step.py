@@ -45,7 +45,9 @@ RTC_OPTS = "-O3 -std=c++17 -fno-slp-vectorize -munsafe-fp-atomics"
 # the bf16x3 objective's kernel under LLVM's max-ILP machine scheduler: 273.3-274.8 vs 277.3-278.2 us
 # per evaluation, L-BFGS 0.3190 vs 0.3220 ms per iteration; the bf16 step is faster on the default
 # scheduler (0.1378 vs 0.1421 ms) - profiles/r6ba_sched_strategy_ab.txt
-RTC_OPTS_LO = " -mllvm -amdgpu-sched-strategy=max-ilp"
+# (and col4_sum on ds_bpermute there: the v_permlane swap form is 0.4 % faster in the bf16 step but
+# 0.8 % slower in this kernel, profiles/r6be_col4_permlane_ab.txt)
+RTC_OPTS_LO = " -mllvm -amdgpu-sched-strategy=max-ilp -DTDQ_COL4_BPERMUTE"
 
 
 def _opts(src=""):
