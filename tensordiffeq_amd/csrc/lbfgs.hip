@@ -26,6 +26,8 @@
 // All scalar state is fp64 in one small device array (layout LB_* below, mirrored by
 // tensordiffeq_amd/optimizers/lbfgs_device.py).  Once a stopping test fires every kernel is a
 // no-op, so graph replays past convergence change nothing.
+#include <cstdlib>
+
 #include "common.h"
 #include "jet_bf3.h"
 
@@ -51,6 +53,8 @@ enum {
   LB_G1,          // |g|_1 at the current x
   LB_REASON,      // why the run stopped (0 = running)
   LB_GTD,         // g.d of the current direction
+  LB_TS0 = 18,    // 18..23: phase stamps (LbCfg::ts): kernel start (block 0), then sums of
+                  // [start, logic entry), step 1, steps 2-3, step 4-5, and the count
   LB_NST = 24
 };
 
@@ -69,6 +73,8 @@ struct LbCfg {
   double tol_x;
   int legacy_stop;  // 1: the reference's effective function-change test |f| < tolX (tf.abs(f, f_old),
                     //    optimizers.py:273 - the second argument is the op name); 0: |f - f_old| < tolX
+  int ts;           // TDQ_LBFGS_TS=1 (fused path): phase stamps of the dots + logic kernel summed into
+                    //    st[LB_TS0 ..] (tools/prof_lbfgs.py --ts)
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -107,14 +113,26 @@ __device__ __forceinline__ void part_st(double* p, double v) {
     *p = v;
 }
 
-__device__ __forceinline__ bool slot_valid(int i, int head, int k, int m) { return ((i - head + m) % m) < k; }
-
-// lane `q` (wave-uniform) of a double, through two v_readlane_b32
-__device__ __forceinline__ double readlane_d(double v, int q) {
-  const unsigned long long b = __double_as_longlong(v);
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, q), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), q);
-  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+// "Am I the last block?" for the fused kernels' hand-off, as a two-level tree of arrival counters:
+// block b adds on counter b % LB_TG (one 128-B line each), the block completing a group adds on the
+// top counter, and the block completing the top runs the tail; every completed counter is re-armed
+// by the block that completed it.  One counter for the whole grid serialises every block's atomic
+// at one address: 7.7 us at 663 blocks, 9.0 us at 783, against ~1.3 us for this tree with 32
+// groups (tools/microbench/ticket_cost.hip, profiles/r6bg_ticket_cost.txt).  Thread 0 only, after
+// its partial stores have drained; the counters: LB_TCNT ints.
+#define LB_TG 32
+#define LB_TCNT (32 * (LB_TG + 1))
+__device__ __forceinline__ bool last_block(int* cnt, int b, int n) {
+  const int g = b % LB_TG, ng = n < LB_TG ? n : LB_TG;
+  const int gs = n / LB_TG + (g < n % LB_TG ? 1 : 0);
+  if (__hip_atomic_fetch_add(&cnt[32 * g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gs - 1) return false;
+  __hip_atomic_store(&cnt[32 * g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__hip_atomic_fetch_add(&cnt[32 * LB_TG], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ng - 1) return false;
+  __hip_atomic_store(&cnt[32 * LB_TG], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
+
+__device__ __forceinline__ bool slot_valid(int i, int head, int k, int m) { return ((i - head + m) % m) < k; }
 
 // d_j = cG g_j + sum_q (cS_q s_qj + cY_q y_qj) over the k history pairs (chronological q): the
 // four waves of a direction block share one 64-element tile, wave w sums the pairs of quarter w
@@ -254,8 +272,21 @@ __global__ void __launch_bounds__(256) lbfgs_dots_kernel(const float* __restrict
 // into LDS while it reduces the dot partials (every load of a thread issued before the first
 // store), patches the pushed slot's row and column in both copies, and solves from LDS.
 //
-// dynamic LDS (doubles): dots[(m+1)*5] | SYl[m*m] | YYl[m*m]
-__host__ __device__ inline size_t lbfgs_logic_lds(int m) { return ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m) * 8; }
+// R^{-1} (R = the upper triangle of S^T Y in chronological order, as below) is kept current by one
+// new column per push: dropping the oldest pair leaves the inverse of the remaining block as the
+// lower-right block of the old inverse, and bordering R with the new column c (c_i = s_i.y_new)
+// and diagonal d = s_new.y_new gives the new column -R^{-1} c / d and the diagonal 1 / d.  The two
+// triangular solves of the compact product become matrix-vector products, whose steps do not
+// depend on each other (a substitution step waits on the previous one: 7.5 us of the update at
+// k = 50 on one wave, profiles/r6bk_lbfgs_solve_stamps.txt).  R^{-1} shares the YY buffer with
+// Y^T Y: for physical slots a, b with a older than b, Y^T Y's entry sits at [a][b] and R^{-1}'s at
+// [b][a]; the diagonal is Y^T Y's (R^{-1}'s is 1 / R[a][a]).  So the LDS image stays at two
+// matrices (a third one cost the fused dots part its occupancy, profiles/r6bp_lbfgs_rinv_packed.txt).
+//
+// dynamic LDS (doubles): dots[(m+1)*5] | SYl[m*m] | YRl[m*m] | vecl[64] | red[256]
+__host__ __device__ inline size_t lbfgs_logic_lds(int m) {
+  return ((size_t)(m + 1) * LB_NF + 2 * (size_t)m * m + 64 + 256) * 8;
+}
 
 template <bool SC1>
 __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, const double* __restrict__ part,
@@ -265,8 +296,17 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   const int tid = threadIdx.x, m = c.m, mm = m * m;
   double* dots = lb_lds;
   double* SYl = dots + (m + 1) * LB_NF;
-  double* YYl = SYl + mm;
-  // 1. copy S^T Y / Y^T Y into LDS and reduce the chunk partials (fixed order: deterministic)
+  double* YYl = SYl + mm;  // Y^T Y and R^{-1} (lbfgs_logic_lds)
+  double* vecl = YYl + mm;
+  double* red = vecl + 64;
+  const unsigned long long ts1 = c.ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // the scalar state, loaded first: its latency overlaps step 1's
+  const double f = (double)fg[c.p];
+  int n_iter = (int)st[LB_NITER];
+  const double fe0 = st[LB_FEVAL], dt1 = st[LB_DT1], fold = st[LB_FOLD], hd_old = st[LB_HDIAG];
+  double minloss = st[LB_MINLOSS];
+  int k = (int)st[LB_K], head = (int)st[LB_HEAD];
+  // 1. copy S^T Y / Y^T Y + R^{-1} into LDS and reduce the chunk partials (fixed order: deterministic)
   {
     constexpr int NE = (LB_MAXM * LB_MAXM + 255) / 256;
     double sv[NE], yv[NE];
@@ -278,33 +318,19 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
     }
     for (int v = tid; v < (m + 1) * LB_NF; v += 256) {
       double a0 = 0.0, a1 = 0.0;
-      int ch = 0;
-      for (; ch + 15 < c.nchunks; ch += 16) {  // sixteen loads in flight
+      // sixteen loads in flight per round (one round up to 16 chunks); even chunks into a0, odd
+      // into a1, each in increasing order (the summation order of every earlier version)
+      for (int ch = 0; ch < c.nchunks; ch += 16) {
         double q[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) q[u] = part_ld<SC1>(&part[(size_t)(ch + u) * (m + 1) * LB_NF + v]);
+        for (int u = 0; u < 16; ++u)
+          q[u] = part_ld<SC1>(&part[(size_t)min(ch + u, c.nchunks - 1) * (m + 1) * LB_NF + v]);
 #pragma unroll
         for (int u = 0; u < 16; u += 2) {
-          a0 += q[u];
-          a1 += q[u + 1];
+          if (ch + u < c.nchunks) a0 += q[u];
+          if (ch + u + 1 < c.nchunks) a1 += q[u + 1];
         }
       }
-      if (ch + 7 < c.nchunks) {
-        double q[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) q[u] = part_ld<SC1>(&part[(size_t)(ch + u) * (m + 1) * LB_NF + v]);
-#pragma unroll
-        for (int u = 0; u < 8; u += 2) {
-          a0 += q[u];
-          a1 += q[u + 1];
-        }
-        ch += 8;
-      }
-      for (; ch + 1 < c.nchunks; ch += 2) {
-        a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
-        a1 += part_ld<SC1>(&part[(size_t)(ch + 1) * (m + 1) * LB_NF + v]);
-      }
-      if (ch < c.nchunks) a0 += part_ld<SC1>(&part[(size_t)ch * (m + 1) * LB_NF + v]);
       dots[v] = a0 + a1;
     }
 #pragma unroll
@@ -317,21 +343,16 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
     }
   }
   __syncthreads();
-  // everything below runs on wave 0: the scalar logic is evaluated by every lane (uniform values,
-  // lane 0 stores), the pair coefficients with one lane per history pair - no further barriers
-  // (LDS accesses of one wave complete in program order; the wavefront fences below only keep
-  // the compiler from reordering them)
-  if (tid >= 64) return;
-  const int lane = tid;
-  const bool L0 = lane == 0;
+  // the scalar logic below is evaluated by every thread (uniform values, thread 0 stores, every
+  // early return uniform); per-pair values with one lane of each wave per history pair (lane j =
+  // chronological pair j), wave 0 storing them; the matrix-vector products split their sums over
+  // the four waves
+  const unsigned long long ts2 = c.ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const int lane = tid & 63, w = tid >> 6;
+  const bool L0 = tid == 0, W0 = w == 0;
   // 2. post-evaluation tests of the previous step (reference optimizers.py:241-296, with the
   //    B9 fixes of eager_lbfgs), then the curvature test and ring push (optimizers.py:168-185)
   const double* sc = dots + m * LB_NF;  // s.y, y.y, s.g, y.g, |g|_1
-  const double f = (double)fg[c.p];
-  int n_iter = (int)st[LB_NITER];
-  const double fe0 = st[LB_FEVAL], dt1 = st[LB_DT1], fold = st[LB_FOLD], hd_old = st[LB_HDIAG];
-  double minloss = st[LB_MINLOSS];
-  int k = (int)st[LB_K], head = (int)st[LB_HEAD];
   int best = 0, done = 0, reason = LB_R_RUN;
   if (L0) st[LB_G1] = sc[4];
   if (n_iter == 0) {
@@ -406,75 +427,99 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   }
   const double gam = n_iter == 1 ? 1.0 : hd;
   // 3. the pushed slot's row / column of S^T Y and Y^T Y, in memory (later iterations) and LDS
-  if (pushed && lane < m && slot_valid(lane, head, k, m)) {
+  if (W0 && pushed && lane < m && slot_valid(lane, head, k, m)) {
     const int j = lane;
     const double* dj = dots + j * LB_NF;
     const double snj = j == slot ? ys : dj[4], sjn = j == slot ? ys : dj[2], yj = j == slot ? yy : dj[3];
     SY[slot * m + j] = snj;  // s_new . y_j
     SY[j * m + slot] = sjn;  // s_j . y_new
-    YY[j * m + slot] = yj;
-    YY[slot * m + j] = yj;
+    YY[j * m + slot] = yj;  // j older than the new pair ([slot][j] holds R^{-1}[j][new], step 4)
     SYl[slot * m + j] = snj;
     SYl[j * m + slot] = sjn;
     YYl[j * m + slot] = yj;
-    YYl[slot * m + j] = yj;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (n_iter == 1 || k == 0) {  // d = -H0 g (first iteration: H0 = I)
-    for (int v = lane; v < 2 * m; v += 64) coef[v] = 0.0;
+    if (W0)
+      for (int v = lane; v < 2 * m; v += 64) coef[v] = 0.0;
     if (L0) coef[2 * m] = -gam;
     return;
   }
+  __syncthreads();  // the patched rows / columns
+  const unsigned long long ts3 = c.ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // 4. compact product (lane j = chronological pair j, physical slot ij):
   //    R u = S^T g ; rhs = D u + gam Y^T Y u - gam Y^T g ; R^T p1 = rhs ;
   //    H g = gam g + S p1 - gam Y u   ->   d = -H g
-  //    R = upper triangle of S^T Y in chronological order.  Each substitution step broadcasts its
-  //    pivot with v_readlane (uniform q) and multiplies by the pivot's reciprocal, computed for
-  //    every lane up front; the LDS operands of a step do not depend on the chain, so the
-  //    8-step unrolled groups keep them ahead of it.
+  //    R = upper triangle of S^T Y in chronological order, R^{-1} kept current (RIl, see
+  //    lbfgs_logic_lds): u = R^{-1} S^T g and p1 = R^{-T} rhs are matrix-vector products.
   const int j = lane;
   const bool jv = j < k;
   int ij = head + j;
   if (ij >= m) ij -= m;
   ij = jv ? ij : 0;
   const double rjj = SYl[ij * m + ij];
-  const double rdj = jv ? 1.0 / rjj : 0.0;
   const bool nwj = pushed && ij == slot;
-  double r = jv ? (nwj ? dots[m * LB_NF + 2] : dots[ij * LB_NF + 0]) : 0.0;  // s_j . g
-  double u = 0.0;
-  // back substitution: q = k-1 .. 0 ; R[j][q] = SYl[ij][iq]
-  int iq = head + k - 1;
-  if (iq >= m) iq -= m;
-#pragma unroll 8
-  for (int q = k - 1; q >= 0; --q) {
-    const double rq = SYl[ij * m + iq];
-    const double uq = readlane_d(r, q) * readlane_d(rdj, q);
-    if (j == q) u = uq;
-    if (j < q) r -= rq * uq;
-    iq = iq == 0 ? m - 1 : iq - 1;
+  const double rdj = jv ? 1.0 / rjj : 0.0;  // R^{-1}[j][j]
+  // sum over q in [qa, qb) of A(j, q) * vec[q], vec[q] = `val` of lane q; A by the pairs' order:
+  //   sel 0: R^{-1}[j][q], q >= j   (at [iq][ij], q > j)
+  //   sel 1: R^{-1}[q][j], q <= j   (at [ij][iq], q < j)
+  //   sel 2: Y^T Y[j][q]            (at [iq][ij] for q < j, [ij][iq] for q > j, the diagonal)
+  // Wave w sums its quarter of [0, k) - operands of four pairs loaded ahead of their products,
+  // the vector read as an LDS broadcast - and every wave adds the four partials in fixed order.
+  auto mv = [&](int sel, double val, int qa, int qb) {
+    if (W0) vecl[lane] = val;
+    __syncthreads();
+    const int q0 = (w * k) >> 2, q1 = ((w + 1) * k) >> 2;
+    int iq = head + q0;
+    if (iq >= m) iq -= m;
+    double a0 = 0.0, a1 = 0.0;
+    for (int q = q0; q < q1; q += 4) {
+      double av[4], bv[4];
+      int ip = iq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int qq = q + t < q1 ? q + t : q, pq = q + t < q1 ? ip : iq;
+        const bool below = sel == 0 || (sel == 2 && qq < j);  // [iq][ij] rather than [ij][iq]
+        av[t] = YYl[below ? pq * m + ij : ij * m + pq];
+        bv[t] = vecl[qq];
+        ip = ip + 1 == m ? 0 : ip + 1;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int qq = q + t;
+        const double a = (sel != 2 && qq == j) ? rdj : av[t];
+        const double v = (qq < q1 && qq >= qa && qq < qb) ? a * bv[t] : 0.0;
+        if (t & 1) a1 += v;
+        else a0 += v;
+      }
+      iq = ip;
+    }
+    red[tid] = a0 + a1;
+    __syncthreads();
+    const double r = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+    __syncthreads();  // red and vecl are rewritten by the next product
+    return r;
+  };
+  if (pushed) {  // the new pair's column of R^{-1} (chronological k-1; c_q = SYl[q][slot] = s_q.y_new)
+    const double cq = (jv && j < k - 1) ? SYl[ij * m + slot] : 0.0;
+    const double v = mv(0, cq, j, k - 1);
+    if (W0 && j < k - 1) {  // R^{-1}[j][new] at [slot][ij]; the diagonal 1 / ys is 1 / rjj
+      const double ri = -v / ys;
+      YYl[slot * m + ij] = ri;
+      YY[slot * m + ij] = ri;
+    }
+    __syncthreads();
   }
+  const double r0 = jv ? (nwj ? dots[m * LB_NF + 2] : dots[ij * LB_NF + 0]) : 0.0;  // s_j . g
+  // u = R^{-1} r0: u_j = sum_{q >= j} RI[j][q] r0_q
+  const double u = mv(0, r0, j, k);
   // rhs = R[j][j] u_j + gam (Y^T Y u)_j - gam y_j.g
-  double yu = 0.0;
-  iq = head;
-#pragma unroll 8
-  for (int q = 0; q < k; ++q) {
-    yu += YYl[iq * m + ij] * readlane_d(u, q);
-    iq = iq + 1 == m ? 0 : iq + 1;
-  }
+  const double yu = mv(2, jv ? u : 0.0, 0, k);
   const double bj = jv ? (nwj ? dots[m * LB_NF + 3] : dots[ij * LB_NF + 1]) : 0.0;  // y_j . g
-  double rr = jv ? rjj * u + gam * yu - gam * bj : 0.0;
-  // forward substitution with R^T: R[q][j] = SYl[iq][ij]
-  double p1 = 0.0;
-  iq = head;
-#pragma unroll 8
-  for (int q = 0; q < k; ++q) {
-    const double cq = SYl[iq * m + ij];
-    const double pq = readlane_d(rr, q) * readlane_d(rdj, q);
-    if (j == q) p1 = pq;
-    if (j > q && jv) rr -= cq * pq;
-    iq = iq + 1 == m ? 0 : iq + 1;
-  }
+  const double rr = jv ? rjj * u + gam * yu - gam * bj : 0.0;
+  // p1 = R^{-T} rr: p1_j = sum_{q <= j} RI[q][j] rr_q
+  const double p1 = mv(1, rr, 0, j + 1);
   // 5. per PHYSICAL slot
+  if (!W0) return;
   if (jv) {
     coef[ij] = -p1;
     coef[m + ij] = gam * u;
@@ -482,6 +527,16 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   for (int v = lane; v < m; v += 64)
     if (((v - head + m) % m) >= k) coef[v] = coef[m + v] = 0.0;
   if (L0) coef[2 * m] = -gam;
+  if (SC1 && c.ts && L0) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const unsigned long long ts4 = __builtin_amdgcn_s_memrealtime();
+    const double t0 = __hip_atomic_load(&st[LB_TS0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st[LB_TS0 + 1] += (double)ts1 - t0;
+    st[LB_TS0 + 2] += (double)(ts2 - ts1);
+    st[LB_TS0 + 3] += (double)(ts3 - ts2);
+    st[LB_TS0 + 4] += (double)(ts4 - ts3);
+    st[LB_TS0 + 5] += 1.0;
+  }
 }
 
 __global__ void __launch_bounds__(256) lbfgs_logic_kernel(const float* __restrict__ fg, const double* __restrict__ part,
@@ -585,13 +640,13 @@ __global__ void __launch_bounds__(256) lbfgs_axpy_kernel(float* __restrict__ x, 
 // ---------------------------------------------------------------------------------------------
 // Fused update: TWO launches per iteration instead of dots -> logic -> dir -> step -> axpy.
 //   lbfgs_dots_logic  the dots grid; every block stores its partials write-through (sc1), waits
-//                     for them, and draws a ticket (agent-scope atomic add); the block that draws
-//                     the last ticket runs the logic on the partials (sc1 loads) and re-arms the
-//                     ticket.  (Hand-off protocol: MI355X_MICROARCH.md, inter-workgroup table row 1.)
+//                     for them, and arrives on the counter tree (last_block); the block that
+//                     arrives last runs the logic on the partials (sc1 loads).  (Hand-off protocol:
+//                     MI355X_MICROARCH.md, inter-workgroup table row 1.)
 //   lbfgs_dir_step    the direction pass, plus the step taken speculatively: t of the NEXT step
 //                     is known before g.d is (min(1, 1/|g|_1) on the first iteration, else the
 //                     fixed lr), so every element does x += t d right after computing d (old x
-//                     kept in x_prev); the last-ticket block reduces g.d / |d|_1 and runs the
+//                     kept in x_prev); the last-arriving block reduces g.d / |d|_1 and runs the
 //                     descent test - in the rare stop case it restores x from x_prev, so the
 //                     trajectory is bit-identical to the five-launch path.  With a weight-image
 //                     target (the split-bf16 objective's scratch) every new x element is also
@@ -613,16 +668,16 @@ __global__ void __launch_bounds__(256) lbfgs_dots_logic_kernel(const float* __re
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st[LB_BEST] = 0.0;
     return;
   }
+  if (c.ts && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    __hip_atomic_store(&st[LB_TS0], (double)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   lbfgs_dots_body<true>(fg, g_old, d, S, Y, st, part, c, red);
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's sc1 partial stores have landed
-    const int nb = (int)(gridDim.x * gridDim.y);
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == nb - 1;
+    last = last_block(ticket, (int)(blockIdx.y * gridDim.x + blockIdx.x), (int)(gridDim.x * gridDim.y));
   }
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   lbfgs_logic_body<true>(fg, part, st, SY, YY, coef, fhist, c, lb_lds);
 }
 
@@ -689,8 +744,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
     part_st<true>(&part2[2 * blockIdx.x], acc[0]);
     part_st<true>(&part2[2 * blockIdx.x + 1], acc[1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == (int)gridDim.x - 1;
+    last = last_block(ticket, (int)blockIdx.x, (int)gridDim.x);
   }
   __syncthreads();
   if (!last) return;
@@ -702,7 +756,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
   __syncthreads();  // red is reused
   block_sum<2>(a2, red);
   if (threadIdx.x == 0) {
-    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const double gtd = a2[0];
     st[LB_GTD] = gtd;
     stop = gtd > -c.tol_x;
@@ -731,16 +784,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
 extern "C" {
 
 int tdq_lbfgs_nst() { return LB_NST; }
+int tdq_lbfgs_ticket_ints() { return LB_TCNT; }
 
 // After an evaluation at x (fg = [g | f]): dots -> logic -> dir -> step.
-//   part: nchunks * (m + 1) * 5 doubles, part2: 2 * nblk doubles, SY / YY: m * m doubles,
+//   part: nchunks * (m + 1) * 5 doubles, part2: 2 * nblk doubles, SY / YY: m * m doubles (YY holds
+//   Y^T Y and R^{-1}, lbfgs_logic_lds),
 //   coef: 2 m + 1 doubles, S / Y: m * p floats, fhist: fhist_len floats (or null).
 int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
                      double* st, double* SY, double* YY, double* coef, double* part, double* part2, float* fhist,
                      int p, int m, int max_iter, int nchunks, int nblk, int fhist_len, double max_eval, double lr,
                      double tol_fun, double tol_x, int legacy_stop, void* stream) {
   if (p <= 0 || m < 1 || m > LB_MAXM || nchunks < 1 || nblk < 1) return (int)hipErrorInvalidValue;
-  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
+  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop, 0};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t lds = lbfgs_logic_lds(m);
   static bool attr = false;
@@ -763,7 +818,8 @@ int tdq_lbfgs_update(const float* x, const float* fg, float* g_old, float* d, fl
 }
 
 // The same update in two launches (lbfgs_dots_logic + lbfgs_dir_step, see above); it also takes
-// the step (no tdq_lbfgs_axpy).  ticket: 2 ints, zero on the first call (re-armed by the kernels);
+// the step (no tdq_lbfgs_axpy).  ticket: 2 tdq_lbfgs_ticket_ints() ints, zero on the first call
+// (re-armed by the kernels);
 // x_prev: p floats; img (nullable): a TailImg (tdq_img_target) whose images the step also writes.
 int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, float* S, float* Y, float* best_x,
                            float* x_prev, double* st, double* SY, double* YY, double* coef, double* part, double* part2,
@@ -776,7 +832,11 @@ int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, fl
     ti = *reinterpret_cast<const TailImg*>(img);
     if (param_count(ti.d) != p) return (int)hipErrorInvalidValue;  // images of another network
   }
-  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop};
+  LbCfg c{p, m, max_iter, nchunks, nblk, fhist_len, max_eval, lr, tol_fun, tol_x, legacy_stop, 0};
+  {
+    const char* e = getenv("TDQ_LBFGS_TS");
+    c.ts = e != nullptr && e[0] == '1';
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t lds = lbfgs_logic_lds(m);
   static bool attr = false;
@@ -790,7 +850,7 @@ int tdq_lbfgs_update_fused(float* x, const float* fg, float* g_old, float* d, fl
                      YY, coef, fhist, ticket, c);
   TDQ_CHECK_LAUNCH();
   hipLaunchKernelGGL(lbfgs_dir_step_kernel, dim3(nblk), dim3(256), 0, s, x, fg, g_old, d, S, Y, best_x, x_prev, st,
-                     coef, part2, ticket + 1, c, ti);
+                     coef, part2, ticket + LB_TCNT, c, ti);
   TDQ_CHECK_LAUNCH();
   return 0;
 }

@@ -81,6 +81,7 @@ def _declare(lib):
         "tdq_loss_meta_sizes": (I, [P]),
         "tdq_loss_reduce_partials": (I, [P, I, I, I, P, P, P, I, P]),
         "tdq_lbfgs_nst": (I, []),
+        "tdq_lbfgs_ticket_ints": (I, []),
         "tdq_lbfgs_update": (I, [P] * 14 + [I] * 6 + [D] * 4 + [I, P]),
         "tdq_lbfgs_axpy": (I, [P, P, P, I, I, P]),
         "tdq_lbfgs_update_fused": (I, [P] * 16 + [I] * 6 + [D] * 4 + [I, P, P]),

@@ -10,7 +10,7 @@ on the GPU and one iteration is a fixed sequence of kernel launches (``csrc/lbfg
 
 so the whole iteration is captured once as a HIP graph and replayed.  By default the update is TWO
 launches (``tdq_lbfgs_update_fused``: dots + logic, then direction + descent test + the step
-itself, each finished by the block that draws the last ticket) instead of five (dots, logic,
+itself, each finished by the block that arrives last on a counter tree) instead of five (dots, logic,
 direction, step, axpy); ``TDQ_LBFGS_FUSED=0`` keeps the five-launch path - both give the same
 trajectory bit for bit (GPU test).  The host reads one flag
 every ``poll_every`` iterations instead of ~6 scalars per iteration (reference host syncs at
@@ -90,7 +90,7 @@ class DeviceLBFGS:
         self.best_x = x.detach().clone()
         self.st = torch.zeros(NST, **f64)
         self.SY = torch.zeros(self.m, self.m, **f64)
-        self.YY = torch.zeros(self.m, self.m, **f64)
+        self.YY = torch.zeros(self.m, self.m, **f64)  # Y^T Y and R^{-1} (lbfgs.hip lbfgs_logic_lds)
         self.coef = torch.zeros(2 * self.m + 1, **f64)
         self.nchunks = max(1, min(64, _ceil(p, 4096)))
         self.nblk = max(1, min(2048, _ceil(p, 64)))  # direction blocks: 64 elements x 4 history quarters
@@ -98,7 +98,9 @@ class DeviceLBFGS:
         self.part2 = torch.zeros(2 * self.nblk, **f64)
         self.fhist = torch.full((self.max_iter + 1,), float("nan"), **f32) if record_history else None
         self.x_prev = torch.empty(p, **f32) if self.fused else None
-        self.ticket = torch.zeros(2, dtype=torch.int32, device=dev) if self.fused else None
+        # two arrival-counter trees (lbfgs.hip last_block), zero at the start, re-armed by the kernels
+        self.ticket = (torch.zeros(2 * _lib.load().tdq_lbfgs_ticket_ints(), dtype=torch.int32, device=dev)
+                       if self.fused else None)
         # the objective's weight-image target (jet_hip.img_target): the fused update writes the new
         # x's images too, so the objective skips its pack launch
         self.img_target = img_target if self.fused else None

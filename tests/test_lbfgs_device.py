@@ -262,16 +262,17 @@ def test_solver_device_lbfgs_on_hip_path(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("use_graph", [False, True])
-def test_fused_update_matches_five_launch_path(use_graph, monkeypatch):
+@pytest.mark.parametrize("use_graph,p", [(False, 3000), (True, 3000), (True, 60000)])
+def test_fused_update_matches_five_launch_path(use_graph, p, monkeypatch):
     """The two-launch update (dots + logic, direction + descent test + step, each finished by the
-    last-ticket block) reproduces the five-launch path bit for bit: iterate, loss history, best
-    iterate, stop reason - incl. the history-ring wrap-around."""
-    fg = _quadratic(p=3000, q=4000, seed=4, device="cuda")
+    block arriving last on its counter tree) reproduces the five-launch path bit for bit: iterate,
+    loss history, best iterate, stop reason - incl. the history-ring wrap-around.  p = 60000:
+    195 dots blocks and 938 direction blocks, every group of the 32-way tree several deep."""
+    fg = _quadratic(p=p, q=4000 if p <= 3000 else 300, seed=4, device="cuda")
     outs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("TDQ_LBFGS_FUSED", fused)
-        x = torch.zeros(3000, device="cuda")
+        x = torch.zeros(p, device="cuda")
         opt = LD.minimize(_evaluator(fg, x), x, 80, m=12, use_graph=use_graph, poll_every=9)
         torch.cuda.synchronize()
         assert opt.fused == (fused == "1")

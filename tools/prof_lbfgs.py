@@ -15,7 +15,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=500)
     ap.add_argument("--npts", type=int, default=50000)
+    ap.add_argument("--ts", action="store_true",
+                    help="phase stamps of the dots + logic kernel (TDQ_LBFGS_TS=1, lbfgs.hip LB_TS0)")
     a = ap.parse_args()
+    if a.ts:
+        os.environ["TDQ_LBFGS_TS"] = "1"
     import torch
     import bench
     m = bench.build_problem(a.npts, 1, "hip", torch.device("cuda", 0), False, "bf16", newton_precision="bf16x3")
@@ -27,6 +31,12 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     info = m.fit_info["lbfgs"]
+    if a.ts:   # 100 MHz real-time counter ticks summed over the iterations that ran the full logic
+        st = m.lbfgs_state.st.cpu().tolist()
+        n = max(1.0, st[23])
+        print(json.dumps({"ts_iters": st[23], "us_dots_until_logic": st[19] / n / 100,
+                          "us_step1_loads": st[20] / n / 100, "us_step2_3_tests": st[21] / n / 100,
+                          "us_step4_5_solves": st[22] / n / 100}))
     print(json.dumps({"iters": info["n_iter"], "reason": info["reason"], "wall_s": dt,
                       "ms_per_iter": 1e3 * dt / max(1, info["n_iter"]),
                       "fused_update": os.environ.get("TDQ_LBFGS_FUSED", "1")}))
