@@ -139,7 +139,7 @@ __device__ __forceinline__ bool slot_valid(int i, int head, int k, int m) { retu
 // (at most LB_MAXM / 4, every load of it in flight together), and wave 0 adds the quarters in
 // fixed order.  Shared by both update paths (same summation order, so the same bits).
 __device__ __forceinline__ double dir_quarter(const float* __restrict__ S, const float* __restrict__ Y,
-                                              const double* __restrict__ coef, int j, int p, int k, int head, int m,
+                                              const double* coef, int j, int p, int k, int head, int m,
                                               int pushed, int slot, float tf, float g, float dj, float oj, int w) {
   const int q0 = (w * k) >> 2, q1 = ((w + 1) * k) >> 2;
   double acc[2] = {0.0, 0.0};
@@ -560,11 +560,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
                                                         LbCfg c) {
   __shared__ double red[8];
   __shared__ double qs[4][64];
+  // the pair coefficients staged in LDS: read as uniform scalar loads they were fetched one at a
+  // time (each result spilled before the next load could issue: ~11 us of a 15.5 us launch)
+  __shared__ double cf[2 * LB_MAXM + 1];
+  if ((int)threadIdx.x <= 2 * c.m) cf[threadIdx.x] = coef[threadIdx.x];
+  __syncthreads();
   const bool best = st[LB_BEST] != 0.0, active = st[LB_ACTIVE] != 0.0;
   const int n_iter = (int)st[LB_NITER], pushed = (int)st[LB_PUSHED], slot = (int)st[LB_SLOT];
   const int k = (int)st[LB_K], head = (int)st[LB_HEAD], m = c.m;
   const float tf = (float)st[LB_T];
-  const double cG = coef[2 * m];
+  const double cG = cf[2 * m];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // w: wave-uniform
   double acc[2] = {0.0, 0.0};
   for (int jb = blockIdx.x * 64; jb < c.p; jb += gridDim.x * 64) {
@@ -573,7 +578,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
     const int jc = in ? j : c.p - 1;  // unconditional loads: all in flight before the first use
     const float g = fg[jc], dj = d[jc], oj = g_old[jc], xj = x[jc];
     // branch-free (k = 0 before the first push: every pair masked; rows stay in range)
-    const double qv = dir_quarter(S, Y, coef, jc, c.p, k, head, m, pushed, slot, tf, g, dj, oj, w);
+    const double qv = dir_quarter(S, Y, cf, jc, c.p, k, head, m, pushed, slot, tf, g, dj, oj, w);
     qs[w][l] = (active && n_iter > 1) ? qv : 0.0;
     const float s = tf * dj, y = g - oj;
     __syncthreads();
@@ -690,6 +695,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
                                                              LbCfg c, TailImg ti) {
   __shared__ double red[8];
   __shared__ double qs[4][64];
+  // the pair coefficients staged in LDS: read as uniform scalar loads they were fetched one at a
+  // time (each result spilled before the next load could issue: ~11 us of a 15.5 us launch)
+  __shared__ double cf[2 * LB_MAXM + 1];
+  if ((int)threadIdx.x <= 2 * c.m) cf[threadIdx.x] = coef[threadIdx.x];
+  __syncthreads();
   __shared__ int last, stop;
   const bool best = st[LB_BEST] != 0.0, active = st[LB_ACTIVE] != 0.0;
   const int n_iter = (int)st[LB_NITER], pushed = (int)st[LB_PUSHED], slot = (int)st[LB_SLOT];
@@ -698,7 +708,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
   // the next step's length (the five-launch lbfgs_step_kernel's formula)
   const double tnext = (n_iter == 1) ? fmin(1.0, 1.0 / st[LB_G1]) : c.lr;
   const float tn = (float)tnext;
-  const double cG = coef[2 * m];
+  const double cG = cf[2 * m];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // w: wave-uniform
   double acc[2] = {0.0, 0.0};
   for (int jb = blockIdx.x * 64; jb < c.p; jb += gridDim.x * 64) {
@@ -707,7 +717,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
     const int jc = in ? j : c.p - 1;  // unconditional loads: all in flight before the first use
     const float g = fg[jc], dj = d[jc], oj = g_old[jc], xj = x[jc];
     // branch-free (k = 0 before the first push: every pair masked; rows stay in range)
-    const double qv = dir_quarter(S, Y, coef, jc, c.p, k, head, m, pushed, slot, tf, g, dj, oj, w);
+    const double qv = dir_quarter(S, Y, cf, jc, c.p, k, head, m, pushed, slot, tf, g, dj, oj, w);
     qs[w][l] = (active && n_iter > 1) ? qv : 0.0;
     const float s = tf * dj, y = g - oj;
     __syncthreads();
@@ -749,9 +759,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) l
   __syncthreads();
   if (!last) return;
   double a2[2] = {0.0, 0.0};
-  for (int b = threadIdx.x; b < c.nblk; b += 256) {
-    a2[0] += part_ld<true>(&part2[2 * b]);
-    a2[1] += part_ld<true>(&part2[2 * b + 1]);
+  // blocks b = tid, tid + 256, ... in increasing order; the coherent (atomic) loads of four of them
+  // issued together - one after the other they cost a memory latency each
+  for (int b0 = threadIdx.x; b0 < c.nblk; b0 += 1024) {
+    double v0[4], v1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int b = min(b0 + 256 * t, c.nblk - 1);
+      v0[t] = part_ld<true>(&part2[2 * b]);
+      v1[t] = part_ld<true>(&part2[2 * b + 1]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (b0 + 256 * t < c.nblk) {
+        a2[0] += v0[t];
+        a2[1] += v1[t];
+      }
   }
   __syncthreads();  // red is reused
   block_sum<2>(a2, red);
