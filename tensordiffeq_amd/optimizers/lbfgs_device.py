@@ -395,7 +395,15 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
         pending, b = None, 0
         launched = 1
 
+        hostprof = os.environ.get("TDQ_LBFGS_HOSTPROF", "0") == "1"   # host enqueue vs wait split
+        opt.host_times = {"enqueue_s": 0.0, "wait_s": 0.0, "batches": 0}
+
         def consume(i):
+            if hostprof:
+                import time
+                t = time.perf_counter()
+                evs[i].synchronize()
+                opt.host_times["wait_s"] += time.perf_counter() - t
             evs[i].synchronize()
             a, it, f = bufs[i].tolist()
             opt.polled = {"active": a != 0.0, "n_iter": int(it), "f": f}
@@ -409,11 +417,17 @@ def minimize(evaluate, x, max_iter, m=50, lr=0.8, tol_fun=1e-12, tol_x=1e-12, al
                 break
             n = max(1, min(poll_every, remaining))
             reps = (n + K - 1) // K
+            if hostprof:
+                import time
+                t_enq = time.perf_counter()
             for _ in range(reps):
                 ga.replay()
                 if gb is not None:
                     all_reduce(fg_static)
                     gb.replay()
+            if hostprof:
+                opt.host_times["enqueue_s"] += time.perf_counter() - t_enq
+                opt.host_times["batches"] += 1
             launched += reps * K
             expected += reps * K
             bufs[b].copy_(torch.index_select(opt.st, 0, sel), non_blocking=pin)

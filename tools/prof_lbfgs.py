@@ -31,6 +31,9 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     info = m.fit_info["lbfgs"]
+    ht = getattr(m.lbfgs_state, "host_times", None)
+    if ht and ht["batches"]:
+        print(json.dumps({"host_enqueue_s": ht["enqueue_s"], "host_wait_s": ht["wait_s"], "batches": ht["batches"]}))
     if a.ts:   # 100 MHz real-time counter ticks summed over the iterations that ran the full logic
         st = m.lbfgs_state.st.cpu().tolist()
         n = max(1.0, st[23])
