@@ -54,7 +54,8 @@ enum {
   LB_REASON,      // why the run stopped (0 = running)
   LB_GTD,         // g.d of the current direction
   LB_TS0 = 18,    // 18..23: phase stamps (LbCfg::ts): kernel start (block 0), then sums of
-                  // [start, logic entry), step 1, steps 2-3, step 4-5, and the count
+                  // the shader clock cycles over the logic, its step 1, steps 2-3, step 4-5 (100 MHz
+                  // ticks), and the count
   LB_NST = 24
 };
 
@@ -300,6 +301,7 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   double* vecl = YYl + mm;
   double* red = vecl + 64;
   const unsigned long long ts1 = c.ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long mt1 = c.ts ? __builtin_amdgcn_s_memtime() : 0ull;  // shader clock cycles
   // the scalar state, loaded first: its latency overlaps step 1's
   const double f = (double)fg[c.p];
   int n_iter = (int)st[LB_NITER];
@@ -530,8 +532,8 @@ __device__ __forceinline__ void lbfgs_logic_body(const float* __restrict__ fg, c
   if (SC1 && c.ts && L0) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const unsigned long long ts4 = __builtin_amdgcn_s_memrealtime();
-    const double t0 = __hip_atomic_load(&st[LB_TS0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st[LB_TS0 + 1] += (double)ts1 - t0;
+    const unsigned long long mt4 = __builtin_amdgcn_s_memtime();
+    st[LB_TS0 + 1] += (double)(mt4 - mt1);  // shader clock cycles over [ts1, ts4]
     st[LB_TS0 + 2] += (double)(ts2 - ts1);
     st[LB_TS0 + 3] += (double)(ts3 - ts2);
     st[LB_TS0 + 4] += (double)(ts4 - ts3);

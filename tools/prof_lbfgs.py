@@ -37,7 +37,8 @@ def main():
     if a.ts:   # 100 MHz real-time counter ticks summed over the iterations that ran the full logic
         st = m.lbfgs_state.st.cpu().tolist()
         n = max(1.0, st[23])
-        print(json.dumps({"ts_iters": st[23], "us_dots_until_logic": st[19] / n / 100,
+        ticks = st[20] + st[21] + st[22]
+        print(json.dumps({"ts_iters": st[23], "shader_clock_mhz": 100.0 * st[19] / max(ticks, 1.0),
                           "us_step1_loads": st[20] / n / 100, "us_step2_3_tests": st[21] / n / 100,
                           "us_step4_5_solves": st[22] / n / 100}))
     print(json.dumps({"iters": info["n_iter"], "reason": info["reason"], "wall_s": dt,
